@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 images/sec (+ BERT-base samples/sec), whole node.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
+is launched by ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).
+W untimed warm-up steps, then EXACTLY K optimizer steps timed between
+barrier + device synchronisation on both sides; the max over ranks is the step
+time.  Rank 0 prints ONE JSON line on stdout (everything else goes to stderr).
+
+Workload (BASELINE.json:8,9): ResNet-50 bf16 data-parallel training on synthetic
+ImageNet-shape batches (NHWC 224x224, 1000 classes, SGD-momentum, fp32 master
+weights), random-init weights; weak scaling (fixed per-GPU batch).  BERT-base
+seq-128 fine-tuning (AdamW) is measured in the same run and reported under
+``extra`` (``--model resnet50`` skips it).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def run_one(model: str, args, world: int):
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    if model == "resnet50":
+        cfg = get_preset("resnet50_ddp", batch_size=args.batch or 256)
+    else:
+        cfg = get_preset("bert_base_ddp", batch_size=args.bert_batch or 128, dropout=0.1)
+    cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
+                      bucket_mb=args.bucket_mb, cuda_graph=args.cuda_graph)
+    tr = Trainer(cfg)
+    s = tr.run()
+    del tr
+    return s
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="both", choices=["both", "resnet50", "bert_base"])
+    ap.add_argument("--batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
+    ap.add_argument("--bert-batch", type=int, default=0, help="BERT-base per-GPU batch (default 128)")
+    ap.add_argument("--native", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--cuda-graph", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from databricks_distributed_deep_learning_amd.parallel import dist as ddist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    ddist.init("auto")
+    results = {}
+    order = ["resnet50", "bert_base"] if args.model == "both" else [args.model]
+    for m in order:
+        results[m] = run_one(m, args, world)
+        log(f"[bench] {m}: {json.dumps(results[m])}")
+        torch.cuda.empty_cache() if torch.cuda.is_available() else None
+
+    head = results.get("resnet50") or results[order[0]]
+    is_r50 = "resnet50" in results
+    line = {
+        "metric": "ResNet-50 images/sec (whole node)" if is_r50 else "BERT-base samples/sec (whole node)",
+        "value": round(head["samples_per_sec"], 2),
+        "unit": "images/s" if is_r50 else "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(head["ms_per_step"], 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,   # BASELINE.json "published": {} — the reference publishes no number
+        "dtype": "bf16",
+        "data": "synthetic (device-resident random NHWC images / token ids), random-init weights",
+        "config": {
+            "model": head["model"],
+            "global_batch": head["global_batch"],
+            "per_gpu_batch": head["per_rank_batch"],
+            "seq_len": head["seq_len"],
+            "image_size": 224 if is_r50 else None,
+            "optimizer": head["optimizer"],
+            "parallelism": f"dp{world}",
+            "native_kernels": head["native"],
+        },
+    }
+    if "bert_base" in results and is_r50:
+        b = results["bert_base"]
+        line["extra"] = {
+            "bert_base_samples_per_sec": round(b["samples_per_sec"], 2),
+            "bert_base_ms_per_step": round(b["ms_per_step"], 3),
+            "bert_base_global_batch": b["global_batch"],
+            "bert_base_seq_len": b["seq_len"],
+        }
+    if ddist.is_main():
+        print(json.dumps(line), flush=True)
+    ddist.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Build the native kernel library for gfx950 (MI355X).
+
+    python csrc/build.py [--clean] [-j N] [--debug]
+
+Compiles every ``csrc/kernels/*.hip`` and ``csrc/runtime/*.cpp`` with
+``hipcc --offload-arch=gfx950`` (cross-compiles without a GPU) into
+``databricks_distributed_deep_learning_amd/_native/libddl_kernels.so``: one
+shared object with a plain C ABI, loaded by ``ops/_lib.py`` via ctypes.  No
+torch headers are involved, so a full rebuild takes seconds, and objects are
+rebuilt only when a source or header is newer than its object.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "native")
+OUT_DIR = os.path.join(ROOT, "databricks_distributed_deep_learning_amd", "_native")
+OUT = os.path.join(OUT_DIR, "libddl_kernels.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DDL_OFFLOAD_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(CSRC, "include"),
+          "-Wno-unused-result", "-ffp-contract=fast", "-munsafe-fp-atomics"]
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + \
+        sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+
+
+def headers():
+    return glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+
+
+def obj_for(src):
+    return os.path.join(BUILD, os.path.basename(src) + ".o")
+
+
+def needs(src, obj, hdr_mtime):
+    if not os.path.exists(obj):
+        return True
+    m = os.path.getmtime(obj)
+    return os.path.getmtime(src) > m or hdr_mtime > m
+
+
+def compile_one(src, debug=False):
+    obj = obj_for(src)
+    flags = list(COMMON)
+    if debug:
+        flags = [f for f in flags if f != "-O3"] + ["-O1", "-g"]
+    if src.endswith(".cpp"):
+        flags += ["-x", "hip"]
+    cmd = [HIPCC, *flags, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool = True) -> str:
+    if clean and os.path.isdir(BUILD):
+        shutil.rmtree(BUILD)
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(OUT_DIR, exist_ok=True)
+    srcs = sources()
+    if not srcs:
+        raise RuntimeError("no native sources found under csrc/")
+    hm = max([os.path.getmtime(h) for h in headers()] + [0.0])
+    todo = [s for s in srcs if needs(s, obj_for(s), hm)]
+    if verbose:
+        print(f"[build] {len(todo)}/{len(srcs)} sources to compile for {ARCH}", file=sys.stderr)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        futs = {ex.submit(compile_one, s, debug): s for s in todo}
+        for f in cf.as_completed(futs):
+            f.result()
+            if verbose:
+                print(f"[build]   ok {os.path.relpath(futs[f], ROOT)}", file=sys.stderr)
+    objs = [obj_for(s) for s in srcs]
+    newest = max(os.path.getmtime(o) for o in objs)
+    if todo or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest:
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp",
+               "-L/opt/rocm/lib", "-Wl,--no-as-needed", "-lamdhip64"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(OUT + ".tmp", OUT)
+        if verbose:
+            print(f"[build] linked {os.path.relpath(OUT, ROOT)}", file=sys.stderr)
+    return OUT
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args()
+    build(a.jobs, a.clean, a.debug)

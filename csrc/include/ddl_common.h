@@ -1,0 +1,152 @@
+// Common device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// Conventions: wave64 everywhere (hard-coded 64, never 32), bf16 stored as raw
+// 16-bit payloads, every memory-bound kernel moves 16 bytes per lane.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+#define DDL_API extern "C" __attribute__((visibility("default")))
+#define DDL_WAVE 64
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Launch-error helper: every C entry point returns the HIP error code (0 = ok).
+#define DDL_RETURN_LAUNCH() return (int)hipGetLastError()
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even; NaN stays NaN.  hipcc lowers the __bf16 cast to
+// v_cvt_pk_bf16_f32 on gfx950.
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    __bf16 h = (__bf16)f;
+    return __builtin_bit_cast(bf16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// 8 bf16 <-> 8 floats through one 16-byte access.
+__device__ __forceinline__ void load8(const bf16_t* p, float* v) {
+    uint4 u = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* v) {
+    uint4 u;
+    u.x = pack2bf(v[0], v[1]);
+    u.y = pack2bf(v[2], v[3]);
+    u.z = pack2bf(v[4], v[5]);
+    u.w = pack2bf(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = u;
+}
+__device__ __forceinline__ void load8(const float* p, float* v) {
+    float4 a = reinterpret_cast<const float4*>(p)[0];
+    float4 b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void load4(const bf16_t* p, float* v) {
+    uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void store4(bf16_t* p, const float* v) {
+    uint2 u; u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]);
+    *reinterpret_cast<uint2*>(p) = u;
+}
+__device__ __forceinline__ void load4(const float* p, float* v) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+__device__ __forceinline__ void store4(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ float to_f(bf16_t x) { return bf2f(x); }
+__device__ __forceinline__ float to_f(float x) { return x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float x) { return f2bf(x); }
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64); `red` holds NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    __syncthreads();
+    return t;
+}
+
+// ---------------------------------------------------------------- math
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+    const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+    const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+    return cdf + x * pdf;
+}
+
+// Counter-based hash RNG (splitmix/murmur finaliser): uniform in [0,1) from
+// (seed, index) so dropout masks are regenerated in backward, never stored.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xBF58476D1CE4E5B9ull + 0x94D049BB133111EBull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 32);
+}
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
+    return hash_u32(seed, idx) >= thresh;   // P(keep) = 1 - thresh / 2^32
+}
+
+// Fast unsigned division by a runtime constant (magic multiply), for index math
+// in hot loops: q = umulhi(n, mul) >> shift, exact for n < 2^31.
+struct FastDiv {
+    uint32_t d, mul, shift;
+};
+__host__ inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f; f.d = d;
+    uint32_t s = 0;
+    while ((1ull << s) < d) ++s;
+    f.shift = s;
+    f.mul = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+    if (d == 1) { f.mul = 0; f.shift = 0; }
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+    if (f.d == 1) return n;
+    uint32_t t = __umulhi(n, f.mul);
+    return (t + n) >> f.shift;
+}

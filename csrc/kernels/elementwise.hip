@@ -1,0 +1,389 @@
+// Memory-bound elementwise / reduction kernels for gfx950: GELU, dropout,
+// bias-gradient column sums, softmax cross-entropy, NHWC pooling, embedding.
+// Every kernel moves 8 elements (16 B of bf16) per lane per access.
+#include "ddl_common.h"
+
+namespace {
+
+inline int grid_for(long n, int nt = 256, int cap = 8192) {
+    long g = (n + nt - 1) / nt;
+    return (int)std::max<long>(1, std::min<long>(g, cap));
+}
+
+// ------------------------------------------------------------------ GELU
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_fwd_k(const T* __restrict__ x, T* __restrict__ y, long n8) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        float v[8];
+        load8(x + i * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+        store8(y + i * 8, v);
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ dy, const T* __restrict__ x, T* __restrict__ dx,
+                                                  long n8) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        float g[8], v[8];
+        load8(dy + i * 8, g);
+        load8(x + i * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = g[j] * gelu_erf_grad(v[j]);
+        store8(dx + i * 8, v);
+    }
+}
+
+// ------------------------------------------------------------------ dropout
+// keep iff hash(seed, idx) >= thresh; mask regenerated in backward.
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_k(const T* __restrict__ x, T* __restrict__ y, long n8, uint64_t seed,
+                                                 uint32_t thresh, float scale) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        float v[8];
+        load8(x + i * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = keep_elem(seed, (uint64_t)(i * 8 + j), thresh) ? v[j] * scale : 0.f;
+        store8(y + i * 8, v);
+    }
+}
+
+// ------------------------------------------------------------------ column sums
+// out[c] = sum_r x[r, c] (bias gradient).  Partial per block then finalize.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ x, long rows, int C, int rows_per_blk,
+                                                        float* __restrict__ part) {
+    // each thread owns 8 columns; the block covers 256*8 columns x rows_per_blk rows
+    const int c0 = (blockIdx.y * 256 + threadIdx.x) * 8;
+    if (c0 >= C) return;
+    const long r0 = (long)blockIdx.x * rows_per_blk;
+    const long r1 = std::min<long>(rows, r0 + rows_per_blk);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (long r = r0; r < r1; ++r) {
+        float v[8];
+        load8(x + r * C + c0, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[j];
+    }
+    store8(part + (long)blockIdx.x * C + c0, s);
+}
+template <typename TO>
+__global__ void colsum_final_k(const float* __restrict__ part, int nblk, int C, TO* __restrict__ out, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += part[(long)b * C + c];
+    if (accumulate) s += to_f(out[c]);
+    out[c] = from_f<TO>(s);
+}
+
+// ------------------------------------------------------------------ softmax CE
+// One block (256 threads) per row.  Writes per-row loss and d(loss)/d(logits)
+// for mean reduction (softmax - onehot) / B, in one pass over the logits.
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_ce_k(const T* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                    int C, float inv_b, float* __restrict__ row_loss,
+                                                    T* __restrict__ dlogits) {
+    __shared__ float red[4];
+    const long row = blockIdx.x;
+    const T* x = logits + row * C;
+    float m = -INFINITY;
+    for (int c = threadIdx.x; c < C; c += 256) m = fmaxf(m, to_f(x[c]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float s = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) s += __expf(to_f(x[c]) - m);
+    s = block_sum<256>(s, red);
+    const float lse = m + __logf(s);
+    const long lab = labels[row];
+    if (threadIdx.x == 0) row_loss[row] = lse - to_f(x[lab]);
+    if (dlogits) {
+        const float inv_s = 1.f / s;
+        for (int c = threadIdx.x; c < C; c += 256) {
+            const float p = __expf(to_f(x[c]) - m) * inv_s;
+            dlogits[row * C + c] = from_f<T>((p - (c == lab ? 1.f : 0.f)) * inv_b);
+        }
+    }
+}
+__global__ void mean_k(const float* __restrict__ v, long n, float* __restrict__ out) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (long i = threadIdx.x; i < n; i += 256) s += v[i];
+    s = block_sum<256>(s, red);
+    if (threadIdx.x == 0) out[0] = s / (float)n;
+}
+template <typename T>
+__global__ __launch_bounds__(256) void scale_k(const T* __restrict__ x, const float* __restrict__ s, T* __restrict__ y,
+                                               long n) {
+    const float a = s[0];
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = from_f<T>(to_f(x[i]) * a);
+}
+
+// ------------------------------------------------------------------ NHWC max-pool 3x3/2
+// Forward also records the window argmax (0..8) so backward is a gather.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ idx,
+                                                     int N, int H, int W, int C, int P, int Q, int K, int S, int pad) {
+    const int c8 = C / 8;
+    const long total = (long)N * P * Q * c8;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cg = (int)(i % c8);
+        long t = i / c8;
+        const int q = (int)(t % Q); t /= Q;
+        const int p = (int)(t % P);
+        const int n = (int)(t / P);
+        float best[8];
+        uint8_t arg[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+        for (int r = 0; r < K; ++r) {
+            const int h = p * S - pad + r;
+            if (h < 0 || h >= H) continue;
+            for (int s = 0; s < K; ++s) {
+                const int w = q * S - pad + s;
+                if (w < 0 || w >= W) continue;
+                float v[8];
+                load8(x + (((long)n * H + h) * W + w) * C + cg * 8, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (v[j] > best[j] || (v[j] != v[j])) { best[j] = v[j]; arg[j] = (uint8_t)(r * K + s); }
+            }
+        }
+        store8(y + i * 8, best);
+        uint2 packed;
+        packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+        packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
+        *reinterpret_cast<uint2*>(idx + i * 8) = packed;
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                     T* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int K,
+                                                     int S, int pad) {
+    const int c8 = C / 8;
+    const long total = (long)N * H * W * c8;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cg = (int)(i % c8);
+        long t = i / c8;
+        const int w = (int)(t % W); t /= W;
+        const int h = (int)(t % H);
+        const int n = (int)(t / H);
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // outputs whose window covers (h, w): p*S - pad <= h <= p*S - pad + K - 1
+        const int p_lo = std::max(0, (h + pad - K + S) / S), p_hi = std::min(P - 1, (h + pad) / S);
+        const int q_lo = std::max(0, (w + pad - K + S) / S), q_hi = std::min(Q - 1, (w + pad) / S);
+        for (int p = p_lo; p <= p_hi; ++p) {
+            const int r = h - (p * S - pad);
+            if (r < 0 || r >= K) continue;
+            for (int q = q_lo; q <= q_hi; ++q) {
+                const int s = w - (q * S - pad);
+                if (s < 0 || s >= K) continue;
+                const long o = (((long)n * P + p) * Q + q) * C + cg * 8;
+                float g[8];
+                load8(dy + o, g);
+                const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
+                const uint8_t want = (uint8_t)(r * K + s);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t word = j < 4 ? packed.x : packed.y;
+                    const uint8_t a = (uint8_t)(word >> (8 * (j & 3)));
+                    if (a == want) acc[j] += g[j];
+                }
+            }
+        }
+        store8(dx + i * 8, acc);
+    }
+}
+
+// ------------------------------------------------------------------ global avg-pool
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N, int HW, int C) {
+    const int c8 = C / 8;
+    const long total = (long)N * c8;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cg = (int)(i % c8);
+        const long n = i / c8;
+        float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < HW; ++k) {
+            float v[8];
+            load8(x + (n * HW + k) * C + cg * 8, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] += v[j];
+        }
+        const float inv = 1.f / HW;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] *= inv;
+        store8(y + n * C + cg * 8, s);
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_bwd_k(const T* __restrict__ dy, T* __restrict__ dx, int N, int HW, int C) {
+    const int c8 = C / 8;
+    const long total = (long)N * HW * c8;
+    const float inv = 1.f / HW;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cg = (int)(i % c8);
+        const long n = i / ((long)HW * c8);
+        float g[8];
+        load8(dy + n * C + cg * 8, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] *= inv;
+        store8(dx + i * 8, g);
+    }
+}
+
+// ------------------------------------------------------------------ embedding
+template <typename T>
+__global__ __launch_bounds__(256) void embed_fwd_k(const int64_t* __restrict__ ids, const T* __restrict__ w,
+                                                   T* __restrict__ y, long n_tok, int D) {
+    const int d8 = D / 8;
+    const long total = n_tok * d8;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long t = i / d8;
+        const int dg = (int)(i % d8);
+        const long id = ids[t];
+        *reinterpret_cast<uint4*>(y + t * D + dg * 8) = *reinterpret_cast<const uint4*>(w + id * D + dg * 8);
+        if (sizeof(T) == 4)
+            *reinterpret_cast<uint4*>(y + t * D + dg * 8 + 4) = *reinterpret_cast<const uint4*>(w + id * D + dg * 8 + 4);
+    }
+}
+// scatter-add into an fp32 accumulator (one 256-B row segment per wave instruction)
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_k(const int64_t* __restrict__ ids, const T* __restrict__ dy,
+                                                   float* __restrict__ acc, long n_tok, int D) {
+    const long total = n_tok * D;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long t = i / D;
+        const int d = (int)(i % D);
+        atomicAdd(acc + ids[t] * D + d, to_f(dy[i]));
+    }
+}
+template <typename TO>
+__global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ x, TO* __restrict__ y, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        y[i] = from_f<TO>(x[i]);
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+#define DISPATCH_T(dtype, KERNEL_CALL_BF16, KERNEL_CALL_F32) \
+    do { if ((dtype) == 1) { KERNEL_CALL_BF16; } else { KERNEL_CALL_F32; } } while (0)
+
+DDL_API int ddl_gelu_fwd(int dtype, const void* x, void* y, long n, hipStream_t st) {
+    if (n % 8) return -1;
+    const long n8 = n / 8;
+    DISPATCH_T(dtype, (gelu_fwd_k<bf16_t><<<grid_for(n8), 256, 0, st>>>((const bf16_t*)x, (bf16_t*)y, n8)),
+               (gelu_fwd_k<float><<<grid_for(n8), 256, 0, st>>>((const float*)x, (float*)y, n8)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_gelu_bwd(int dtype, const void* dy, const void* x, void* dx, long n, hipStream_t st) {
+    if (n % 8) return -1;
+    const long n8 = n / 8;
+    DISPATCH_T(dtype,
+               (gelu_bwd_k<bf16_t><<<grid_for(n8), 256, 0, st>>>((const bf16_t*)dy, (const bf16_t*)x, (bf16_t*)dx, n8)),
+               (gelu_bwd_k<float><<<grid_for(n8), 256, 0, st>>>((const float*)dy, (const float*)x, (float*)dx, n8)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_dropout(int dtype, const void* x, void* y, long n, uint64_t seed, float p, hipStream_t st) {
+    if (n % 8) return -1;
+    const long n8 = n / 8;
+    const uint32_t thresh = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+    const float scale = 1.f / (1.f - p);
+    DISPATCH_T(dtype,
+               (dropout_k<bf16_t><<<grid_for(n8), 256, 0, st>>>((const bf16_t*)x, (bf16_t*)y, n8, seed, thresh, scale)),
+               (dropout_k<float><<<grid_for(n8), 256, 0, st>>>((const float*)x, (float*)y, n8, seed, thresh, scale)));
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_colsum_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(256, (rows + 63) / 64)); }
+
+// out[c] (+)= sum_r x[r, c]; `part` needs ddl_colsum_nblk(rows) * C floats.
+DDL_API int ddl_colsum(int dtype, const void* x, long rows, int C, float* part, void* out, int out_dtype,
+                       int accumulate, hipStream_t st) {
+    if (C % 8) return -1;
+    const int nblk = ddl_colsum_nblk(rows);
+    const int rpb = (int)((rows + nblk - 1) / nblk);
+    dim3 g(nblk, (C / 8 + 255) / 256);
+    DISPATCH_T(dtype, (colsum_partial_k<bf16_t><<<g, 256, 0, st>>>((const bf16_t*)x, rows, C, rpb, part)),
+               (colsum_partial_k<float><<<g, 256, 0, st>>>((const float*)x, rows, C, rpb, part)));
+    if (out_dtype == 1) colsum_final_k<bf16_t><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, (bf16_t*)out, accumulate);
+    else colsum_final_k<float><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, (float*)out, accumulate);
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_softmax_ce(int dtype, const void* logits, const int64_t* labels, long B, int C, float* row_loss,
+                           float* loss, void* dlogits, hipStream_t st) {
+    const float inv_b = 1.f / (float)B;
+    DISPATCH_T(dtype,
+               (softmax_ce_k<bf16_t><<<B, 256, 0, st>>>((const bf16_t*)logits, labels, C, inv_b, row_loss,
+                                                        (bf16_t*)dlogits)),
+               (softmax_ce_k<float><<<B, 256, 0, st>>>((const float*)logits, labels, C, inv_b, row_loss,
+                                                       (float*)dlogits)));
+    mean_k<<<1, 256, 0, st>>>(row_loss, B, loss);
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_scale_by(int dtype, const void* x, const float* s, void* y, long n, hipStream_t st) {
+    DISPATCH_T(dtype, (scale_k<bf16_t><<<grid_for(n), 256, 0, st>>>((const bf16_t*)x, s, (bf16_t*)y, n)),
+               (scale_k<float><<<grid_for(n), 256, 0, st>>>((const float*)x, s, (float*)y, n)));
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q,
+                            int K, int S, int pad, hipStream_t st) {
+    if (C % 8) return -1;
+    const long tot = (long)N * P * Q * (C / 8);
+    DISPATCH_T(dtype,
+               (maxpool_fwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)x, (bf16_t*)y, idx, N, H, W, C, P,
+                                                                      Q, K, S, pad)),
+               (maxpool_fwd_k<float><<<grid_for(tot), 256, 0, st>>>((const float*)x, (float*)y, idx, N, H, W, C, P, Q,
+                                                                     K, S, pad)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int P,
+                            int Q, int K, int S, int pad, hipStream_t st) {
+    if (C % 8) return -1;
+    const long tot = (long)N * H * W * (C / 8);
+    DISPATCH_T(dtype,
+               (maxpool_bwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)dy, idx, (bf16_t*)dx, N, H, W, C,
+                                                                      P, Q, K, S, pad)),
+               (maxpool_bwd_k<float><<<grid_for(tot), 256, 0, st>>>((const float*)dy, idx, (float*)dx, N, H, W, C, P, Q,
+                                                                     K, S, pad)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_avgpool_fwd(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t st) {
+    if (C % 8) return -1;
+    const long tot = (long)N * (C / 8);
+    DISPATCH_T(dtype, (avgpool_fwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)x, (bf16_t*)y, N, HW, C)),
+               (avgpool_fwd_k<float><<<grid_for(tot), 256, 0, st>>>((const float*)x, (float*)y, N, HW, C)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_avgpool_bwd(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
+    if (C % 8) return -1;
+    const long tot = (long)N * HW * (C / 8);
+    DISPATCH_T(dtype, (avgpool_bwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)dy, (bf16_t*)dx, N, HW, C)),
+               (avgpool_bwd_k<float><<<grid_for(tot), 256, 0, st>>>((const float*)dy, (float*)dx, N, HW, C)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_embedding_fwd(int dtype, const int64_t* ids, const void* w, void* y, long n_tok, int D, hipStream_t st) {
+    if (D % 8) return -1;
+    const long tot = n_tok * (D / 8);
+    DISPATCH_T(dtype, (embed_fwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>(ids, (const bf16_t*)w, (bf16_t*)y, n_tok, D)),
+               (embed_fwd_k<float><<<grid_for(tot), 256, 0, st>>>(ids, (const float*)w, (float*)y, n_tok, D)));
+    DDL_RETURN_LAUNCH();
+}
+// acc must be zeroed (fp32 [V, D]); then cast into dw (dtype) of V*D elements.
+DDL_API int ddl_embedding_bwd(int dtype, const int64_t* ids, const void* dy, float* acc, void* dw, long n_tok, long V,
+                              int D, hipStream_t st) {
+    const long tot = n_tok * D;
+    DISPATCH_T(dtype, (embed_bwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>(ids, (const bf16_t*)dy, acc, n_tok, D)),
+               (embed_bwd_k<float><<<grid_for(tot), 256, 0, st>>>(ids, (const float*)dy, acc, n_tok, D)));
+    const long n = V * D;
+    DISPATCH_T(dtype, (cast_f32_k<bf16_t><<<grid_for(n), 256, 0, st>>>(acc, (bf16_t*)dw, n)),
+               (cast_f32_k<float><<<grid_for(n), 256, 0, st>>>(acc, (float*)dw, n)));
+    DDL_RETURN_LAUNCH();
+}

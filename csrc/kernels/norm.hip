@@ -1,0 +1,517 @@
+// BatchNorm (NHWC, channels innermost) and LayerNorm kernels for gfx950.
+//
+// BatchNorm training forward = 3 launches:
+//   bn_stats_partial  : per-block per-channel (sum, sumsq), 16-byte loads
+//   bn_stats_finalize : merge partials in fp64, mean/invstd, running-stat update,
+//                       fold gamma/beta into per-channel (scale, shift)
+//   bn_apply          : y = x*scale + shift (+ residual) (ReLU), one pass
+// BatchNorm backward = bn_bwd_partial (sum dz, sum dz*xhat) -> bn_bwd_finalize
+// (dgamma, dbeta) -> bn_bwd_apply (dx, and dresidual = dz when the residual add
+// was fused).  The ReLU mask is recomputed from the saved output, never stored.
+//
+// LayerNorm: one wave per row (H % 256 == 0: BERT-base 768, BERT-large 1024),
+// fused residual add, fp32 statistics saved for backward; backward computes dx
+// per row and per-block dgamma/dbeta partials reduced by a second kernel.
+#include "ddl_common.h"
+
+namespace {
+
+constexpr int BN_NT = 256;
+
+// ------------------------------------------------------------------ BN stats
+template <typename T>
+__global__ __launch_bounds__(BN_NT) void bn_stats_partial_k(const T* __restrict__ x, long M, int C,
+                                                            int rows_per_blk, float* __restrict__ part) {
+    __shared__ float s_red[2 * BN_NT * 8];
+    const int tpr = C / 8;            // threads per row (each owns 8 channels)
+    const int rpi = BN_NT / tpr;      // rows per iteration
+    const int tid = threadIdx.x;
+    const int cg = tid % tpr, rr = tid / tpr;
+    const long r0 = (long)blockIdx.x * rows_per_blk;
+    const long r1 = min(M, r0 + rows_per_blk);
+    float s[8], q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+    for (long r = r0 + rr; r < r1; r += rpi) {
+        float v[8];
+        load8(x + r * C + cg * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s[j] += v[j]; q[j] += v[j] * v[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        s_red[tid * 8 + j] = s[j];
+        s_red[BN_NT * 8 + tid * 8 + j] = q[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += BN_NT) {
+        float a = 0.f, b = 0.f;
+        for (int i = 0; i < rpi; ++i) {
+            a += s_red[i * C + c];
+            b += s_red[BN_NT * 8 + i * C + c];
+        }
+        part[(long)blockIdx.x * 2 * C + c] = a;
+        part[(long)blockIdx.x * 2 * C + C + c] = b;
+    }
+}
+
+template <typename TP>
+__global__ void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M, const TP* __restrict__ gamma,
+                                    const TP* __restrict__ beta, float* __restrict__ running_mean,
+                                    float* __restrict__ running_var, float momentum, float eps,
+                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int b = 0; b < nblk; ++b) {
+        s += part[(long)b * 2 * C + c];
+        q += part[(long)b * 2 * C + C + c];
+    }
+    const double mean = s / (double)M;
+    double var = q / (double)M - mean * mean;
+    if (var < 0) var = 0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[c] = (float)mean;
+    save_invstd[c] = invstd;
+    if (running_mean) {
+        const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+    }
+    const float g = gamma ? to_f(gamma[c]) : 1.f;
+    const float bb = beta ? to_f(beta[c]) : 0.f;
+    scale[c] = g * invstd;
+    shift[c] = bb - (float)mean * g * invstd;
+}
+
+// eval mode: scale/shift from running statistics
+template <typename TP>
+__global__ void bn_eval_coeffs_k(int C, const TP* __restrict__ gamma, const TP* __restrict__ beta,
+                                 const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                 float* __restrict__ scale, float* __restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float inv = rsqrtf(rv[c] + eps);
+    const float g = gamma ? to_f(gamma[c]) : 1.f;
+    const float bb = beta ? to_f(beta[c]) : 0.f;
+    scale[c] = g * inv;
+    shift[c] = bb - rm[c] * g * inv;
+}
+
+template <typename T, bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
+                                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  T* __restrict__ y, long n8, int C) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        const int c0 = (int)((i * 8) % C);
+        float v[8], sc[8], sh[8];
+        load8(x + i * 8, v);
+        load8(scale + c0, sc);
+        load8(shift + c0, sh);
+        float r[8];
+        if (RES) load8(res + i * 8, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float t = v[j] * sc[j] + sh[j];
+            if (RES) t += r[j];
+            if (RELU) t = fmaxf(t, 0.f);
+            v[j] = t;
+        }
+        store8(y + i * 8, v);
+    }
+}
+
+// ------------------------------------------------------------------ BN backward
+template <typename T, bool RELU>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ dy, const T* __restrict__ yout,
+                                                          const T* __restrict__ x, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, long M, int C,
+                                                          int rows_per_blk, float* __restrict__ part) {
+    __shared__ float s_red[2 * BN_NT * 8];
+    const int tpr = C / 8, rpi = BN_NT / tpr, tid = threadIdx.x;
+    const int cg = tid % tpr, rr = tid / tpr;
+    const long r0 = (long)blockIdx.x * rows_per_blk;
+    const long r1 = min(M, r0 + rows_per_blk);
+    float mu[8], is[8], a[8], b[8];
+    load8(mean + cg * 8, mu);
+    load8(invstd + cg * 8, is);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
+    for (long r = r0 + rr; r < r1; r += rpi) {
+        float g[8], xv[8], yo[8];
+        load8(dy + r * C + cg * 8, g);
+        load8(x + r * C + cg * 8, xv);
+        if (RELU) load8(yout + r * C + cg * 8, yo);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float dz = RELU ? (yo[j] > 0.f ? g[j] : 0.f) : g[j];
+            a[j] += dz;
+            b[j] += dz * (xv[j] - mu[j]) * is[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        s_red[tid * 8 + j] = a[j];
+        s_red[BN_NT * 8 + tid * 8 + j] = b[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += BN_NT) {
+        float s = 0.f, q = 0.f;
+        for (int i = 0; i < rpi; ++i) {
+            s += s_red[i * C + c];
+            q += s_red[BN_NT * 8 + i * C + c];
+        }
+        part[(long)blockIdx.x * 2 * C + c] = s;
+        part[(long)blockIdx.x * 2 * C + C + c] = q;
+    }
+}
+
+template <typename TP>
+__global__ void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+                                  const TP* __restrict__ gamma, const float* __restrict__ invstd,
+                                  TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int b = 0; b < nblk; ++b) {
+        s += part[(long)b * 2 * C + c];
+        q += part[(long)b * 2 * C + C + c];
+    }
+    if (dgamma) dgamma[c] = from_f<TP>((float)q);
+    if (dbeta) dbeta[c] = from_f<TP>((float)s);
+    const float g = gamma ? to_f(gamma[c]) : 1.f;
+    coef[c] = g * invstd[c];                 // k1
+    coef[C + c] = (float)(s / (double)M);    // mean(dz)
+    coef[2 * C + c] = (float)(q / (double)M);// mean(dz*xhat)
+}
+
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ yout,
+                                                      const T* __restrict__ x, const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
+                                                      T* __restrict__ dx, T* __restrict__ dres, long n8, int C) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        const int c0 = (int)((i * 8) % C);
+        float g[8], xv[8], yo[8], mu[8], is[8], k1[8], mb[8], mg[8];
+        load8(dy + i * 8, g);
+        load8(x + i * 8, xv);
+        if (RELU) load8(yout + i * 8, yo);
+        load8(mean + c0, mu);
+        load8(invstd + c0, is);
+        load8(coef + c0, k1);
+        load8(coef + C + c0, mb);
+        load8(coef + 2 * C + c0, mg);
+        float o[8], dz[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dz[j] = RELU ? (yo[j] > 0.f ? g[j] : 0.f) : g[j];
+            const float xh = (xv[j] - mu[j]) * is[j];
+            o[j] = k1[j] * (dz[j] - mb[j] - xh * mg[j]);
+        }
+        store8(dx + i * 8, o);
+        if (DRES) store8(dres + i * 8, dz);
+    }
+}
+
+// ------------------------------------------------------------------ LayerNorm
+// One wave per row; each lane owns VPL = H/256 chunks of 4 contiguous elements
+// (lane chunk k covers columns 256*k + 4*lane .. +3): every load is 8 B/lane,
+// fully coalesced per wave.
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T* __restrict__ res, long res_rows,
+                                                const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
+                                                float* __restrict__ save_mean, float* __restrict__ save_rstd, long rows,
+                                                int H, float eps) {
+    const int lane = threadIdx.x & 63;
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    float v[VPL][4];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        const int col = 256 * k + 4 * lane;
+        load4(x + row * H + col, v[k]);
+        if (res) {
+            float r[4];
+            load4(res + (row % res_rows) * H + col, r);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[k][j] += r[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += v[k][j];
+    }
+    const float mean = wave_sum(s) / H;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[k][j] - mean; q += d * d; }
+    const float rstd = rsqrtf(wave_sum(q) / H + eps);
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        const int col = 256 * k + 4 * lane;
+        float g[4], b[4], o[4];
+        load4(gamma + col, g);
+        load4(beta + col, b);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + b[j];
+        store4(y + row * H + col, o);
+    }
+    if (lane == 0) { save_mean[row] = mean; save_rstd[row] = rstd; }
+}
+
+// dx per row + dgamma/dbeta partials per block (ROWS_PER_BLK rows, 4 waves).
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                const T* __restrict__ res, long res_rows, const T* __restrict__ gamma,
+                                                const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                T* __restrict__ dx, float* __restrict__ part, long rows, int H,
+                                                int rows_per_blk) {
+    __shared__ float s_acc[2][4][VPL * 256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float dg[VPL][4], db[VPL][4], g[VPL][4];
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        load4(gamma + 256 * k + 4 * lane, g[k]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; }
+    }
+    const long r0 = (long)blockIdx.x * rows_per_blk;
+    const long r1 = min(rows, r0 + rows_per_blk);
+    for (long row = r0 + w; row < r1; row += 4) {
+        const float mu = mean[row], rs = rstd[row];
+        float xh[VPL][4], gy[VPL][4];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+            const int col = 256 * k + 4 * lane;
+            float xv[4], d[4];
+            load4(x + row * H + col, xv);
+            if (res) {
+                float r[4];
+                load4(res + (row % res_rows) * H + col, r);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) xv[j] += r[j];
+            }
+            load4(dy + row * H + col, d);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                xh[k][j] = (xv[j] - mu) * rs;
+                gy[k][j] = d[j] * g[k][j];
+                s1 += gy[k][j];
+                s2 += gy[k][j] * xh[k][j];
+                dg[k][j] += d[j] * xh[k][j];
+                db[k][j] += d[j];
+            }
+        }
+        const float m1 = wave_sum(s1) / H, m2 = wave_sum(s2) / H;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
+            store4(dx + row * H + 256 * k + 4 * lane, o);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < VPL; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            s_acc[0][w][256 * k + 4 * lane + j] = dg[k][j];
+            s_acc[1][w][256 * k + 4 * lane + j] = db[k][j];
+        }
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += 256) {
+        part[(long)blockIdx.x * 2 * H + c] = s_acc[0][0][c] + s_acc[0][1][c] + s_acc[0][2][c] + s_acc[0][3][c];
+        part[(long)blockIdx.x * 2 * H + H + c] = s_acc[1][0][c] + s_acc[1][1][c] + s_acc[1][2][c] + s_acc[1][3][c];
+    }
+}
+
+template <typename TP>
+__global__ void colsum_partials_k(const float* __restrict__ part, int nblk, int H, TP* __restrict__ dg,
+                                  TP* __restrict__ db) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= H) return;
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < nblk; ++i) {
+        a += part[(long)i * 2 * H + c];
+        b += part[(long)i * 2 * H + H + c];
+    }
+    dg[c] = from_f<TP>(a);
+    db[c] = from_f<TP>(b);
+}
+
+inline int grid_for(long n, int nt = 256, int cap = 4096) {
+    long g = (n + nt - 1) / nt;
+    return (int)std::max<long>(1, std::min<long>(g, cap));
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+// dtype codes: 0 = fp32, 1 = bf16
+
+DDL_API int ddl_bn_stats_nblk(long M, int C) {
+    const int rpi = BN_NT / (C / 8);
+    long nblk = std::min<long>(2048, (M + rpi - 1) / rpi);
+    return (int)std::max<long>(1, nblk);
+}
+
+DDL_API int ddl_bn_fwd_train(int dtype, const void* x, long M, int C, const void* gamma, const void* beta,
+                             float* running_mean, float* running_var, float momentum, float eps, float* part,
+                             float* save_mean, float* save_invstd, float* scale, float* shift, hipStream_t st) {
+    if (C % 8 || (BN_NT % (C / 8) != 0)) return -1;
+    const int nblk = ddl_bn_stats_nblk(M, C);
+    const int rpi = BN_NT / (C / 8);
+    long rpb = (M + nblk - 1) / nblk;
+    rpb = (rpb + rpi - 1) / rpi * rpi;
+    if (dtype == 1) {
+        bn_stats_partial_k<bf16_t><<<nblk, BN_NT, 0, st>>>((const bf16_t*)x, M, C, (int)rpb, part);
+        bn_stats_finalize_k<bf16_t><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
+            (const bf16_t*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+    } else {
+        bn_stats_partial_k<float><<<nblk, BN_NT, 0, st>>>((const float*)x, M, C, (int)rpb, part);
+        bn_stats_finalize_k<float><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, M, (const float*)gamma,
+            (const float*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+    }
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_bn_eval_coeffs(int dtype, int C, const void* gamma, const void* beta, const float* rm,
+                               const float* rv, float eps, float* scale, float* shift, hipStream_t st) {
+    if (dtype == 1)
+        bn_eval_coeffs_k<bf16_t><<<(C + 255) / 256, 256, 0, st>>>(C, (const bf16_t*)gamma, (const bf16_t*)beta, rm, rv,
+                                                                  eps, scale, shift);
+    else
+        bn_eval_coeffs_k<float><<<(C + 255) / 256, 256, 0, st>>>(C, (const float*)gamma, (const float*)beta, rm, rv,
+                                                                 eps, scale, shift);
+    DDL_RETURN_LAUNCH();
+}
+
+template <typename T>
+static void bn_apply_dispatch(const T* x, const T* res, const float* sc, const float* sh, T* y, long n, int C, int relu,
+                              hipStream_t st) {
+    const long n8 = n / 8;
+    const int g = grid_for(n8, 256, 8192);
+    if (res) {
+        if (relu) bn_apply_k<T, true, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
+        else bn_apply_k<T, true, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
+    } else {
+        if (relu) bn_apply_k<T, false, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
+        else bn_apply_k<T, false, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
+    }
+}
+
+DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float* scale, const float* shift, void* y,
+                         long n, int C, int relu, hipStream_t st) {
+    if (n % 8 || C % 8) return -1;
+    if (dtype == 1) bn_apply_dispatch((const bf16_t*)x, (const bf16_t*)res, scale, shift, (bf16_t*)y, n, C, relu, st);
+    else bn_apply_dispatch((const float*)x, (const float*)res, scale, shift, (float*)y, n, C, relu, st);
+    DDL_RETURN_LAUNCH();
+}
+
+template <typename T>
+static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float* mean, const float* invstd,
+                            const T* gamma, long M, int C, int relu, float* part, T* dgamma, T* dbeta, float* coef,
+                            T* dx, T* dres, hipStream_t st) {
+    const int nblk = ddl_bn_stats_nblk(M, C);
+    const int rpi = BN_NT / (C / 8);
+    long rpb = (M + nblk - 1) / nblk;
+    rpb = (rpb + rpi - 1) / rpi * rpi;
+    if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
+    else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
+    bn_bwd_finalize_k<T><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef);
+    const long n8 = M * C / 8;
+    const int g = grid_for(n8, 256, 8192);
+    if (relu) {
+        if (dres) bn_bwd_apply_k<T, true, true><<<g, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, n8, C);
+        else bn_bwd_apply_k<T, true, false><<<g, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, n8, C);
+    } else {
+        if (dres) bn_bwd_apply_k<T, false, true><<<g, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, n8, C);
+        else bn_bwd_apply_k<T, false, false><<<g, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, n8, C);
+    }
+}
+
+DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* yout, const void* x, const float* mean,
+                       const float* invstd, const void* gamma, long M, int C, int relu, float* part, void* dgamma,
+                       void* dbeta, float* coef, void* dx, void* dres, hipStream_t st) {
+    if (C % 8 || (BN_NT % (C / 8) != 0)) return -1;
+    if (dtype == 1)
+        bn_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)yout, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M,
+                        C, relu, part, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, st);
+    else
+        bn_bwd_dispatch((const float*)dy, (const float*)yout, (const float*)x, mean, invstd, (const float*)gamma, M, C,
+                        relu, part, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, st);
+    DDL_RETURN_LAUNCH();
+}
+
+// ---------------------------------------------------------------- LayerNorm
+template <typename T>
+static int ln_fwd_dispatch(const T* x, const T* res, long res_rows, const T* g, const T* b, T* y, float* mean,
+                           float* rstd, long rows, int H, float eps, hipStream_t st) {
+    const int grid = (int)((rows + 3) / 4);
+    switch (H / 256) {
+        case 1: ln_fwd_k<T, 1><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 2: ln_fwd_k<T, 2><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 3: ln_fwd_k<T, 3><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 4: ln_fwd_k<T, 4><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 5: ln_fwd_k<T, 5><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 6: ln_fwd_k<T, 6><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 8: ln_fwd_k<T, 8><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        default: return -1;
+    }
+    return 0;
+}
+
+DDL_API int ddl_ln_supported(int H) {
+    const int v = H / 256;
+    return (H % 256 == 0) && (v >= 1 && v <= 8 && v != 7);
+}
+
+DDL_API int ddl_ln_fwd(int dtype, const void* x, const void* res, long res_rows, const void* g, const void* b, void* y,
+                       float* mean, float* rstd, long rows, int H, float eps, hipStream_t st) {
+    if (!ddl_ln_supported(H)) return -1;
+    if (res_rows <= 0) res_rows = rows;
+    int rc = dtype == 1 ? ln_fwd_dispatch((const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
+                                          (const bf16_t*)b, (bf16_t*)y, mean, rstd, rows, H, eps, st)
+                        : ln_fwd_dispatch((const float*)x, (const float*)res, res_rows, (const float*)g,
+                                          (const float*)b, (float*)y, mean, rstd, rows, H, eps, st);
+    if (rc) return rc;
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(1024, (rows + 31) / 32)); }
+
+template <typename T>
+static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
+                           const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, hipStream_t st) {
+    const int nblk = ddl_ln_bwd_nblk(rows);
+    const int rpb = (int)((rows + nblk - 1) / nblk);
+    switch (H / 256) {
+        case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 4: ln_bwd_k<T, 4><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 5: ln_bwd_k<T, 5><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 6: ln_bwd_k<T, 6><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        default: return -1;
+    }
+    colsum_partials_k<T><<<(H + 255) / 256, 256, 0, st>>>(part, nblk, H, dg, db);
+    return 0;
+}
+
+DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res, long res_rows, const void* g,
+                       const float* mean, const float* rstd, void* dx, float* part, void* dg, void* db, long rows, int H,
+                       hipStream_t st) {
+    if (!ddl_ln_supported(H)) return -1;
+    if (res_rows <= 0) res_rows = rows;
+    int rc = dtype == 1
+                 ? ln_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
+                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, st)
+                 : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
+                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, st);
+    if (rc) return rc;
+    DDL_RETURN_LAUNCH();
+}

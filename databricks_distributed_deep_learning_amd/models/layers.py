@@ -1,0 +1,129 @@
+"""NN modules over the fused op layer (T-L2 in SURVEY §1.2).
+
+Parameters use the PyTorch/HF names so state dicts map one-to-one onto
+torchvision/HF checkpoints (conv weights are stored [Cout, KH, KW, Cin] and
+converted on load, see ``models.convert``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+class Conv2d(nn.Module):
+    """Bias-free NHWC convolution; weight [Cout, KH, KW, Cin]."""
+
+    def __init__(self, cin: int, cout: int, k: int, stride: int = 1, padding: int = 0):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride, self.padding = cin, cout, k, stride, padding
+        self.weight = nn.Parameter(torch.empty(cout, k, k, cin))
+        # kaiming_normal_(mode="fan_out", nonlinearity="relu") as torchvision's ResNet
+        std = math.sqrt(2.0 / (cout * k * k))
+        nn.init.normal_(self.weight, 0.0, std)
+
+    def forward(self, x):
+        return ops.conv2d(x, self.weight, self.stride, self.padding)
+
+    def extra_repr(self):
+        return f"{self.cin}, {self.cout}, k={self.k}, stride={self.stride}, padding={self.padding}"
+
+
+class BatchNorm2d(nn.Module):
+    """NHWC BatchNorm with optional fused ReLU and fused residual add.
+
+    Running statistics stay fp32 whatever the compute dtype.
+    """
+
+    def __init__(self, c: int, eps: float = 1e-5, momentum: float = 0.1, relu: bool = False,
+                 zero_init: bool = False):
+        super().__init__()
+        self.c, self.eps, self.momentum, self.relu = c, eps, momentum, relu
+        self.weight = nn.Parameter(torch.zeros(c) if zero_init else torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def forward(self, x, residual: Optional[torch.Tensor] = None):
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var,
+                              self.training, self.momentum, self.eps, self.relu, residual)
+
+    def _apply(self, fn, recurse=True):
+        # keep running stats in fp32 when the module is cast to bf16
+        rm, rv = self.running_mean, self.running_var
+        super()._apply(fn, recurse)
+        if self.running_mean.dtype != torch.float32:
+            self.running_mean = self.running_mean.float()
+            self.running_var = self.running_var.float()
+        return self
+
+    def extra_repr(self):
+        return f"{self.c}, eps={self.eps}, relu={self.relu}"
+
+
+class Linear(nn.Module):
+    def __init__(self, fin: int, fout: int, bias: bool = True, act: Optional[str] = None,
+                 init_std: Optional[float] = None):
+        super().__init__()
+        self.fin, self.fout, self.act = fin, fout, act
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.bias = nn.Parameter(torch.zeros(fout)) if bias else None
+        if init_std is not None:
+            nn.init.normal_(self.weight, 0.0, init_std)
+        else:
+            nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+            if self.bias is not None:
+                bound = 1.0 / math.sqrt(fin)
+                nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):
+        return ops.linear(x, self.weight, self.bias, self.act)
+
+    def extra_repr(self):
+        return f"{self.fin}, {self.fout}, bias={self.bias is not None}, act={self.act}"
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, d: int, eps: float = 1e-12):
+        super().__init__()
+        self.d, self.eps = d, eps
+        self.weight = nn.Parameter(torch.ones(d))
+        self.bias = nn.Parameter(torch.zeros(d))
+
+    def forward(self, x, residual: Optional[torch.Tensor] = None):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual)
+
+
+class Embedding(nn.Module):
+    def __init__(self, n: int, d: int, init_std: float = 0.02):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(n, d))
+        nn.init.normal_(self.weight, 0.0, init_std)
+
+    def forward(self, ids):
+        return ops.embedding(ids, self.weight)
+
+
+class Dropout(nn.Module):
+    def __init__(self, p: float):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        return ops.dropout(x, self.p, self.training)
+
+
+def cast_params(module: nn.Module, dtype: torch.dtype) -> nn.Module:
+    """Cast parameters (not BN running statistics) to ``dtype``."""
+    for m in module.modules():
+        for name, p in list(m._parameters.items()):
+            if p is not None and p.dtype != dtype and p.is_floating_point():
+                m._parameters[name] = nn.Parameter(p.data.to(dtype), requires_grad=p.requires_grad)
+    return module

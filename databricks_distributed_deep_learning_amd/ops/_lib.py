@@ -1,0 +1,174 @@
+"""Loader for the in-tree native kernel library (``libddl_kernels.so``).
+
+The HIP kernels in ``csrc/kernels/*.hip`` are compiled by ``csrc/build.py``
+(``hipcc --offload-arch=gfx950``) into one shared object with a plain C ABI:
+every launcher takes raw device pointers, shapes and a ``hipStream_t``.  We load
+it with ctypes *after* ``import torch`` so it binds to the HIP runtime PyTorch
+already loaded (same SONAME ``libamdhip64.so.7``) and launches on PyTorch's
+current stream — so the kernels are stream-ordered with ATen work and can be
+captured into hipGraphs.
+
+Policy (``DDL_NATIVE`` env or ``set_mode``):
+  * ``auto`` (default): GPU tensors use the HIP kernels; if the library is
+    missing on a GPU box we FAIL LOUDLY rather than silently fall back.
+  * ``off``: stock PyTorch ops everywhere (the baseline arm of the benchmark).
+  * CPU tensors always use the PyTorch reference implementations.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_DIR, "_native", "libddl_kernels.so")
+
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+_mode = os.environ.get("DDL_NATIVE", "auto").lower()
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def set_mode(mode: str) -> None:
+    global _mode
+    if mode not in ("auto", "on", "off"):
+        raise ValueError(mode)
+    _mode = mode
+
+
+def mode() -> str:
+    return _mode
+
+
+def load() -> Optional[ctypes.CDLL]:
+    global _lib, _load_error
+    if _lib is not None or _load_error is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        _load_error = f"{LIB_PATH} not built (run `python csrc/build.py`)"
+        return None
+    try:
+        _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:
+        _load_error = str(e)
+        return None
+    return _lib
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def load_error() -> Optional[str]:
+    load()
+    return _load_error
+
+
+def use_native(*tensors: torch.Tensor) -> bool:
+    """True when these (GPU) tensors should go through the HIP kernels."""
+    if _mode == "off":
+        return False
+    if not all(t is None or t.is_cuda for t in tensors):
+        return False
+    if load() is None:
+        raise NativeUnavailable(
+            f"HIP kernel library unavailable on a GPU run: {_load_error}. "
+            "Build it with `python csrc/build.py` or set DDL_NATIVE=off for stock PyTorch ops.")
+    return True
+
+
+def get() -> ctypes.CDLL:
+    lib = load()
+    if lib is None:
+        raise NativeUnavailable(_load_error)
+    return lib
+
+
+def stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"native kernel {what} failed with HIP error {rc}")
+
+
+# ------------------------------------------------------------------ signatures
+P, I, L, F, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_uint64
+_SIGS = {
+    # norm.hip
+    "ddl_bn_stats_nblk": [L, I],
+    "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],
+    "ddl_bn_eval_coeffs": [I, I, P, P, P, P, F, P, P, P],
+    "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P],
+    "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, P],
+    "ddl_ln_supported": [I],
+    "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, P],
+    "ddl_ln_bwd_nblk": [L],
+    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, P],
+    # elementwise.hip
+    "ddl_gelu_fwd": [I, P, P, L, P],
+    "ddl_gelu_bwd": [I, P, P, P, L, P],
+    "ddl_dropout": [I, P, P, L, U64, F, P],
+    "ddl_colsum_nblk": [L],
+    "ddl_colsum": [I, P, L, I, P, P, I, I, P],
+    "ddl_softmax_ce": [I, P, P, L, I, P, P, P, P],
+    "ddl_scale_by": [I, P, P, P, L, P],
+    "ddl_maxpool_fwd": [I, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "ddl_maxpool_bwd": [I, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "ddl_avgpool_fwd": [I, P, P, I, I, I, P],
+    "ddl_avgpool_bwd": [I, P, P, I, I, I, P],
+    "ddl_embedding_fwd": [I, P, P, P, L, I, P],
+    "ddl_embedding_bwd": [I, P, P, P, P, L, L, I, P],
+    # optim.hip
+    "ddl_sgd_step": [I, P, P, I, P, P, P, I, P, F, F, F, I, I, P],
+    "ddl_adamw_step": [I, P, P, I, P, P, P, P, I, P, F, F, F, F, F, F, F, P],
+    "ddl_lamb_step": [I, P, P, I, P, P, P, P, I, P, F, F, F, F, F, F, F, P, P],
+    "ddl_sumsq": [I, P, L, P, P],
+}
+_fns = {}
+
+
+def fn(name: str):
+    """Typed handle to a C entry point (argtypes from _SIGS, int return)."""
+    f = _fns.get(name)
+    if f is None:
+        f = getattr(get(), name)
+        if name in _SIGS:
+            f.argtypes = _SIGS[name]
+        f.restype = ctypes.c_int
+        _fns[name] = f
+    return f
+
+
+def call(name: str, *args) -> None:
+    """Call a launcher on the current stream (stream appended automatically)."""
+    rc = fn(name)(*args, stream())
+    if rc != 0:
+        raise RuntimeError(f"native kernel {name} failed with code {rc}")
+
+
+def register(sigs: dict) -> None:
+    _SIGS.update(sigs)
+
+
+def dcode(t: torch.Tensor) -> int:
+    """dtype code used by the C ABI: 0 fp32, 1 bf16."""
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError(f"native kernels support fp32/bf16, got {t.dtype}")
+
+
+def p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()

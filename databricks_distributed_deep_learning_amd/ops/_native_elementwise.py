@@ -1,0 +1,71 @@
+"""Autograd bindings for GELU / dropout (csrc/kernels/elementwise.hip)."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, dcode, p
+
+
+def new_seed() -> int:
+    """Host-side 62-bit seed from torch's CPU generator (no device sync)."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class _Gelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call("ddl_gelu_fwd", dcode(x), p(x), p(y), x.numel())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        call("ddl_gelu_bwd", dcode(x), p(dy), p(x), p(dx), x.numel())
+        return dx
+
+
+def gelu(x):
+    if x.numel() % 8 or x.dtype not in (torch.bfloat16, torch.float32):
+        import torch.nn.functional as F
+        return F.gelu(x)
+    return _Gelu.apply(x)
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, prob):
+        x = x.contiguous()
+        seed = new_seed()
+        y = torch.empty_like(x)
+        call("ddl_dropout", dcode(x), p(x), p(y), x.numel(), seed, float(prob))
+        ctx.seed, ctx.prob = seed, prob
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        call("ddl_dropout", dcode(dy), p(dy), p(dx), dy.numel(), ctx.seed, float(ctx.prob))
+        return dx, None
+
+
+def dropout(x, prob):
+    if x.numel() % 8 or x.dtype not in (torch.bfloat16, torch.float32):
+        import torch.nn.functional as F
+        return F.dropout(x, prob, True)
+    return _Dropout.apply(x, prob)
+
+
+def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """out[c] (+)= sum_r x[r, c]  (bias gradients)."""
+    from . import _lib
+    rows, C = x2d.shape
+    nblk = _lib.fn("ddl_colsum_nblk")(rows)
+    part = torch.empty(nblk * C, dtype=torch.float32, device=x2d.device)
+    call("ddl_colsum", dcode(x2d), p(x2d), rows, C, p(part), p(out), dcode(out), int(accumulate))
+    return out

@@ -1,0 +1,143 @@
+"""Autograd bindings for the HIP BatchNorm / LayerNorm kernels (csrc/kernels/norm.hip)."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import call, dcode, p
+
+
+def _bn_supported(C: int) -> bool:
+    return C % 8 == 0 and 256 % (C // 8) == 0
+
+
+class _BatchNormTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        dt = dcode(x)
+        nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        part = torch.empty(nblk * 2 * C, **f32)
+        stats = torch.empty(4, C, **f32)           # mean, invstd, scale, shift
+        call("ddl_bn_fwd_train", dt, p(x), M, C, p(weight), p(bias), p(running_mean), p(running_var),
+             float(momentum), float(eps), p(part), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
+        res = residual.contiguous() if residual is not None else None
+        y = torch.empty_like(x)
+        call("ddl_bn_apply", dt, p(x), p(res), p(stats[2]), p(stats[3]), p(y), x.numel(), C, int(relu))
+        ctx.relu = bool(relu)
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if relu else None, weight, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, stats = ctx.saved_tensors
+        dy = dy.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        part = torch.empty(nblk * 2 * C, **f32)
+        coef = torch.empty(3 * C, **f32)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        dgamma = torch.empty_like(weight) if weight is not None else None
+        dbeta = torch.empty_like(weight) if weight is not None else None
+        call("ddl_bn_bwd", dcode(x), p(dy), p(y), p(x), p(stats[0]), p(stats[1]), p(weight), M, C, int(ctx.relu),
+             p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres))
+        return dx, dgamma, dbeta, None, None, None, None, None, dres
+
+
+class _BatchNormEval(torch.autograd.Function):
+    """Inference BN: per-channel affine from running stats (+res)(ReLU), one pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, relu, residual):
+        x = x.contiguous()
+        C = x.shape[-1]
+        coeff = torch.empty(2, C, dtype=torch.float32, device=x.device)
+        call("ddl_bn_eval_coeffs", dcode(x), C, p(weight), p(bias), p(running_mean), p(running_var), float(eps),
+             p(coeff[0]), p(coeff[1]))
+        y = torch.empty_like(x)
+        res = residual.contiguous() if residual is not None else None
+        call("ddl_bn_apply", dcode(x), p(x), p(res), p(coeff[0]), p(coeff[1]), p(y), x.numel(), C, int(relu))
+        return y
+
+
+def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual):
+    from .norm import batch_norm_reference
+    C = x.shape[-1]
+    if not _bn_supported(C) or x.dtype not in (torch.bfloat16, torch.float32):
+        return batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu,
+                                    residual)
+    if weight is not None and weight.dtype != x.dtype:
+        weight, bias = weight.to(x.dtype), bias.to(x.dtype)
+    if training:
+        return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual)
+    if torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)):
+        # eval-mode BN with gradients (frozen-statistics fine-tuning): reference path
+        return batch_norm_reference(x, weight, bias, running_mean, running_var, False, momentum, eps, relu,
+                                    residual)
+    return _BatchNormEval.apply(x, weight, bias, running_mean, running_var, eps, relu, residual)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, residual):
+        x = x.contiguous()
+        H = x.shape[-1]
+        rows = x.numel() // H
+        res = residual.contiguous() if residual is not None else None
+        res_rows = res.numel() // H if res is not None else rows
+        stats = torch.empty(2, rows, dtype=torch.float32, device=x.device)
+        y = torch.empty_like(x)
+        call("ddl_ln_fwd", dcode(x), p(x), p(res), res_rows, p(weight), p(bias), p(y), p(stats[0]), p(stats[1]),
+             rows, H, float(eps))
+        ctx.res_shape = residual.shape if residual is not None else None
+        ctx.res_rows = res_rows
+        ctx.save_for_backward(x, res, weight, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, weight, stats = ctx.saved_tensors
+        dy = dy.contiguous()
+        H = x.shape[-1]
+        rows = x.numel() // H
+        nblk = _lib.fn("ddl_ln_bwd_nblk")(rows)
+        part = torch.empty(nblk * 2 * H, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        dg = torch.empty_like(weight)
+        db = torch.empty_like(weight)
+        call("ddl_ln_bwd", dcode(x), p(dy), p(x), p(res), ctx.res_rows, p(weight), p(stats[0]), p(stats[1]), p(dx),
+             p(part), p(dg), p(db), rows, H)
+        dres = None
+        if ctx.res_shape is not None:
+            if ctx.res_rows == rows:
+                dres = dx.view(ctx.res_shape)
+            else:
+                dres = dx.view(-1, ctx.res_rows, H).float().sum(0).to(dx.dtype).view(ctx.res_shape)
+        return dx, dg, db, None, dres
+
+
+def layer_norm(x, weight, bias, eps, residual: Optional[torch.Tensor] = None):
+    from .norm import layer_norm_reference
+    H = x.shape[-1]
+    ok = bool(_lib.fn("ddl_ln_supported")(H)) and x.dtype in (torch.bfloat16, torch.float32)
+    if residual is not None:
+        ok = ok and residual.dtype == x.dtype and residual.shape[-1] == H and \
+            (x.numel() // H) % max(1, residual.numel() // H) == 0
+        if ok and residual.numel() != x.numel():
+            # only leading-dimension broadcast ([1, S, H] against [B, S, H]) is supported
+            ok = residual.dim() == x.dim() and all(r in (1, s) for r, s in zip(residual.shape, x.shape)) and \
+                residual.shape[0] == 1 and tuple(residual.shape[1:]) == tuple(x.shape[1:])
+    if not ok:
+        return layer_norm_reference(x, weight, bias, eps, residual)
+    if weight.dtype != x.dtype:
+        weight, bias = weight.to(x.dtype), bias.to(x.dtype)
+    return _LayerNorm.apply(x, weight, bias, eps, residual)

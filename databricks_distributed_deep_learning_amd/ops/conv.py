@@ -1,0 +1,35 @@
+"""2-D convolution on NHWC activations with [Cout, KH, KW, Cin] weights.
+
+Kernel family K1/K2/K3.  The reference's ResNet-50 forward
+(``notebooks/cv/onnx_experiments.py:32,174``) runs these inside ATen/MIOpen; here
+the GPU path is an implicit-GEMM MFMA kernel (csrc/kernels/conv_igemm.hip):
+M = N·P·Q output pixels, N_gemm = Cout, K = KH·KW·Cin gathered on the fly.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def conv2d_reference(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0) -> torch.Tensor:
+    """Plain PyTorch NHWC convolution (CPU oracle / native=off path)."""
+    xn = x.permute(0, 3, 1, 2)
+    wn = w.permute(0, 3, 1, 2)
+    if x.is_cuda:
+        xn = xn.contiguous(memory_format=torch.channels_last)
+        wn = wn.contiguous(memory_format=torch.channels_last)
+    y = F.conv2d(xn, wn, stride=stride, padding=padding)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0) -> torch.Tensor:
+    if _lib.use_native(x):
+        from . import _native_conv
+        return _native_conv.conv2d(x, w, stride, padding)
+    return conv2d_reference(x, w, stride, padding)
+
+
+def out_hw(h: int, w: int, k: int, stride: int, padding: int):
+    return (h + 2 * padding - k) // stride + 1, (w + 2 * padding - k) // stride + 1

@@ -1,0 +1,48 @@
+"""Dense layer with fused bias + activation epilogue (kernel families K9/K13/K17).
+
+``y = act(x @ W^T + b)`` with W in [out, in] (PyTorch / HF layout).  On MI355X
+the GEMM runs on MFMA (csrc/kernels/gemm.hip) with bias and GELU/ReLU/tanh
+applied in the epilogue from the fp32 accumulator — no extra pass over the
+[tokens, 3072] FFN activation.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+ACTS = (None, "gelu", "relu", "tanh")
+
+
+def _act(y: torch.Tensor, act: Optional[str]) -> torch.Tensor:
+    if act is None:
+        return y
+    if act == "gelu":
+        return F.gelu(y)
+    if act == "relu":
+        return torch.relu(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    raise ValueError(act)
+
+
+def linear_reference(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+                     act: Optional[str] = None) -> torch.Tensor:
+    if x.is_cuda or x.dtype == torch.float32:
+        y = F.linear(x, w, b)
+        return _act(y, act)
+    y = F.linear(x.float(), w.float(), b.float() if b is not None else None)
+    return _act(y, act).to(x.dtype)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+           act: Optional[str] = None) -> torch.Tensor:
+    if act not in ACTS:
+        raise ValueError(f"act must be one of {ACTS}")
+    if _lib.use_native(x):
+        from . import _native_linear
+        return _native_linear.linear(x, w, b, act)
+    return linear_reference(x, w, b, act)

@@ -1,0 +1,60 @@
+"""BatchNorm (+ReLU, +residual add) over NHWC and LayerNorm (+residual add).
+
+Kernel families K4/K5/K6 (BN statistics, fused apply+act, fused backward) and
+K16 (LayerNorm fwd/bwd) — SURVEY §2.3.  BatchNorm normalises over every axis but
+the last (channels innermost), LayerNorm over the last axis only.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+# ----------------------------------------------------------------- BatchNorm
+def batch_norm_reference(x, weight, bias, running_mean, running_var, training: bool,
+                         momentum: float = 0.1, eps: float = 1e-5, relu: bool = False,
+                         residual: Optional[torch.Tensor] = None):
+    C = x.shape[-1]
+    xf = x.reshape(-1, C)
+    if training:
+        y = F.batch_norm(xf.float(), running_mean, running_var, weight.float() if weight is not None else None,
+                         bias.float() if bias is not None else None, True, momentum, eps)
+    else:
+        y = F.batch_norm(xf.float(), running_mean, running_var, weight.float() if weight is not None else None,
+                         bias.float() if bias is not None else None, False, momentum, eps)
+    y = y.view_as(x)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def batch_norm(x, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
+               eps: float = 1e-5, relu: bool = False, residual: Optional[torch.Tensor] = None):
+    if _lib.use_native(x):
+        from . import _native_norm
+        return _native_norm.batch_norm(x, weight, bias, running_mean, running_var, training,
+                                       momentum, eps, relu, residual)
+    return batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps,
+                                relu, residual)
+
+
+# ----------------------------------------------------------------- LayerNorm
+def layer_norm_reference(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Tensor] = None):
+    h = x if residual is None else x + residual
+    y = F.layer_norm(h.float(), (h.shape[-1],), weight.float() if weight is not None else None,
+                     bias.float() if bias is not None else None, eps)
+    return y.to(x.dtype)
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Tensor] = None):
+    """``LayerNorm(x + residual)`` over the last axis; fp32 statistics."""
+    if _lib.use_native(x):
+        from . import _native_norm
+        return _native_norm.layer_norm(x, weight, bias, eps, residual)
+    return layer_norm_reference(x, weight, bias, eps, residual)

@@ -1,0 +1,207 @@
+"""Bucketed data-parallel gradient reducer over RCCL (north-star N6 / N7).
+
+Design (MI355X-first, not a DDP re-implementation):
+
+* gradients already live in one flat arena (``optim.arena.ParamArena``) ordered
+  in reverse registration order, so a *bucket* is just a contiguous slice of it:
+  no flatten/unflatten copies, and the all-reduce payload is the gradient
+  memory itself;
+* bucket boundaries: a small first bucket (``first_bucket_mb``, default 4 MB) so
+  the first RCCL ring starts while most of backward is still running, then
+  large buckets (``bucket_mb``, default 64 MB) — an 8-GPU xGMI ring is
+  per-link bound (~153 GB/s/link, 7 links), so few large messages that let RCCL
+  spread channels over all links beat many small latency-bound ones;
+* readiness: ``register_post_accumulate_grad_hook`` per parameter counts down a
+  bucket; the last gradient of a bucket launches an async all-reduce, which
+  ProcessGroupNCCL (RCCL) runs on its own HIP stream ordered after the
+  producing kernels — comm overlaps the rest of backward;
+* ``no_sync()`` for gradient accumulation (BASELINE.json:11): micro-steps skip
+  communication; with ``accumulate_fp32`` the micro-step gradients are summed
+  into an fp32 arena so bf16 accumulation error does not grow with grad_accum;
+* the 1/world average is folded into the optimizer (``grad_scale``) instead of
+  an extra pass over the buckets.
+"""
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import dist as ddist
+from ..optim.arena import ParamArena
+
+
+@dataclass
+class Bucket:
+    index: int
+    start: int
+    end: int
+    entry_ids: List[int]
+    pending: int = 0
+    handle: Optional[object] = None
+    launched: bool = False
+    payload: Optional[torch.Tensor] = None
+    grads_seen: set = field(default_factory=set)
+
+
+class DataParallel(nn.Module):
+    """Wrap ``module`` for data-parallel training.
+
+    ``arena`` may be supplied (shared with a flat optimizer); otherwise one is
+    created.  After ``loss.backward()`` call :meth:`finish` (or use the
+    optimizer's ``step(reducer=...)``), which waits on every in-flight bucket.
+    """
+
+    def __init__(self, module: nn.Module, arena: Optional[ParamArena] = None,
+                 bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
+                 reduce_dtype: Optional[torch.dtype] = None, broadcast_buffers: bool = False,
+                 accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True):
+        super().__init__()
+        self.module = module
+        self.arena = arena if arena is not None else ParamArena(list(module.named_parameters()))
+        self.pg = process_group
+        self.world = ddist.world_size()
+        self.broadcast_buffers = broadcast_buffers
+        self.reduce_dtype = reduce_dtype or self.arena.dtype
+        self.accumulate_fp32 = accumulate_fp32
+        self._sync = True
+        self._acc32: Optional[torch.Tensor] = None
+        self._acc_active = False
+        if broadcast_init and self.world > 1:
+            ddist.broadcast_tensors([self.arena.flat] + [b for b in module.buffers()])
+        self.buckets = self._build_buckets(bucket_mb, first_bucket_mb)
+        self._entry_bucket = {}
+        for b in self.buckets:
+            for ei in b.entry_ids:
+                self._entry_bucket[ei] = b.index
+        self._hooks = []
+        for ei, e in enumerate(self.arena.entries):
+            self._hooks.append(e.param.register_post_accumulate_grad_hook(self._make_hook(ei)))
+        self._reset()
+
+    # ------------------------------------------------------------------
+    def _build_buckets(self, bucket_mb: float, first_bucket_mb: float) -> List[Bucket]:
+        esz = torch.empty((), dtype=self.reduce_dtype).element_size()
+        buckets: List[Bucket] = []
+        cap = int(first_bucket_mb * (1 << 20)) // esz
+        cur: List[int] = []
+        start = 0
+        for ei, e in enumerate(self.arena.entries):
+            end = e.offset + e.numel
+            cur.append(ei)
+            if end - start >= cap:
+                nxt = self.arena.entries[ei + 1].offset if ei + 1 < len(self.arena.entries) else self.arena.numel
+                buckets.append(Bucket(len(buckets), start, nxt, cur))
+                cur, start = [], nxt
+                cap = int(bucket_mb * (1 << 20)) // esz
+        if cur:
+            buckets.append(Bucket(len(buckets), start, self.arena.numel, cur))
+        return buckets
+
+    def _reset(self) -> None:
+        for b in self.buckets:
+            b.pending = len(b.entry_ids)
+            b.handle = None
+            b.launched = False
+            b.payload = None
+            b.grads_seen = set()
+
+    def _make_hook(self, ei: int):
+        def hook(_p):
+            if not self._sync:
+                return
+            b = self.buckets[self._entry_bucket[ei]]
+            if ei in b.grads_seen:   # parameter used twice in one graph: count once
+                return
+            b.grads_seen.add(ei)
+            b.pending -= 1
+            if b.pending == 0:
+                self._launch(b)
+        return hook
+
+    def _payload(self, b: Bucket) -> torch.Tensor:
+        g = self.arena.grad[b.start:b.end]
+        if self._acc_active:
+            acc = self._acc32[b.start:b.end]
+            acc.add_(g)
+            return acc
+        if self.reduce_dtype != g.dtype:
+            return g.to(self.reduce_dtype)
+        return g
+
+    def _launch(self, b: Bucket) -> None:
+        if b.launched:
+            return
+        b.launched = True
+        b.payload = self._payload(b)
+        if self.world > 1:
+            b.handle = dist.all_reduce(b.payload, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    # ------------------------------------------------------------------
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Skip gradient communication inside (micro-steps of grad accumulation)."""
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
+            if self.accumulate_fp32:
+                # drain this micro-step's bf16 grads into the fp32 accumulator
+                if self._acc32 is None:
+                    self._acc32 = torch.zeros(self.arena.numel, dtype=torch.float32, device=self.arena.device)
+                self._acc32.add_(self.arena.grad)
+                self.arena.grad.zero_()
+                self._acc_active = True
+
+    def finish(self) -> torch.Tensor:
+        """Wait for all buckets; return the flat reduced gradient (SUM over ranks).
+
+        The caller scales by ``1/world`` (optimizers take ``grad_scale``).
+        """
+        for b in self.buckets:
+            if not b.launched:
+                self._launch(b)
+        for b in self.buckets:
+            if b.handle is not None:
+                b.handle.wait()
+        if self._acc_active:
+            out = self._acc32
+        elif self.reduce_dtype != self.arena.dtype:
+            out = torch.empty(self.arena.numel, dtype=self.reduce_dtype, device=self.arena.device)
+            for b in self.buckets:
+                out[b.start:b.end].copy_(b.payload)
+        else:
+            out = self.arena.grad
+        self._reset()
+        if self.broadcast_buffers and self.world > 1:
+            ddist.broadcast_tensors(list(self.module.buffers()))
+        return out
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        self.arena.zero_grad()
+        if self._acc32 is not None:
+            self._acc32.zero_()
+        self._acc_active = False
+
+    def bucket_sizes_mb(self) -> List[float]:
+        esz = torch.empty((), dtype=self.reduce_dtype).element_size()
+        return [(b.end - b.start) * esz / (1 << 20) for b in self.buckets]
+
+    def state_dict(self, *a, **k):
+        return self.module.state_dict(*a, **k)
+
+    def load_state_dict(self, *a, **k):
+        return self.module.load_state_dict(*a, **k)

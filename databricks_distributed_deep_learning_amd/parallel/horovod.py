@@ -1,0 +1,177 @@
+"""HorovodRunner-compatible shim + a tiny ``hvd``-style facade (north-star N2).
+
+``HorovodRunner(np=8).run(main, **kwargs)`` mirrors the public
+``sparkdl.HorovodRunner`` surface; negative ``np`` (Databricks' "run locally on
+the driver with |np| processes") is treated the same as positive on one node.
+The facade (``init/rank/size/local_rank/allreduce/allgather/broadcast/
+broadcast_parameters/broadcast_optimizer_state/DistributedOptimizer``) is backed
+by ``torch.distributed`` over RCCL and by :class:`..parallel.ddp.DataParallel`'s
+bucketed reducer, so Horovod-style training scripts run unchanged in structure.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import dist as ddist
+from .launcher import Distributor
+
+Average = "average"
+Sum = "sum"
+Adasum = "adasum"  # accepted for API compatibility; implemented as Average
+
+
+class HorovodRunner:
+    def __init__(self, np: int = -1, driver_log_verbosity: str = "log_callback_only", use_gpu: Optional[bool] = None):
+        self.num_processes = abs(int(np)) or 1
+        self.driver_log_verbosity = driver_log_verbosity
+        self.use_gpu = use_gpu
+
+    def run(self, main: Callable, **kwargs) -> Any:
+        return Distributor(self.num_processes, local_mode=True, use_gpu=self.use_gpu).run(main, **kwargs)
+
+
+# ---------------------------------------------------------------- facade
+def init(backend: str = "auto") -> None:
+    ddist.init(backend=backend)
+
+
+def rank() -> int:
+    return ddist.rank()
+
+
+def size() -> int:
+    return ddist.world_size()
+
+
+def local_rank() -> int:
+    return ddist.local_rank()
+
+
+def local_size() -> int:
+    import os
+    return int(os.environ.get("LOCAL_WORLD_SIZE", size()))
+
+
+def _prep(t: torch.Tensor):
+    if ddist.is_initialized() and dist.get_backend() == "nccl" and not t.is_cuda:
+        return t.cuda(), True
+    return t, False
+
+
+def allreduce(tensor: torch.Tensor, average: Optional[bool] = None, name: Optional[str] = None,
+              op: str = Average) -> torch.Tensor:
+    if average is not None:
+        op = Average if average else Sum
+    out = tensor.detach().clone()
+    if size() == 1:
+        return out
+    t, moved = _prep(out)
+    dist.all_reduce(t)
+    if op in (Average, Adasum):
+        t.div_(size())
+    return t.to(tensor.device) if moved else t
+
+
+def allreduce_(tensor: torch.Tensor, average: Optional[bool] = None, name: Optional[str] = None,
+               op: str = Average) -> torch.Tensor:
+    tensor.copy_(allreduce(tensor, average=average, op=op))
+    return tensor
+
+
+def allgather(tensor: torch.Tensor, name: Optional[str] = None) -> torch.Tensor:
+    """Concatenate along dim 0 (Horovod semantics; equal first dims)."""
+    if size() == 1:
+        return tensor.detach().clone()
+    t, moved = _prep(tensor.detach().contiguous())
+    outs = [torch.empty_like(t) for _ in range(size())]
+    dist.all_gather(outs, t)
+    r = torch.cat(outs, 0)
+    return r.to(tensor.device) if moved else r
+
+
+def broadcast(tensor: torch.Tensor, root_rank: int = 0, name: Optional[str] = None) -> torch.Tensor:
+    out = tensor.detach().clone()
+    if size() == 1:
+        return out
+    t, moved = _prep(out)
+    dist.broadcast(t, src=root_rank)
+    return t.to(tensor.device) if moved else t
+
+
+def broadcast_(tensor: torch.Tensor, root_rank: int = 0, name: Optional[str] = None) -> torch.Tensor:
+    tensor.copy_(broadcast(tensor, root_rank))
+    return tensor
+
+
+def broadcast_parameters(params, root_rank: int = 0) -> None:
+    if isinstance(params, dict):
+        tensors = list(params.values())
+    else:
+        tensors = [p for _, p in params] if params and isinstance(next(iter(params)), tuple) else list(params)
+    with torch.no_grad():
+        ddist.broadcast_tensors([t.data if hasattr(t, "data") else t for t in tensors], src=root_rank)
+
+
+def broadcast_object(obj: Any, root_rank: int = 0) -> Any:
+    return ddist.broadcast_object(obj, src=root_rank)
+
+
+def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
+    sd = optimizer.state_dict()
+    sd = ddist.broadcast_object(sd, src=root_rank)
+    optimizer.load_state_dict(sd)
+
+
+class _DistributedOptimizer:
+    """Wraps a torch optimizer: averages gradients across ranks before ``step``.
+
+    Communication is bucketed and overlapped with backward through the same
+    hook-driven reducer as :class:`DataParallel` (grads are views into one flat
+    arena, all-reduced slice by slice as they become ready).
+    """
+
+    def __init__(self, optimizer: torch.optim.Optimizer, named_parameters: Optional[Iterable] = None,
+                 backward_passes_per_step: int = 1, op: str = Average, bucket_mb: float = 64.0):
+        from .ddp import DataParallel
+        from ..optim.arena import ParamArena
+        self.optimizer = optimizer
+        if named_parameters is None:
+            named_parameters = [(f"p{i}", p) for g in optimizer.param_groups for i, p in enumerate(g["params"])]
+        self.arena = ParamArena(list(named_parameters))
+
+        class _Holder(torch.nn.Module):
+            pass
+        self._reducer = DataParallel(_Holder(), arena=self.arena, bucket_mb=bucket_mb, broadcast_init=False)
+        self.backward_passes_per_step = backward_passes_per_step
+        self.op = op
+        self._passes = 0
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        self._reducer.zero_grad()
+
+    def synchronize(self) -> None:
+        self._reducer.finish()
+        if self.op in (Average, Adasum) and size() > 1:
+            self.arena.grad.mul_(1.0 / size())
+
+    def step(self, closure=None):
+        self.synchronize()
+        return self.optimizer.step(closure)
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def load_state_dict(self, sd):
+        return self.optimizer.load_state_dict(sd)
+
+
+def DistributedOptimizer(optimizer, named_parameters=None, backward_passes_per_step: int = 1,
+                         op: str = Average, **kw) -> _DistributedOptimizer:
+    return _DistributedOptimizer(optimizer, named_parameters, backward_passes_per_step, op, **kw)

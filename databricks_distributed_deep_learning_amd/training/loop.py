@@ -1,0 +1,203 @@
+"""Notebook-style ``train(cfg)`` for CV and NLP (north-star N4).
+
+The same function runs in a notebook cell (world 1, no launcher), under
+``Distributor(8).run(train, cfg)`` / ``HorovodRunner(8).run(train, cfg=cfg)``,
+and under ``torchrun``.  Per rank:
+
+    model (random init, bf16 params) -> flat ParamArena -> DataParallel reducer
+    -> flat optimizer (fp32 master) -> synthetic device-resident loader
+    for step: [micro-steps under no_sync] fwd, bwd (bucketed RCCL all-reduce
+              overlapped with backward) -> finish() -> fused optimizer step
+
+Returns a summary dict (rank-aggregated throughput, final loss, config).
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+import time
+from typing import Any, Callable, Dict, Optional
+
+import torch
+
+from .. import ops
+from ..config import TrainConfig, apply_overrides
+from ..data import SyntheticImageNet, SyntheticTokens
+from ..models import build_model, cast_params, count_params
+from ..optim import LRSchedule, ParamArena, build_optimizer
+from ..parallel import dist as ddist
+from ..parallel.ddp import DataParallel
+from ..utils import checkpoint as ckpt
+from ..utils.faults import maybe_fail
+from ..utils.metrics import JsonlLogger, StepTimer, ThroughputMeter, memory_stats
+
+DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
+
+
+class Trainer:
+    """Holds the per-rank training state; ``train()`` is the notebook-facing wrapper."""
+
+    def __init__(self, cfg: TrainConfig):
+        self.cfg = cfg
+        ddist.init(cfg.backend)
+        self.device = ddist.device()
+        if cfg.native != "auto":
+            ops.set_native_mode("off" if cfg.native == "off" else "auto")
+        self.rank, self.world = ddist.rank(), ddist.world_size()
+        self.dtype = DTYPES[cfg.dtype]
+        self.task = cfg.resolved_task
+        torch.manual_seed(cfg.seed)
+        model = build_model(cfg.model, num_classes=cfg.num_classes, dropout=cfg.dropout,
+                            image_size=cfg.image_size)
+        model = model.to(self.device)
+        cast_params(model, self.dtype)
+        self.model = model
+        self.n_params = count_params(model)
+        self.arena = ParamArena(list(model.named_parameters()))
+        accumulate_fp32 = cfg.grad_accum > 1 and self.dtype != torch.float32
+        rd = {"auto": None, "fp32": torch.float32, "bf16": torch.bfloat16}[cfg.grad_reduce_dtype]
+        self.ddp = DataParallel(model, self.arena, bucket_mb=cfg.bucket_mb, first_bucket_mb=cfg.first_bucket_mb,
+                                reduce_dtype=rd, broadcast_buffers=cfg.broadcast_buffers,
+                                accumulate_fp32=accumulate_fp32)
+        self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg)
+        self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
+        if cfg.batch_size <= 0:
+            cfg.batch_size = self._auto_batch()
+        self.loader = self._make_loader()
+        self.step = 0
+        self.logger = JsonlLogger(cfg.log_file, enabled=ddist.is_main())
+        if cfg.resume and cfg.checkpoint_dir and ckpt.latest(cfg.checkpoint_dir):
+            meta = ckpt.load(cfg.checkpoint_dir, model, self.opt)
+            self.step = int(meta["step"])
+
+    # ------------------------------------------------------------------
+    def _make_loader(self):
+        c = self.cfg
+        if self.task == "cv":
+            return SyntheticImageNet(c.batch_size, c.image_size, c.num_classes, self.device, self.dtype,
+                                     rank=self.rank, seed=c.seed, pool=c.synthetic_pool)
+        return SyntheticTokens(c.batch_size, c.seq_len, c.vocab_size, c.num_classes, self.device,
+                               rank=self.rank, seed=c.seed, pool=c.synthetic_pool)
+
+    def _auto_batch(self) -> int:
+        from ..utils.memory import fit_batch_size
+        c = self.cfg
+
+        def probe(b):
+            old = c.batch_size
+            c.batch_size = b
+            ld = self._make_loader()
+            self.ddp.zero_grad()
+            with self.ddp.no_sync():
+                loss = self.loss_fn(ld.next())
+                loss.backward()
+            self.ddp.zero_grad()
+            c.batch_size = old
+        return fit_batch_size(probe, self.device, start=8)
+
+    def loss_fn(self, batch) -> torch.Tensor:
+        if self.task == "cv":
+            x, y = batch
+            return ops.cross_entropy(self.model(x), y)
+        loss, _ = self.model(batch["input_ids"], batch.get("attention_mask"), None, batch["labels"])
+        return loss
+
+    def train_step(self) -> torch.Tensor:
+        c = self.cfg
+        self.ddp.zero_grad()
+        loss_sum = None
+        for micro in range(c.grad_accum):
+            batch = self.loader.next()
+            ctx = self.ddp.no_sync() if micro < c.grad_accum - 1 else contextlib.nullcontext()
+            with ctx:
+                loss = self.loss_fn(batch)
+                loss.backward()
+            loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+        grad = self.ddp.finish()
+        self.opt.step(grad, grad_scale=1.0 / (self.world * c.grad_accum), lr=self.sched(self.step))
+        self.step += 1
+        return loss_sum / c.grad_accum
+
+    @property
+    def samples_per_step(self) -> int:
+        return self.cfg.batch_size * self.cfg.grad_accum * self.world
+
+    def run(self, steps: Optional[int] = None, warmup: Optional[int] = None,
+            callback: Optional[Callable[[int, float], None]] = None) -> Dict[str, Any]:
+        c = self.cfg
+        steps = c.steps if steps is None else steps
+        warmup = c.warmup_steps if warmup is None else warmup
+        self.model.train()
+        for _ in range(warmup):
+            self.train_step()
+        timer = StepTimer(self.device)
+        meter = ThroughputMeter(self.samples_per_step)
+        ddist.barrier()
+        timer.start()
+        t_seg = 0.0
+        last_loss = float("nan")
+        seg_steps = 0
+        for i in range(steps):
+            maybe_fail(self.step, c.fault_rank, c.fault_step)
+            loss = self.train_step()
+            seg_steps += 1
+            if c.log_every and (i + 1) % c.log_every == 0 or i == steps - 1:
+                last_loss = float(loss)          # device sync only at log points
+                if callback:
+                    callback(self.step, last_loss)
+                self.logger.log({"step": self.step, "loss": last_loss, "lr": self.opt.lr,
+                                 **memory_stats(self.device)})
+            if c.checkpoint_every and c.checkpoint_dir and self.step % c.checkpoint_every == 0:
+                t_pause = timer.stop()
+                t_seg += t_pause
+                ckpt.save(c.checkpoint_dir, self.model, self.opt, self.step, c.to_dict())
+                timer.start()
+        ddist.barrier()
+        t_seg += timer.stop()
+        meter.update(t_seg, steps)
+        t_max = ddist.all_reduce_scalars([t_seg], op="max")[0]
+        summary = {
+            "model": c.model, "task": self.task, "world_size": self.world, "steps": steps, "warmup": warmup,
+            "per_rank_batch": c.batch_size, "grad_accum": c.grad_accum, "global_batch": self.samples_per_step,
+            "seq_len": c.seq_len if self.task == "nlp" else None, "dtype": c.dtype,
+            "optimizer": c.resolved_optimizer, "params": self.n_params,
+            "seconds": t_max, "ms_per_step": 1000.0 * t_max / max(1, steps),
+            "samples_per_sec": self.samples_per_step * steps / t_max if t_max > 0 else 0.0,
+            "final_loss": last_loss, "native": ops.native_mode(),
+            "buckets_mb": [round(b, 2) for b in self.ddp.bucket_sizes_mb()],
+        }
+        summary.update(memory_stats(self.device))
+        if c.checkpoint_dir and not c.checkpoint_every:
+            ckpt.save(c.checkpoint_dir, self.model, self.opt, self.step, c.to_dict())
+        return summary
+
+
+def train(cfg: Optional[TrainConfig] = None, **overrides) -> Dict[str, Any]:
+    """Notebook-style entry point.  ``train(get_preset("resnet50_ddp"), steps=20)``."""
+    cfg = (cfg or TrainConfig()).replace(**overrides) if overrides else (cfg or TrainConfig())
+    trainer = Trainer(cfg)
+    return trainer.run()
+
+
+def main(argv=None) -> int:
+    """CLI: ``python -m databricks_distributed_deep_learning_amd.training.loop --preset resnet50_ddp --steps 20``."""
+    import json
+    import sys
+    from ..config import get_preset
+    argv = list(sys.argv[1:] if argv is None else argv)
+    preset = "resnet50_ddp"
+    if "--preset" in argv:
+        i = argv.index("--preset")
+        preset = argv[i + 1]
+        del argv[i:i + 2]
+    cfg = apply_overrides(get_preset(preset), argv)
+    out = train(cfg)
+    if ddist.is_main():
+        print(json.dumps(out))
+    ddist.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

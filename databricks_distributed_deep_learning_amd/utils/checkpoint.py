@@ -1,0 +1,72 @@
+"""Checkpoint / resume.
+
+The reference only *saves* — a whole-module pickle (``torch.save(resnet50, ...)``,
+``notebooks/cv/onnx_experiments.py:198``) and a TorchScript trace (:215) — with
+no optimizer state and no load path.  Here a checkpoint is a directory:
+
+* ``model.safetensors``  - weights (no pickle: loading executes nothing)
+* ``optim.safetensors``  - flat optimizer state (fp32 master, moments)
+* ``meta.json``          - step, config, optimizer scalars, RNG seeds
+
+Rank 0 writes, every rank barriers, every rank loads (collective C5).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..parallel import dist as ddist
+
+
+def _cpu(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    return {k: v.detach().to("cpu").contiguous() for k, v in sd.items() if isinstance(v, torch.Tensor)}
+
+
+def save(path: str, model: torch.nn.Module, optimizer=None, step: int = 0, config: Optional[Dict] = None,
+         extra: Optional[Dict[str, Any]] = None) -> None:
+    from safetensors.torch import save_file
+    if ddist.is_main():
+        os.makedirs(path, exist_ok=True)
+        msd = model.state_dict()
+        # safetensors refuses shared storage; clone so views of the arena are independent
+        save_file({k: v.clone() for k, v in _cpu(msd).items()}, os.path.join(path, "model.safetensors"))
+        meta: Dict[str, Any] = {"step": step, "config": config or {}, "extra": extra or {}}
+        if optimizer is not None:
+            st = optimizer.state_dict()
+            tensors = {k: v for k, v in st.items() if isinstance(v, torch.Tensor)}
+            scalars = {k: v for k, v in st.items() if not isinstance(v, torch.Tensor)}
+            save_file(_cpu(tensors), os.path.join(path, "optim.safetensors"))
+            meta["optimizer"] = scalars
+        meta["rng"] = {"torch": int(torch.initial_seed())}
+        tmp = os.path.join(path, "meta.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True, default=str)
+        os.replace(tmp, os.path.join(path, "meta.json"))
+    ddist.barrier()
+
+
+def load(path: str, model: torch.nn.Module, optimizer=None, map_location=None) -> Dict[str, Any]:
+    from safetensors.torch import load_file
+    ddist.barrier()
+    with open(os.path.join(path, "meta.json")) as f:
+        meta = json.load(f)
+    dev = map_location or next(model.parameters()).device
+    msd = load_file(os.path.join(path, "model.safetensors"), device="cpu")
+    own = model.state_dict()
+    with torch.no_grad():
+        for k, v in msd.items():
+            if k in own:
+                own[k].copy_(v.to(own[k].dtype))
+    if optimizer is not None and os.path.exists(os.path.join(path, "optim.safetensors")):
+        ost = load_file(os.path.join(path, "optim.safetensors"), device="cpu")
+        st = dict(meta.get("optimizer", {}))
+        st.update({k: v.to(dev) for k, v in ost.items()})
+        optimizer.load_state_dict(st)
+    return meta
+
+
+def latest(path: str) -> Optional[str]:
+    return path if os.path.exists(os.path.join(path, "meta.json")) else None

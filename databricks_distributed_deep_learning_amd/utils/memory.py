@@ -1,0 +1,49 @@
+"""HBM-aware batch sizing (north-star N13, BASELINE.json:11 "288 GB HBM batch sizing").
+
+``fit_batch_size`` probes: run one fwd+bwd at a candidate micro-batch, read the
+peak allocation, extrapolate linearly (activation memory is linear in batch),
+and back off on OOM, keeping ``headroom`` of the device free.  Everything is
+sized for one MI355X's 288 GB.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+
+def fit_batch_size(step_fn: Callable[[int], None], device: torch.device, start: int = 8,
+                   max_batch: int = 4096, headroom: float = 0.15, multiple: int = 8) -> int:
+    if device.type != "cuda":
+        return start
+    total = torch.cuda.get_device_properties(device).total_memory
+    budget = total * (1.0 - headroom)
+
+    def peak_at(b: int) -> float:
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(device)
+        base = torch.cuda.memory_allocated(device)
+        step_fn(b)
+        torch.cuda.synchronize(device)
+        return torch.cuda.max_memory_allocated(device) - base
+
+    b0 = start
+    while True:
+        try:
+            p0 = peak_at(b0)
+            break
+        except torch.cuda.OutOfMemoryError:
+            b0 //= 2
+            if b0 < 1:
+                raise
+    static = torch.cuda.memory_allocated(device)
+    per_sample = p0 / b0
+    est = int((budget - static) / max(per_sample, 1.0))
+    est = max(b0, min(max_batch, est // multiple * multiple))
+    while est > b0:
+        try:
+            peak_at(est)
+            return est
+        except torch.cuda.OutOfMemoryError:
+            est = max(b0, int(est * 0.8) // multiple * multiple)
+    return b0

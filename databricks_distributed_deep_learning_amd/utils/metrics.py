@@ -1,0 +1,98 @@
+"""Throughput meter, device timers and rank-0 JSONL metrics.
+
+The reference times one sample with ``time.time()`` and no warm-up or device
+sync (``notebooks/cv/onnx_experiments.py:92-104,133-140``); here timing is
+bracketed by device synchronisation, warm-up is excluded, and results are
+aggregated across ranks.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, Optional
+
+import torch
+
+
+def sync(device: Optional[torch.device] = None) -> None:
+    if device is not None and device.type == "cuda":
+        torch.cuda.synchronize(device)
+    elif device is None and torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+class StepTimer:
+    """Host wall clock bracketed by device synchronisation."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.t0 = 0.0
+
+    def start(self) -> None:
+        sync(self.device)
+        self.t0 = time.perf_counter()
+
+    def stop(self) -> float:
+        sync(self.device)
+        return time.perf_counter() - self.t0
+
+
+class EventTimer:
+    """HIP-event timer for a region on the current stream (no host sync inside)."""
+
+    def __init__(self):
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.b = torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        self.a.record()
+        return self
+
+    def __exit__(self, *exc):
+        self.b.record()
+
+    def ms(self) -> float:
+        self.b.synchronize()
+        return self.a.elapsed_time(self.b)
+
+
+class ThroughputMeter:
+    def __init__(self, items_per_step: int):
+        self.items_per_step = items_per_step
+        self.steps = 0
+        self.seconds = 0.0
+
+    def update(self, seconds: float, steps: int = 1) -> None:
+        self.steps += steps
+        self.seconds += seconds
+
+    @property
+    def items_per_sec(self) -> float:
+        return self.items_per_step * self.steps / self.seconds if self.seconds > 0 else 0.0
+
+    @property
+    def ms_per_step(self) -> float:
+        return 1000.0 * self.seconds / self.steps if self.steps else 0.0
+
+
+class JsonlLogger:
+    def __init__(self, path: str = "", enabled: bool = True):
+        self.path = path
+        self.enabled = enabled and bool(path)
+        if self.enabled:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+
+    def log(self, record: Dict) -> None:
+        if not self.enabled:
+            return
+        record = dict(record, ts=time.time())
+        with open(self.path, "a") as f:
+            f.write(json.dumps(record) + "\n")
+
+
+def memory_stats(device: torch.device) -> Dict[str, float]:
+    if device.type != "cuda":
+        return {}
+    return {"mem_alloc_gb": torch.cuda.memory_allocated(device) / 2**30,
+            "mem_peak_gb": torch.cuda.max_memory_allocated(device) / 2**30}

@@ -1,0 +1,156 @@
+"""Distributed plumbing on CPU / gloo, world_size 2 (BASELINE.json:7)."""
+import os
+
+import pytest
+import torch
+
+from databricks_distributed_deep_learning_amd.parallel import ChildFailed, Distributor, HorovodRunner
+
+
+# ---------------------------------------------------------------- helpers run in children
+def _rank_info(tag):
+    import torch.distributed as dist
+    t = torch.tensor([dist.get_rank() + 1.0])
+    dist.all_reduce(t)
+    return {"tag": tag, "rank": dist.get_rank(), "world": dist.get_world_size(), "sum": t.item()}
+
+
+def _fail_on_rank1():
+    import torch.distributed as dist
+    if dist.get_rank() == 1:
+        raise ValueError("boom from rank 1")
+    dist.barrier()
+    return "unreachable"
+
+
+def _tiny_model():
+    torch.manual_seed(11)
+    return torch.nn.Sequential(torch.nn.Linear(10, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+
+
+def _data(n=8):
+    g = torch.Generator().manual_seed(5)
+    return torch.randn(n, 10, generator=g), torch.randint(0, 3, (n,), generator=g)
+
+
+def _ddp_equivalence(accum):
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.optim import FlatSGD, ParamArena
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    rank, world = dist.get_rank(), dist.get_world_size()
+    x, y = _data(8 * accum)
+    # reference: one process, full batch
+    ref = _tiny_model()
+    loss = torch.nn.functional.cross_entropy(ref(x), y)
+    loss.backward()
+    with torch.no_grad():
+        for p in ref.parameters():
+            p -= 0.1 * p.grad
+    # DP: each rank gets its shard, split further into `accum` micro-batches
+    m = _tiny_model()
+    arena = ParamArena(list(m.named_parameters()))
+    ddp = DataParallel(m, arena, bucket_mb=0.0005, first_bucket_mb=0.0002)
+    opt = FlatSGD(arena, lr=0.1, momentum=0.0)
+    xs, ys = x[rank::world], y[rank::world]
+    ddp.zero_grad()
+    for i in range(accum):
+        xm, ym = xs[i::accum], ys[i::accum]
+        ctx = ddp.no_sync() if i < accum - 1 else torch.enable_grad()
+        with ctx:
+            torch.nn.functional.cross_entropy(ddp(xm), ym).backward()
+    g = ddp.finish()
+    opt.step(g, grad_scale=1.0 / (world * accum))
+    err = max((a - b).abs().max().item() for a, b in zip(m.parameters(), ref.parameters()))
+    return {"err": err, "nbuckets": len(ddp.buckets)}
+
+
+def _hvd_equivalence():
+    from databricks_distributed_deep_learning_amd.parallel import hvd
+    hvd.init()
+    x, y = _data(8)
+    ref = _tiny_model()
+    torch.nn.functional.cross_entropy(ref(x), y).backward()
+    with torch.no_grad():
+        for p in ref.parameters():
+            p -= 0.1 * p.grad
+    m = _tiny_model()
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), named_parameters=m.named_parameters())
+    hvd.broadcast_parameters(m.state_dict(), root_rank=0)
+    opt.zero_grad()
+    r, w = hvd.rank(), hvd.size()
+    torch.nn.functional.cross_entropy(m(x[r::w]), y[r::w]).backward()
+    opt.step()
+    err = max((a - b).abs().max().item() for a, b in zip(m.parameters(), ref.parameters()))
+    ar = hvd.allreduce(torch.tensor([float(r)]), average=True)
+    ag = hvd.allgather(torch.tensor([[float(r)]]))
+    bc = hvd.broadcast(torch.tensor([float(r + 5)]), root_rank=1)
+    return {"err": err, "avg": ar.item(), "gather": ag.flatten().tolist(), "bcast": bc.item()}
+
+
+def _train_resnet18_gloo(tmpdir):
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    cfg = get_preset("resnet18_gloo", batch_size=2, image_size=32, steps=2, warmup_steps=1,
+                     checkpoint_dir=os.path.join(tmpdir, "ck"), num_classes=10)
+    s = Trainer(cfg).run()
+    # resume from the checkpoint written at the end of the run
+    cfg2 = cfg.replace(resume=True, steps=1, warmup_steps=0, checkpoint_dir=cfg.checkpoint_dir)
+    t2 = Trainer(cfg2)
+    resumed_step = t2.step
+    s2 = t2.run()
+    return {"summary": s, "resumed_step": resumed_step, "loss2": s2["final_loss"]}
+
+
+def _broadcast_init_check():
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    torch.manual_seed(dist.get_rank())          # deliberately different init per rank
+    m = torch.nn.Linear(4, 4)
+    DataParallel(m)
+    w = m.weight.detach().clone()
+    dist.all_reduce(w)
+    return (w / dist.get_world_size() - m.weight.detach()).abs().max().item()
+
+
+# ---------------------------------------------------------------- tests
+def test_distributor_returns_rank0_value():
+    out = Distributor(num_processes=2, use_gpu=False).run(_rank_info, "hello")
+    assert out == {"tag": "hello", "rank": 0, "world": 2, "sum": 3.0}
+
+
+def test_distributor_single_process_inline():
+    assert Distributor(1, use_gpu=False, init_process_group=False).run(lambda a: a + 1, 41) == 42
+
+
+def test_distributor_propagates_child_failure():
+    with pytest.raises(ChildFailed) as ei:
+        Distributor(num_processes=2, use_gpu=False, timeout_s=120).run(_fail_on_rank1)
+    assert ei.value.rank == 1 and "boom from rank 1" in str(ei.value)
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_ddp_matches_single_process_large_batch(accum):
+    out = Distributor(num_processes=2, use_gpu=False).run(_ddp_equivalence, accum)
+    assert out["err"] < 1e-6, out
+    assert out["nbuckets"] > 1
+
+
+def test_ddp_broadcasts_rank0_params():
+    assert Distributor(num_processes=2, use_gpu=False).run(_broadcast_init_check) < 1e-7
+
+
+def test_horovod_runner_and_facade():
+    out = HorovodRunner(np=2, use_gpu=False).run(_hvd_equivalence)
+    assert out["err"] < 1e-6
+    assert out["avg"] == 0.5
+    assert out["gather"] == [0.0, 1.0]
+    assert out["bcast"] == 6.0
+
+
+def test_notebook_train_resnet18_gloo_world2_with_resume(tmp_path):
+    out = Distributor(num_processes=2, use_gpu=False, timeout_s=600).run(_train_resnet18_gloo, str(tmp_path))
+    s = out["summary"]
+    assert s["world_size"] == 2 and s["global_batch"] == 4
+    assert s["samples_per_sec"] > 0 and s["final_loss"] == s["final_loss"]
+    assert out["resumed_step"] == 3
+    assert out["loss2"] == out["loss2"]

@@ -1,0 +1,200 @@
+"""Numerics of the HIP kernels against plain-PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import gpu_device
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol=0.0, what=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"{what}: max err {err:.3e} > tol {tol:.3e}"
+
+
+def _native_lib_loaded():
+    from databricks_distributed_deep_learning_amd.ops import _lib
+    assert _lib.available(), _lib.load_error()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_batchnorm_train(dtype, relu, res, C):
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd.ops import norm
+    torch.manual_seed(0)
+    N, H, W = 4, 7, 9
+    x = (torch.randn(N, H, W, C, device=dev) * 2 + 0.5).to(dtype)
+    r = torch.randn(N, H, W, C, device=dev).to(dtype) if res else None
+    g = (torch.rand(C, device=dev) + 0.5).to(dtype)
+    b = (torch.randn(C, device=dev) * 0.1).to(dtype)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm.clone(), rv.clone()
+    xs = [x.clone().requires_grad_(True), x.float().clone().requires_grad_(True)]
+    gs = [g.clone().requires_grad_(True), g.float().clone().requires_grad_(True)]
+    bs = [b.clone().requires_grad_(True), b.float().clone().requires_grad_(True)]
+    rs = [r.clone().requires_grad_(True), r.float().clone().requires_grad_(True)] if res else [None, None]
+    y = norm.batch_norm(xs[0], gs[0], bs[0], rm, rv, True, 0.1, 1e-5, relu, rs[0])
+    yr = norm.batch_norm_reference(xs[1], gs[1], bs[1], rm2, rv2, True, 0.1, 1e-5, relu, rs[1])
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, yr, tol, tol, "bn fwd")
+    _close(rm, rm2, 1e-4, 1e-3, "running_mean")
+    _close(rv, rv2, 1e-4, 1e-3, "running_var")
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dtype))
+    yr.backward(dy)
+    _close(xs[0].grad, xs[1].grad, tol, tol, "bn dx")
+    _close(gs[0].grad, gs[1].grad, tol * 10, tol, "bn dgamma")
+    _close(bs[0].grad, bs[1].grad, tol * 10, tol, "bn dbeta")
+    if res:
+        _close(rs[0].grad, rs[1].grad, tol, tol, "bn dres")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [768, 1024])
+@pytest.mark.parametrize("res", [None, "full", "bcast"])
+def test_layernorm(dtype, H, res):
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd.ops import norm
+    torch.manual_seed(1)
+    B, S = 3, 37
+    x = torch.randn(B, S, H, device=dev).to(dtype)
+    g = (torch.rand(H, device=dev) + 0.5).to(dtype)
+    b = (torch.randn(H, device=dev) * 0.1).to(dtype)
+    r = None
+    if res == "full":
+        r = torch.randn(B, S, H, device=dev).to(dtype)
+    elif res == "bcast":
+        r = torch.randn(1, S, H, device=dev).to(dtype)
+    leaves = lambda t: None if t is None else t.clone().requires_grad_(True)  # noqa: E731
+    a = [leaves(x), leaves(g), leaves(b), leaves(r)]
+    f = [leaves(x.float()), leaves(g.float()), leaves(b.float()), leaves(None if r is None else r.float())]
+    y = norm.layer_norm(a[0], a[1], a[2], 1e-12, a[3])
+    yr = norm.layer_norm_reference(f[0], f[1], f[2], 1e-12, f[3])
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, yr, tol, tol, "ln fwd")
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dtype))
+    yr.backward(dy)
+    _close(a[0].grad, f[0].grad, tol, tol, "ln dx")
+    _close(a[1].grad, f[1].grad, tol * 20, tol, "ln dgamma")
+    _close(a[2].grad, f[2].grad, tol * 20, tol, "ln dbeta")
+    if r is not None:
+        _close(a[3].grad, f[3].grad, tol * 10, tol, "ln dres")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gelu_dropout(dtype):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_elementwise as E
+    x = torch.randn(4096, 96, device=dev).to(dtype).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    y = E.gelu(x)
+    yr = F.gelu(xr)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    _close(y, yr, tol, tol, "gelu")
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    _close(x.grad, xr.grad, tol * 2, tol, "gelu bwd")
+    # dropout: keep-rate and scaling; backward reuses the same mask
+    ones = torch.ones(1 << 20, device=dev, dtype=dtype, requires_grad=True)
+    d = E.dropout(ones, 0.1)
+    kept = (d != 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.005
+    _close(d[d != 0], torch.full_like(d[d != 0], 1 / 0.9), 1e-2)
+    d.backward(torch.ones_like(d))
+    assert torch.equal(ones.grad != 0, d != 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [2, 1000])
+def test_cross_entropy(dtype, C):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_loss as L
+    logits = (torch.randn(64, C, device=dev) * 3).to(dtype).requires_grad_(True)
+    lr = logits.detach().float().requires_grad_(True)
+    y = torch.randint(0, C, (64,), device=dev)
+    loss = L.cross_entropy(logits, y)
+    ref = F.cross_entropy(lr, y)
+    _close(loss, ref, 1e-3 if dtype == torch.bfloat16 else 1e-5, 1e-3)
+    (loss * 2).backward()
+    (ref * 2).backward()
+    _close(logits.grad, lr.grad, 1e-3, 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pools(dtype):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_pool as Pn, pool
+    x = torch.randn(2, 15, 13, 64, device=dev).to(dtype).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    y = Pn.max_pool2d(x, 3, 2, 1)
+    yr = pool.max_pool2d_reference(xr, 3, 2, 1)
+    _close(y, yr, 0.0, 0.0, "maxpool fwd")
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    _close(x.grad, xr.grad, 1e-2 if dtype == torch.bfloat16 else 1e-6, 0, "maxpool bwd")
+    z = torch.randn(4, 7, 7, 256, device=dev).to(dtype).requires_grad_(True)
+    zr = z.detach().float().requires_grad_(True)
+    a = Pn.global_avg_pool(z)
+    ar = zr.mean(dim=(1, 2))
+    _close(a, ar, 1e-2 if dtype == torch.bfloat16 else 1e-6)
+    g = torch.randn_like(ar)
+    a.backward(g.to(dtype))
+    ar.backward(g)
+    _close(z.grad, zr.grad, 1e-3)
+
+
+def test_embedding():
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_embedding as Em
+    w = torch.randn(1000, 768, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    wr = w.detach().float().requires_grad_(True)
+    ids = torch.randint(0, 1000, (8, 128), device=dev)
+    y = Em.embedding(ids, w)
+    yr = F.embedding(ids, wr)
+    _close(y, yr, 0.0)
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    _close(w.grad, wr.grad, 5e-2, 1e-2)
+
+
+@pytest.mark.parametrize("name", ["sgd", "adamw", "lamb"])
+@pytest.mark.parametrize("pdtype", [torch.float32, torch.bfloat16])
+def test_flat_optimizers_match_torch_path(name, pdtype):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.config import TrainConfig
+    from databricks_distributed_deep_learning_amd.ops import _lib
+    from databricks_distributed_deep_learning_amd.optim import ParamArena, build_optimizer
+
+    def make():
+        torch.manual_seed(3)
+        m = torch.nn.Sequential(torch.nn.Linear(67, 129), torch.nn.LayerNorm(129), torch.nn.Linear(129, 5)).to(dev)
+        for prm in m.parameters():
+            prm.data = prm.data.to(pdtype)
+        return m
+
+    cfg = TrainConfig(lr=1e-2, weight_decay=0.1, momentum=0.9, max_grad_norm=1.0 if name == "lamb" else 0.0)
+    outs = []
+    for mode in ("auto", "off"):
+        _lib.set_mode(mode)
+        m = make()
+        arena = ParamArena(list(m.named_parameters()))
+        opt = build_optimizer(name, arena, cfg)
+        g = torch.Generator(device=dev).manual_seed(7)
+        for _ in range(3):
+            arena.grad.copy_(torch.randn(arena.numel, generator=g, device=dev).to(pdtype))
+            opt.step(arena.grad, grad_scale=0.5)
+        outs.append((opt.params32.clone(), arena.flat.clone()))
+    _lib.set_mode("auto")
+    _close(outs[0][0], outs[1][0], 1e-5, 1e-5, f"{name} master")
+    _close(outs[0][1], outs[1][1], 1e-2 if pdtype == torch.bfloat16 else 1e-5, 1e-5, f"{name} param")
