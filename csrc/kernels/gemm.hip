@@ -1,0 +1,472 @@
+// bf16 MFMA GEMM + implicit-GEMM convolution for gfx950 (kernel families K1/K2/K3/K9/K13).
+//
+//   C[m][n] = sum_k A(m,k) * B(n,k)  (+ bias[n]) (activation)     fp32 accumulate
+//
+// Operand loaders (template parameters) cover every GEMM the models issue
+// without any transpose copies:
+//   KC  : X(r,k) = X[r*ld + k]          (row-major, reduction contiguous)
+//   KO  : X(r,k) = X[k*ld + r]          (reduction outer: dgrad weights, wgrad activations)
+//   CONV: A(m,k) = implicit im2col of an NHWC tensor (conv fwd / dgrad)
+//   CONVW: B(n,k) = im2col with the reduction over output pixels (conv wgrad)
+//
+// Tiling (CDNA4): 128x128x64 block tile, 256 threads = 4 wave64 in a 2x2 grid,
+// each wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16 tiles.  Operands are staged
+// global -> registers -> LDS (double-buffered, one barrier per K-step; the next
+// tile's global loads are in flight under the current tile's MFMAs).  LDS
+// images are XOR-swizzled so both fragment reads are bank-conflict free:
+//   KC image  [128 rows][64 k], 128-B rows, chunk' = chunk ^ ((row>>1)&7),
+//             fragments by ds_read_b128;
+//   KO image  [64 k][128 cols], 256-B rows, chunk' = chunk ^ 2*((r&3)|((r>>3)&1)<<2),
+//             fragments by ds_read_b64_tr_b16 (hardware transpose).
+// The MFMA is issued as (B-fragment, A-fragment) so each lane's accumulator
+// holds 4 consecutive output COLUMNS of one row: the epilogue stores 8/16 B per
+// lane and applies bias / GELU / ReLU / tanh from fp32 before rounding once.
+// Split-K writes fp32 partial slabs reduced (with the epilogue) by gemm_reduce.
+// Block ids are remapped so the blocks that share an XCD's L2 (ids congruent
+// mod 8) walk neighbouring tiles (bijective remap, §5.5 T1).
+#include "ddl_common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;   // 16 KB per operand tile
+
+enum Layout { KC = 0, KO = 1, CONV = 2, CONVW = 3 };
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4 };
+
+struct ConvDesc {
+    int N, H, W, C;                 // input NHWC
+    int P, Q;                       // GEMM output-pixel grid
+    int stride, h_off, w_off, h_step, w_step;
+    int R, S;                       // taps (after sub-setting for dgrad classes)
+    FastDiv fd_PQ, fd_Q, fd_C, fd_S;
+    int OH, OW, ostep, oa, ob;      // output pixel (n, p*ostep+oa, q*ostep+ob) in [OH, OW]
+};
+
+struct Params {
+    const bf16_t* A;
+    const bf16_t* B;
+    long lda, ldb;
+    void* C;
+    long ldc;
+    int M, N, K;
+    const void* bias;
+    int bias_bf16;
+    int act;
+    void* aux;        // ACT_GELU: pre-activation output (bf16, ldc); ACT_DGELU: pre-activation input
+    int out_f32;
+    int splits, kt_per_split;
+    long split_stride;
+    int row_remap;    // conv output rows -> strided output pixels
+    ConvDesc cd;
+    int tiles_m, tiles_n;
+};
+
+// Loads are unconditional from a clamped (always valid) address and the VALUE is
+// selected, so hipcc never materialises a zero vector in scratch for a
+// select-of-pointers.
+__device__ __forceinline__ uint4 ldg16(const bf16_t* ptr) { return *reinterpret_cast<const uint4*>(ptr); }
+__device__ __forceinline__ uint4 sel(bool ok, uint4 a, uint4 z) {
+    return make_uint4(ok ? a.x : z.x, ok ? a.y : z.y, ok ? a.z : z.z, ok ? a.w : z.w);
+}
+
+__device__ __forceinline__ int swz_ko(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+// ------------------------------------------------------------------ loaders
+// Each thread stages 4 chunks (16 B) of each operand per K-step.
+template <int L, bool IS_A>
+struct Loader {
+    // KC / CONV: thread -> chunk c = t&7, rows (t>>3) + 32 i
+    // KO / CONVW: thread -> chunk c = t&15, k-rows (t>>4) + 16 i
+    const bf16_t* base;
+    long ld;
+    int rows_total;   // M or N extent of this operand
+    int K;
+    int r0;           // tile origin (m0 or n0)
+    // conv state
+    int hb[4], wb[4];
+    const bf16_t* img[4];
+    bool rowok[4];
+    int ctap_r, ctap_s, cci;   // CONVW: column tap decomposition (fixed per thread)
+    bool colok;
+
+    __device__ __forceinline__ void init(const Params& p, int origin) {
+        const int t = threadIdx.x;
+        base = IS_A ? p.A : p.B;
+        ld = IS_A ? p.lda : p.ldb;
+        rows_total = IS_A ? p.M : p.N;
+        K = p.K;
+        r0 = origin;
+        if (L == CONV) {
+            const ConvDesc& cd = p.cd;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = r0 + (t >> 3) + 32 * i;
+                rowok[i] = m < rows_total;
+                const int mm = rowok[i] ? m : 0;
+                const int n = (int)fdiv((uint32_t)mm, cd.fd_PQ);
+                const int rem = mm - n * cd.P * cd.Q;
+                const int pp = (int)fdiv((uint32_t)rem, cd.fd_Q);
+                const int qq = rem - pp * cd.Q;
+                hb[i] = pp * cd.stride + cd.h_off;
+                wb[i] = qq * cd.stride + cd.w_off;
+                img[i] = base + (long)n * cd.H * cd.W * cd.C;
+            }
+        }
+        if (L == CONVW) {
+            const ConvDesc& cd = p.cd;
+            const int col = r0 + 8 * (t & 15);
+            colok = col < rows_total;
+            const int cc = colok ? col : 0;
+            const int tap = (int)fdiv((uint32_t)cc, cd.fd_C);
+            cci = cc - tap * cd.C;
+            ctap_r = (int)fdiv((uint32_t)tap, cd.fd_S);
+            ctap_s = tap - ctap_r * cd.S;
+        }
+    }
+
+    __device__ __forceinline__ void load(const Params& p, int k0, uint4 (&v)[4]) {
+        const int t = threadIdx.x;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        if (L == KC) {
+            const int c = t & 7;
+            const int k = k0 + 8 * c;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = r0 + (t >> 3) + 32 * i;
+                const bool ok = r < rows_total && k < K;
+                v[i] = sel(ok, ldg16(ok ? base + (long)r * ld + k : base), z);
+            }
+        } else if (L == KO) {
+            const int col = r0 + 8 * (t & 15);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = k0 + (t >> 4) + 16 * i;
+                const bool ok = k < K && col < rows_total;
+                v[i] = sel(ok, ldg16(ok ? base + (long)k * ld + col : base), z);
+            }
+        } else if (L == CONV) {
+            const ConvDesc& cd = p.cd;
+            const int k = k0 + 8 * (t & 7);
+            const int kk = k < K ? k : 0;
+            const int tap = (int)fdiv((uint32_t)kk, cd.fd_C);
+            const int ci = kk - tap * cd.C;
+            const int rr = (int)fdiv((uint32_t)tap, cd.fd_S);
+            const int ss = tap - rr * cd.S;
+            const int dh = rr * cd.h_step, dw = ss * cd.w_step;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int h = hb[i] + dh, w = wb[i] + dw;
+                const bool ok = rowok[i] && k < K && (unsigned)h < (unsigned)cd.H && (unsigned)w < (unsigned)cd.W;
+                v[i] = sel(ok, ldg16(ok ? img[i] + ((long)h * cd.W + w) * cd.C + ci : base), z);
+            }
+        } else {  // CONVW: reduction rows are output pixels m
+            const ConvDesc& cd = p.cd;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = k0 + (t >> 4) + 16 * i;
+                bool ok = colok && m < K;
+                const int mm = ok ? m : 0;
+                const int n = (int)fdiv((uint32_t)mm, cd.fd_PQ);
+                const int rem = mm - n * cd.P * cd.Q;
+                const int pp = (int)fdiv((uint32_t)rem, cd.fd_Q);
+                const int qq = rem - pp * cd.Q;
+                const int h = pp * cd.stride + cd.h_off + ctap_r * cd.h_step;
+                const int w = qq * cd.stride + cd.w_off + ctap_s * cd.w_step;
+                ok = ok && (unsigned)h < (unsigned)cd.H && (unsigned)w < (unsigned)cd.W;
+                v[i] = sel(ok, ldg16(ok ? base + (((long)n * cd.H + h) * cd.W + w) * cd.C + cci : base), z);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store(char* lds, const uint4 (&v)[4]) {
+        const int t = threadIdx.x;
+        if (L == KC || L == CONV) {
+            const int c = t & 7;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = (t >> 3) + 32 * i;
+                *reinterpret_cast<uint4*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = v[i];
+            }
+        } else {
+            const int c = t & 15;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = (t >> 4) + 16 * i;
+                *reinterpret_cast<uint4*>(lds + r * 256 + ((c ^ swz_ko(r)) << 4)) = v[i];
+            }
+        }
+    }
+};
+
+// Fragment for rows [rbase, rbase+16) of the tile, k-subtile kk (0/1):
+// lane l gets row rbase + (l&15), k = 32 kk + 8 (l>>4) + 0..7.
+template <int L>
+__device__ __forceinline__ bf16x8 read_frag(const char* lds, int rbase, int kk) {
+    const int l = threadIdx.x & 63;
+    if (L == KC || L == CONV) {
+        const int r = rbase + (l & 15);
+        const int c = kk * 4 + (l >> 4);
+        return *reinterpret_cast<const bf16x8*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+    } else {
+        const int g = l >> 4, q = (l >> 2) & 3, pq = l & 3;
+        const int col = rbase + 4 * pq;
+        const int chunk = col >> 3;
+        const int r_a = kk * 32 + 8 * g + q;
+        const int r_b = r_a + 4;
+        typedef __attribute__((address_space(3))) s16x4 lds_v4;
+        const char* pa = lds + r_a * 256 + ((chunk ^ swz_ko(r_a)) << 4) + (pq & 1) * 8;
+        const char* pb = lds + r_b * 256 + ((chunk ^ swz_ko(r_b)) << 4) + (pq & 1) * 8;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pa);
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pb);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, r);
+    }
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+    switch (act) {
+        case ACT_GELU: return gelu_erf(v);
+        case ACT_RELU: return fmaxf(v, 0.f);
+        case ACT_TANH: return tanhf(v);
+        default: return v;
+    }
+}
+
+__device__ __forceinline__ long out_row(const Params& p, int m) {
+    if (!p.row_remap) return m;
+    const ConvDesc& cd = p.cd;
+    const int n = (int)fdiv((uint32_t)m, cd.fd_PQ);
+    const int rem = m - n * cd.P * cd.Q;
+    const int pp = (int)fdiv((uint32_t)rem, cd.fd_Q);
+    const int qq = rem - pp * cd.Q;
+    return ((long)n * cd.OH + pp * cd.ostep + cd.oa) * cd.OW + qq * cd.ostep + cd.ob;
+}
+
+template <int LA, int LB>
+__global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+    // ---- XCD-aware bijective tile remap
+    const int nwg = p.tiles_m * p.tiles_n;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
+    const int wg = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+    const int tm = wg / p.tiles_n, tn = wg - tm * p.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int split = blockIdx.y;
+
+    const int nk_total = (p.K + BK - 1) / BK;
+    const int kt0 = split * p.kt_per_split;
+    const int kt1 = min(nk_total, kt0 + p.kt_per_split);
+
+    Loader<LA, true> la;
+    Loader<LB, false> lb;
+    la.init(p, m0);
+    lb.init(p, n0);
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = w & 1, wn = w >> 1;
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    if (kt0 < kt1) {
+        uint4 ra[4], rb[4];
+        la.load(p, kt0 * BK, ra);
+        lb.load(p, kt0 * BK, rb);
+        la.store(smem, ra);
+        lb.store(smem + TILE_BYTES, rb);
+        __syncthreads();
+        for (int kt = kt0; kt < kt1; ++kt) {
+            const int cur = (kt - kt0) & 1;
+            char* sa = smem + cur * 2 * TILE_BYTES;
+            char* sb = sa + TILE_BYTES;
+            const bool more = kt + 1 < kt1;
+            if (more) {
+                la.load(p, (kt + 1) * BK, ra);
+                lb.load(p, (kt + 1) * BK, rb);
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                bf16x8 af[4], bfr[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = read_frag<LA>(sa, wm * 64 + i * 16, kk);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bfr[j] = read_frag<LB>(sb, wn * 64 + j * 16, kk);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+            }
+            if (more) {
+                char* na = smem + (cur ^ 1) * 2 * TILE_BYTES;
+                la.store(na, ra);
+                lb.store(na + TILE_BYTES, rb);
+            }
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: lane holds C[m][n..n+3]
+    const int g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+        if (m >= p.M) continue;
+        const long orow = out_row(p, m);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + j * 16 + 4 * g;
+            if (n >= p.N) continue;
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            const bool full = n + 3 < p.N;
+            if (p.out_f32 && p.splits > 1) {
+                float* c = (float*)p.C + split * p.split_stride + orow * p.ldc + n;
+                if (full) store4(c, v);
+                else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) if (n + r < p.N) c[r] = v[r];
+                }
+                continue;
+            }
+            if (p.bias) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (n + r < p.N)
+                        v[r] += p.bias_bf16 ? bf2f(((const bf16_t*)p.bias)[n + r]) : ((const float*)p.bias)[n + r];
+            }
+            if (p.act == ACT_DGELU) {
+                float z[4];
+                const bf16_t* ap = (const bf16_t*)p.aux + orow * p.ldc + n;
+                if (full) load4(ap, z);
+                else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) z[r] = n + r < p.N ? bf2f(ap[r]) : 0.f;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] *= gelu_erf_grad(z[r]);
+            } else if (p.act != ACT_NONE) {
+                if (p.aux) {  // keep the pre-activation for backward
+                    bf16_t* ap = (bf16_t*)p.aux + orow * p.ldc + n;
+                    if (full) store4(ap, v);
+                    else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) if (n + r < p.N) ap[r] = f2bf(v[r]);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+            }
+            if (p.out_f32) {
+                float* c = (float*)p.C + orow * p.ldc + n;
+                if (full) store4(c, v);
+                else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) if (n + r < p.N) c[r] = v[r];
+                }
+            } else {
+                bf16_t* c = (bf16_t*)p.C + orow * p.ldc + n;
+                if (full) store4(c, v);
+                else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) if (n + r < p.N) c[r] = f2bf(v[r]);
+                }
+            }
+        }
+    }
+}
+
+// Sum split-K fp32 partials, apply the epilogue, write bf16/fp32.
+__global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ part, int splits, long split_stride,
+                                                     int M, int N, long ldc, void* out, int out_f32,
+                                                     const void* bias, int bias_bf16, int act, void* aux) {
+    const long total = (long)M * N;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int m = (int)(i / N), n = (int)(i - (long)m * N);
+        float v = 0.f;
+        for (int s = 0; s < splits; ++s) v += part[s * split_stride + (long)m * ldc + n];
+        if (bias) v += bias_bf16 ? bf2f(((const bf16_t*)bias)[n]) : ((const float*)bias)[n];
+        if (act == ACT_DGELU) v *= gelu_erf_grad(bf2f(((const bf16_t*)aux)[(long)m * ldc + n]));
+        else if (act != ACT_NONE) {
+            if (aux) ((bf16_t*)aux)[(long)m * ldc + n] = f2bf(v);
+            v = apply_act(v, act);
+        }
+        if (out_f32) ((float*)out)[(long)m * ldc + n] = v;
+        else ((bf16_t*)out)[(long)m * ldc + n] = f2bf(v);
+    }
+}
+
+template <int LA, int LB>
+int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t st) {
+    p.tiles_m = (p.M + BM - 1) / BM;
+    p.tiles_n = (p.N + BN - 1) / BN;
+    const int nk = (p.K + BK - 1) / BK;
+    if (splits < 1) splits = 1;
+    if (splits > nk) splits = nk > 0 ? nk : 1;
+    p.kt_per_split = (nk + splits - 1) / splits;
+    splits = nk > 0 ? (nk + p.kt_per_split - 1) / p.kt_per_split : 1;
+    p.splits = splits;
+    void* final_out = p.C;
+    const int final_f32 = p.out_f32;
+    if (splits > 1) {
+        p.split_stride = (long)p.M * p.ldc;
+        if (!workspace || ws_elems < p.split_stride * splits) return -2;
+        if (p.row_remap) return -3;
+        p.C = workspace;
+        p.out_f32 = 1;
+    }
+    dim3 grid(p.tiles_m * p.tiles_n, splits);
+    hipLaunchKernelGGL((gemm_k<LA, LB>), grid, dim3(NT), 0, st, p);
+    if (splits > 1) {
+        const long total = (long)p.M * p.N;
+        const int g = (int)std::min<long>(8192, (total + 255) / 256);
+        gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.M, p.N, p.ldc, final_out, final_f32,
+                                          p.bias, p.bias_bf16, p.act, p.aux);
+    }
+    return (int)hipGetLastError();
+}
+
+void fill_conv(ConvDesc& cd, const int* d) {
+    // d: N H W C P Q stride h_off w_off h_step w_step R S OH OW ostep oa ob
+    cd.N = d[0]; cd.H = d[1]; cd.W = d[2]; cd.C = d[3]; cd.P = d[4]; cd.Q = d[5];
+    cd.stride = d[6]; cd.h_off = d[7]; cd.w_off = d[8]; cd.h_step = d[9]; cd.w_step = d[10];
+    cd.R = d[11]; cd.S = d[12]; cd.OH = d[13]; cd.OW = d[14]; cd.ostep = d[15]; cd.oa = d[16]; cd.ob = d[17];
+    cd.fd_PQ = make_fastdiv((uint32_t)(cd.P * cd.Q));
+    cd.fd_Q = make_fastdiv((uint32_t)cd.Q);
+    cd.fd_C = make_fastdiv((uint32_t)cd.C);
+    cd.fd_S = make_fastdiv((uint32_t)std::max(1, cd.S));
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+// mode: 0 = A KC, B KC   (y = x W^T, Linear fwd)
+//       1 = A KC, B KO   (dx = dy W,  Linear dgrad)
+//       2 = A KO, B KO   (dW = dy^T x, Linear wgrad)
+//       3 = A CONV, B KC (conv fwd / dgrad by implicit GEMM; conv desc required)
+//       4 = A KO, B CONVW (conv wgrad; conv desc required)
+// act: 0 none, 1 gelu (aux <- pre-activation if aux), 2 relu, 3 tanh, 4 dgelu (v *= gelu'(aux))
+DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
+                     int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
+                     float* workspace, long ws_elems, const int* conv, int row_remap, hipStream_t st) {
+    Params p{};
+    p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
+    p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+    p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = aux; p.out_f32 = out_f32;
+    p.row_remap = row_remap;
+    if (conv) fill_conv(p.cd, conv);
+    if (M <= 0 || N <= 0) return 0;
+    switch (mode) {
+        case 0: return launch<KC, KC>(p, workspace, ws_elems, splits, st);
+        case 1: return launch<KC, KO>(p, workspace, ws_elems, splits, st);
+        case 2: return launch<KO, KO>(p, workspace, ws_elems, splits, st);
+        case 3: return launch<CONV, KC>(p, workspace, ws_elems, splits, st);
+        case 4: return launch<KO, CONVW>(p, workspace, ws_elems, splits, st);
+        default: return -1;
+    }
+}

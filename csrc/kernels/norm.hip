@@ -32,6 +32,7 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_partial_k(const T* __restrict_
     float s[8], q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+#pragma unroll 4
     for (long r = r0 + rr; r < r1; r += rpi) {
         float v[8];
         load8(x + r * C + cg * 8, v);
@@ -55,19 +56,38 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_partial_k(const T* __restrict_
     }
 }
 
-template <typename TP>
-__global__ void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M, const TP* __restrict__ gamma,
-                                    const TP* __restrict__ beta, float* __restrict__ running_mean,
-                                    float* __restrict__ running_var, float momentum, float eps,
-                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                    float* __restrict__ scale, float* __restrict__ shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int b = 0; b < nblk; ++b) {
-        s += part[(long)b * 2 * C + c];
-        q += part[(long)b * 2 * C + C + c];
+// Sum the per-block partials: block = 64 channels x 4 partial-row groups, so
+// each wave reads 64 consecutive floats per partial row (coalesced, independent
+// loads in flight) instead of one thread walking every partial serially.
+__device__ __forceinline__ void sum_partials_64(const float* __restrict__ part, int nblk, int C, int c, double& s,
+                                                double& q, double* red) {
+    const int grp = threadIdx.x >> 6;
+    double a = 0.0, b = 0.0;
+    if (c < C) {
+        for (int blk = grp; blk < nblk; blk += 4) {
+            a += part[(long)blk * 2 * C + c];
+            b += part[(long)blk * 2 * C + C + c];
+        }
     }
+    red[threadIdx.x] = a;
+    red[256 + threadIdx.x] = b;
+    __syncthreads();
+    const int l = threadIdx.x & 63;
+    s = red[l] + red[64 + l] + red[128 + l] + red[192 + l];
+    q = red[256 + l] + red[320 + l] + red[384 + l] + red[448 + l];
+}
+
+template <typename TP>
+__global__ __launch_bounds__(256) void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+                                    const TP* __restrict__ gamma, const TP* __restrict__ beta,
+                                    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum,
+                                    float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+    __shared__ double red[512];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    double s, q;
+    sum_partials_64(part, nblk, C, c, s, q, red);
+    if (threadIdx.x >= 64 || c >= C) return;
     const double mean = s / (double)M;
     double var = q / (double)M - mean * mean;
     if (var < 0) var = 0;
@@ -138,6 +158,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
     load8(invstd + cg * 8, is);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
+#pragma unroll 2
     for (long r = r0 + rr; r < r1; r += rpi) {
         float g[8], xv[8], yo[8];
         load8(dy + r * C + cg * 8, g);
@@ -168,16 +189,14 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
 }
 
 template <typename TP>
-__global__ void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+__global__ __launch_bounds__(256) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
                                   const TP* __restrict__ gamma, const float* __restrict__ invstd,
                                   TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int b = 0; b < nblk; ++b) {
-        s += part[(long)b * 2 * C + c];
-        q += part[(long)b * 2 * C + C + c];
-    }
+    __shared__ double red[512];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    double s, q;
+    sum_partials_64(part, nblk, C, c, s, q, red);
+    if (threadIdx.x >= 64 || c >= C) return;
     if (dgamma) dgamma[c] = from_f<TP>((float)q);
     if (dbeta) dbeta[c] = from_f<TP>((float)s);
     const float g = gamma ? to_f(gamma[c]) : 1.f;
@@ -354,7 +373,7 @@ inline int grid_for(long n, int nt = 256, int cap = 4096) {
 
 DDL_API int ddl_bn_stats_nblk(long M, int C) {
     const int rpi = BN_NT / (C / 8);
-    long nblk = std::min<long>(2048, (M + rpi - 1) / rpi);
+    long nblk = std::min<long>(1024, (M + rpi * 8 - 1) / (rpi * 8));
     return (int)std::max<long>(1, nblk);
 }
 
@@ -368,11 +387,11 @@ DDL_API int ddl_bn_fwd_train(int dtype, const void* x, long M, int C, const void
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (dtype == 1) {
         bn_stats_partial_k<bf16_t><<<nblk, BN_NT, 0, st>>>((const bf16_t*)x, M, C, (int)rpb, part);
-        bn_stats_finalize_k<bf16_t><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
+        bn_stats_finalize_k<bf16_t><<<(C + 63) / 64, 256, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
             (const bf16_t*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
     } else {
         bn_stats_partial_k<float><<<nblk, BN_NT, 0, st>>>((const float*)x, M, C, (int)rpb, part);
-        bn_stats_finalize_k<float><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, M, (const float*)gamma,
+        bn_stats_finalize_k<float><<<(C + 63) / 64, 256, 0, st>>>(part, nblk, C, M, (const float*)gamma,
             (const float*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
     }
     DDL_RETURN_LAUNCH();
@@ -421,7 +440,7 @@ static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float*
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
-    bn_bwd_finalize_k<T><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef);
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 256, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef);
     const long n8 = M * C / 8;
     const int g = grid_for(n8, 256, 8192);
     if (relu) {

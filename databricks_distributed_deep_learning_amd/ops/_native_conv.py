@@ -1,6 +1,126 @@
-"""Conv binding (interim: MIOpen via F.conv2d until conv_igemm.hip lands)."""
-from .conv import conv2d_reference
+"""NHWC convolution as implicit GEMM on MFMA (csrc/kernels/gemm.hip), with autograd.
+
+forward : y[m, k]  = sum_(r,s,c) x[pix(m, r, s), c] * W[k, r, s, c]   mode CONV
+          (1x1 / stride-1 convs are plain NT GEMMs over [N*H*W, C])
+dgrad   : stride 1 -> a stride-1 conv of dy with the flipped, transposed weight
+          stride 2 -> four output-parity classes, each a small stride-1 conv of dy
+          over the taps of that parity, written through a strided row remap (no
+          zero-insertion, no wasted MFMA work)
+wgrad   : dW[k, (r,s,c)] = sum_m dy[m, k] * im2col(x)[m, (r,s,c)]      mode CONVW,
+          split-K over the N*P*Q output pixels with fp32 partial slabs
+Inputs whose channel count is not a multiple of 8 (the RGB stem) are zero-padded
+to 8 channels so every gathered chunk is one 16-byte load.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm
+
+
+def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep=1, oa=0, ob=0):
+    return [N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep, oa, ob]
+
+
+def _fwd(x, w, stride, pad):
+    N, H, W_, C = x.shape
+    K, R, S, _ = w.shape
+    P = (H + 2 * pad - R) // stride + 1
+    Q = (W_ + 2 * pad - S) // stride + 1
+    y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
+    M = N * P * Q
+    if R == 1 and S == 1 and stride == 1 and pad == 0:
+        gemm(MODE_NT, x, C, w, C, y, K, M, K, C)
+    else:
+        gemm(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C,
+             conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q))
+    return y
+
+
+def _dgrad(dy, w, x_shape, stride, pad):
+    N, H, W_, C = x_shape
+    K, R, S, _ = w.shape
+    _, P, Q, _ = dy.shape
+    if R == 1 and S == 1 and stride == 1 and pad == 0:
+        dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
+        gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K)
+        return dx
+    if stride == 1:
+        wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()       # [C, R, S, K]
+        dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
+        gemm(MODE_CONV, dy, 0, wt, R * S * K, dx, C, N * H * W_, C, R * S * K,
+             conv=_desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_))
+        return dx
+    # stride s: output-parity classes (a, b); taps r = a+pad (mod s)
+    classes = []
+    empty = False
+    for a in range(stride):
+        rs = [r for r in range(R) if (r - a - pad) % stride == 0]
+        for b in range(stride):
+            ss = [s for s in range(S) if (s - b - pad) % stride == 0]
+            Ho = (H - a + stride - 1) // stride
+            Wo = (W_ - b + stride - 1) // stride
+            if not rs or not ss or Ho <= 0 or Wo <= 0:
+                empty = True
+                continue
+            classes.append((a, b, rs, ss, Ho, Wo))
+    dx = (torch.zeros if empty else torch.empty)(N, H, W_, C, dtype=dy.dtype, device=dy.device)
+    for a, b, rs, ss, Ho, Wo in classes:
+        wc = w[:, rs][:, :, ss].permute(3, 1, 2, 0).contiguous()   # [C, R', S', K]
+        h_off = (a + pad - rs[0]) // stride
+        w_off = (b + pad - ss[0]) // stride
+        Rp, Sp = len(rs), len(ss)
+        gemm(MODE_CONV, dy, 0, wc, Rp * Sp * K, dx, C, N * Ho * Wo, C, Rp * Sp * K,
+             conv=_desc(N, P, Q, K, Ho, Wo, 1, h_off, w_off, -1, -1, Rp, Sp, H, W_, stride, a, b),
+             row_remap=True)
+    return dx
+
+
+def _wgrad(dy, x, w_shape, stride, pad):
+    N, H, W_, C = x.shape
+    K, R, S, _ = w_shape
+    _, P, Q, _ = dy.shape
+    dw = torch.empty(K, R, S, C, dtype=dy.dtype, device=dy.device)
+    M = N * P * Q
+    if R == 1 and S == 1 and stride == 1 and pad == 0:
+        gemm(MODE_TN, dy, K, x, C, dw, C, K, C, M)
+    else:
+        gemm(MODE_CONVW, dy, K, x, 0, dw, R * S * C, K, R * S * C, M,
+             conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q))
+    return dw
+
+
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        x = x.contiguous()
+        w = w.contiguous()
+        ctx.stride, ctx.pad = stride, pad
+        ctx.save_for_backward(x, w)
+        return _fwd(x, w, stride, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
+        return dx, dw, None, None
 
 
 def conv2d(x, w, stride, padding):
-    return conv2d_reference(x, w, stride, padding)
+    from .conv import conv2d_reference
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return conv2d_reference(x, w, stride, padding)
+    C = x.shape[-1]
+    if C % 8:
+        c8 = (C + 7) // 8 * 8
+        x = F.pad(x, (0, c8 - C))
+        w = F.pad(w, (0, c8 - C))
+    if w.shape[0] % 8:
+        return conv2d_reference(x, w, stride, padding)
+    return _Conv.apply(x, w, stride, padding)

@@ -1,6 +1,85 @@
-"""Linear binding (interim: hipBLASLt via F.linear until gemm.hip lands)."""
-from .linear import linear_reference
+"""Linear layer on the MFMA GEMM (csrc/kernels/gemm.hip), with autograd.
+
+forward : y = act(x W^T + b)      mode NT, bias+act in the epilogue; with GELU the
+          pre-activation z is written by the same epilogue for backward
+backward: dz = dy * act'(z)       (GELU: ddl_gelu_bwd; tanh/relu from the output)
+          dx = dz W               mode NN (W read reduction-outer through the
+                                  LDS transpose reads; no W^T copy)
+          dW = dz^T x             mode TN, split-K over tokens
+          db = colsum(dz)
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._lib import call, dcode, p
+from ._native_gemm import MODE_NN, MODE_NT, MODE_TN, gemm
+from . import _native_elementwise as E
 
 
-def linear(x, w, b, act):
-    return linear_reference(x, w, b, act)
+def _ok(x, w) -> bool:
+    K = x.shape[-1]
+    N = w.shape[0]
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0
+            and x.numel() > 0)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        w = w.contiguous()
+        M = x2.shape[0]
+        y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        z = None
+        if act == "gelu" and torch.is_grad_enabled():
+            z = torch.empty_like(y)
+        gemm(MODE_NT, x2, K, w, K, y, N, M, N, K, bias=b, act=act, aux=z)
+        ctx.act = act
+        ctx.has_bias = b is not None
+        ctx.save_for_backward(x2, w, z if act == "gelu" else (y if act in ("tanh", "relu") else None))
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, saved = ctx.saved_tensors
+        M, K = x2.shape
+        N = w.shape[0]
+        dy2 = dy.reshape(M, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        if ctx.act == "gelu":
+            dz = torch.empty_like(dy2)
+            call("ddl_gelu_bwd", dcode(dy2), p(dy2), p(saved), p(dz), dz.numel())
+        elif ctx.act == "tanh":
+            dz = (dy2.float() * (1 - saved.float() ** 2)).to(dy2.dtype)
+        elif ctx.act == "relu":
+            dz = dy2 * (saved > 0)
+        else:
+            dz = dy2
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
+            gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
+            dx = dx.view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
+            gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.empty(N, dtype=w.dtype, device=w.device)
+            E.colsum(dz, db)
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str]) -> torch.Tensor:
+    if not _ok(x, w) or (b is not None and b.dtype != w.dtype):
+        from .linear import linear_reference
+        return linear_reference(x, w, b, act)
+    return _Linear.apply(x, w, b, act)
