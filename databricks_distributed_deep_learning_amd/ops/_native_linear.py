@@ -38,7 +38,7 @@ class _Linear(torch.autograd.Function):
         M = x2.shape[0]
         y = torch.empty(M, N, dtype=x.dtype, device=x.device)
         z = None
-        if act == "gelu" and torch.is_grad_enabled():
+        if act == "gelu" and any(ctx.needs_input_grad[:3]):   # grad mode is off inside forward
             z = torch.empty_like(y)
         gemm(MODE_NT, x2, K, w, K, y, N, M, N, K, bias=b, act=act, aux=z)
         ctx.act = act

@@ -1,0 +1,94 @@
+"""Fused attention vs an fp32 PyTorch reference (GPU only), incl. dropout-mask parity."""
+import math
+
+import pytest
+import torch
+
+from conftest import gpu_device
+
+pytestmark = pytest.mark.gpu
+
+M64 = (1 << 64) - 1
+
+
+def _s64(v):
+    v &= M64
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+C1, C2, C3 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
+
+
+def _lsr(z, k):
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def hash_u32(seed, idx):
+    """torch re-implementation of ddl_common.h hash_u32 (int64 wraps like uint64)."""
+    z = idx * C2 + _s64(seed * C1 + C3)
+    z = (z ^ _lsr(z, 30)) * C2
+    z = (z ^ _lsr(z, 27)) * C3
+    z = z ^ _lsr(z, 31)
+    return _lsr(z, 32)
+
+
+def ref_attention(qkv, H, mask=None, keep=None, p=0.0):
+    B, S, hd3 = qkv.shape
+    D = hd3 // (3 * H)
+    q, k, v = qkv.float().view(B, S, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)
+    s = q @ k.transpose(-1, -2) / math.sqrt(D)
+    if mask is not None:
+        s = s + mask.view(B, 1, 1, S)
+    pr = torch.softmax(s, -1)
+    if keep is not None:
+        pr = pr * keep / (1 - p)
+    return (pr @ v).permute(0, 2, 1, 3).reshape(B, S, H * D)
+
+
+@pytest.mark.parametrize("B,S,H", [(2, 128, 12), (3, 197, 2), (1, 64, 4), (2, 100, 3), (1, 512, 2)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_fwd_bwd(B, S, H, masked):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_attention as NA
+    torch.manual_seed(0)
+    qkv = torch.randn(B, S, 3 * H * 64, device=dev).to(torch.bfloat16).requires_grad_(True)
+    mask = None
+    if masked:
+        lens = torch.randint(S // 2, S + 1, (B,), device=dev)
+        mask = ((torch.arange(S, device=dev)[None] >= lens[:, None]).float() * -10000.0)
+    out = NA.attention(qkv, H, mask, 0.0)
+    q32 = qkv.detach().float().requires_grad_(True)
+    ref = ref_attention(q32, H, mask)
+    err = (out.float() - ref).abs().max().item()
+    assert err < 2e-2 * ref.abs().max().item() + 1e-2, err
+    g = torch.randn_like(ref)
+    out.backward(g.to(torch.bfloat16))
+    ref.backward(g.to(torch.bfloat16).float())
+    gerr = (qkv.grad.float() - q32.grad).abs().max().item()
+    assert gerr < 3e-2 * q32.grad.abs().max().item() + 1e-2, gerr
+
+
+def test_attention_dropout_mask_parity():
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_attention as NA
+    torch.manual_seed(1)
+    B, S, H, p = 2, 96, 3, 0.25
+    qkv = torch.randn(B, S, 3 * H * 64, device=dev).to(torch.bfloat16).requires_grad_(True)
+    torch.manual_seed(123)
+    out = NA.attention(qkv, H, None, p)
+    torch.manual_seed(123)
+    seed = NA.new_seed()
+    thresh = min(int(p * 2 ** 32), 2 ** 32 - 1)
+    bh = torch.arange(B * H, device=dev).view(B, H, 1, 1)
+    qi = torch.arange(S, device=dev).view(1, 1, S, 1)
+    ki = torch.arange(S, device=dev).view(1, 1, 1, S)
+    idx = (bh * S + qi) * S + ki
+    keep = (hash_u32(seed, idx) >= thresh).float()
+    assert abs(keep.mean().item() - (1 - p)) < 0.02
+    q32 = qkv.detach().float().requires_grad_(True)
+    ref = ref_attention(q32, H, None, keep, p)
+    assert (out.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item() + 1e-2
+    g = torch.randn_like(ref)
+    out.backward(g.to(torch.bfloat16))
+    ref.backward(g.to(torch.bfloat16).float())
+    assert (qkv.grad.float() - q32.grad).abs().max().item() < 3e-2 * q32.grad.abs().max().item() + 1e-2
