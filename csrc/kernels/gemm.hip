@@ -58,6 +58,7 @@ struct Params {
     int splits, kt_per_split;
     long split_stride;
     int row_remap;    // conv output rows -> strided output pixels
+    const bf16_t* res;  // optional residual added before the activation (same layout as C)
     ConvDesc cd;
     int tiles_m, tiles_n;
 };
@@ -340,6 +341,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
                     if (n + r < p.N)
                         v[r] += p.bias_bf16 ? bf2f(((const bf16_t*)p.bias)[n + r]) : ((const float*)p.bias)[n + r];
             }
+            if (p.res) {
+                float rr[4];
+                const bf16_t* rp = p.res + orow * p.ldc + n;
+                if (full) load4(rp, rr);
+                else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) rr[r] = n + r < p.N ? bf2f(rp[r]) : 0.f;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += rr[r];
+            }
             if (p.act == ACT_DGELU) {
                 float z[4];
                 const bf16_t* ap = (const bf16_t*)p.aux + orow * p.ldc + n;
@@ -384,13 +396,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
 // Sum split-K fp32 partials, apply the epilogue, write bf16/fp32.
 __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ part, int splits, long split_stride,
                                                      int M, int N, long ldc, void* out, int out_f32,
-                                                     const void* bias, int bias_bf16, int act, void* aux) {
+                                                     const void* bias, int bias_bf16, int act, void* aux,
+                                                     const bf16_t* __restrict__ res) {
     const long total = (long)M * N;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int m = (int)(i / N), n = (int)(i - (long)m * N);
         float v = 0.f;
         for (int s = 0; s < splits; ++s) v += part[s * split_stride + (long)m * ldc + n];
         if (bias) v += bias_bf16 ? bf2f(((const bf16_t*)bias)[n]) : ((const float*)bias)[n];
+        if (res) v += bf2f(res[(long)m * ldc + n]);
         if (act == ACT_DGELU) v *= gelu_erf_grad(bf2f(((const bf16_t*)aux)[(long)m * ldc + n]));
         else if (act != ACT_NONE) {
             if (aux) ((bf16_t*)aux)[(long)m * ldc + n] = f2bf(v);
@@ -426,7 +440,7 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
         const long total = (long)p.M * p.N;
         const int g = (int)std::min<long>(8192, (total + 255) / 256);
         gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.M, p.N, p.ldc, final_out, final_f32,
-                                          p.bias, p.bias_bf16, p.act, p.aux);
+                                          p.bias, p.bias_bf16, p.act, p.aux, p.res);
     }
     return (int)hipGetLastError();
 }
@@ -453,12 +467,14 @@ void fill_conv(ConvDesc& cd, const int* d) {
 // act: 0 none, 1 gelu (aux <- pre-activation if aux), 2 relu, 3 tanh, 4 dgelu (v *= gelu'(aux))
 DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                      int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
-                     float* workspace, long ws_elems, const int* conv, int row_remap, hipStream_t st) {
+                     float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
+                     hipStream_t st) {
     Params p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = aux; p.out_f32 = out_f32;
     p.row_remap = row_remap;
+    p.res = (const bf16_t*)res;
     if (conv) fill_conv(p.cd, conv);
     if (M <= 0 || N <= 0) return 0;
     switch (mode) {

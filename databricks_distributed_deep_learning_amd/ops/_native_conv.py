@@ -23,7 +23,7 @@ def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, 
     return [N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep, oa, ob]
 
 
-def _fwd(x, w, stride, pad):
+def _fwd(x, w, stride, pad, bias=None, act=None, residual=None):
     N, H, W_, C = x.shape
     K, R, S, _ = w.shape
     P = (H + 2 * pad - R) // stride + 1
@@ -31,9 +31,9 @@ def _fwd(x, w, stride, pad):
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
     M = N * P * Q
     if R == 1 and S == 1 and stride == 1 and pad == 0:
-        gemm(MODE_NT, x, C, w, C, y, K, M, K, C)
+        gemm(MODE_NT, x, C, w, C, y, K, M, K, C, bias=bias, act=act, residual=residual)
     else:
-        gemm(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C,
+        gemm(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C, bias=bias, act=act, residual=residual,
              conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q))
     return y
 
@@ -124,3 +124,14 @@ def conv2d(x, w, stride, padding):
     if w.shape[0] % 8:
         return conv2d_reference(x, w, stride, padding)
     return _Conv.apply(x, w, stride, padding)
+
+
+def conv2d_bias_act(x, w, b, stride, padding, relu=False, residual=None):
+    """Inference conv with the folded-BN bias, residual add and ReLU in the GEMM epilogue."""
+    C = x.shape[-1]
+    if C % 8:
+        c8 = (C + 7) // 8 * 8
+        x = F.pad(x, (0, c8 - C))
+        w = F.pad(w, (0, c8 - C))
+    res = residual.contiguous() if residual is not None else None
+    return _fwd(x.contiguous(), w.contiguous(), stride, padding, bias=b, act="relu" if relu else None, residual=res)

@@ -9,7 +9,7 @@ import torch
 from . import _lib
 from ._lib import I, L, P
 
-_lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P]})
+_lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
 ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4}
@@ -32,7 +32,8 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
 def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
          M: int, N: int, K: int, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
          aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
-         conv: Optional[Sequence[int]] = None, row_remap: bool = False) -> torch.Tensor:
+         conv: Optional[Sequence[int]] = None, row_remap: bool = False,
+         residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     out_f32 = 1 if C.dtype == torch.float32 else 0
     s = 1 if row_remap else pick_splits(M, N, K, splits)
     ws = None
@@ -44,7 +45,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
     rc = _lib.fn("ddl_gemm")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
                              _lib.p(bias), bias_bf16, ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws),
-                             0 if ws is None else ws.numel(), conv_arr, int(row_remap), _lib.stream())
+                             0 if ws is None else ws.numel(), conv_arr, int(row_remap), _lib.p(residual),
+                             _lib.stream())
     if rc != 0:
         raise RuntimeError(f"ddl_gemm(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
     return C

@@ -33,3 +33,22 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0) 
 
 def out_hw(h: int, w: int, k: int, stride: int, padding: int):
     return (h + 2 * padding - k) // stride + 1, (w + 2 * padding - k) // stride + 1
+
+
+def conv2d_bias_act_reference(x, w, b, stride=1, padding=0, relu=False, residual=None):
+    y = conv2d_reference(x.float(), w.float(), stride, padding)
+    if b is not None:
+        y = y + b.float()
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def conv2d_bias_act(x, w, b, stride=1, padding=0, relu=False, residual=None):
+    """Inference-only fused conv (+bias from folded BN) (+residual) (+ReLU)."""
+    if _lib.use_native(x) and x.dtype == torch.bfloat16 and w.shape[0] % 8 == 0:
+        from . import _native_conv
+        return _native_conv.conv2d_bias_act(x, w, b, stride, padding, relu, residual)
+    return conv2d_bias_act_reference(x, w, b, stride, padding, relu, residual)

@@ -146,7 +146,7 @@ def test_pools(dtype):
     g = torch.randn_like(yr)
     y.backward(g.to(dtype))
     yr.backward(g.to(dtype).float())
-    _close(x.grad, xr.grad, 1e-2 if dtype == torch.bfloat16 else 1e-6, 0, "maxpool bwd")
+    _close(x.grad, xr.grad, 1e-6, 1e-2 if dtype == torch.bfloat16 else 1e-6, "maxpool bwd")
     z = torch.randn(4, 7, 7, 256, device=dev).to(dtype).requires_grad_(True)
     zr = z.detach().float().requires_grad_(True)
     a = Pn.global_avg_pool(z)
@@ -196,8 +196,12 @@ def test_flat_optimizers_match_torch_path(name, pdtype):
         arena = ParamArena(list(m.named_parameters()))
         opt = build_optimizer(name, arena, cfg)
         g = torch.Generator(device=dev).manual_seed(7)
+        pad_mask = torch.zeros(arena.numel, dtype=torch.bool, device=dev)
+        for e in arena.entries:
+            pad_mask[e.offset:e.offset + e.numel] = True
         for _ in range(3):
-            arena.grad.copy_(torch.randn(arena.numel, generator=g, device=dev).to(pdtype))
+            # real gradients are zero in the alignment padding between tensors
+            arena.grad.copy_((torch.randn(arena.numel, generator=g, device=dev) * pad_mask).to(pdtype))
             opt.step(arena.grad, grad_scale=0.5)
         outs.append((opt.params32.clone(), arena.flat.clone()))
     _lib.set_mode("auto")
