@@ -50,7 +50,12 @@ def bench_gemm(results):
         dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
         dw = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
+        from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+        NG.set_big_gemm(False)
+        small = timeit(lambda: gemm(MODE_NT, a, K, w, K, c, N, M, N, K))
+        NG.set_big_gemm(True)
         rows = {
+            "fwd_ours128": small,
             "fwd_ours": timeit(lambda: gemm(MODE_NT, a, K, w, K, c, N, M, N, K)),
             "fwd_torch": timeit(lambda: torch.mm(a, w.t())),
             "dgrad_ours": timeit(lambda: gemm(MODE_NN, dy, N, w, K, dx, K, M, K, N)),

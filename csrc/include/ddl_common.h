@@ -150,3 +150,32 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
     uint32_t t = __umulhi(n, f.mul);
     return (t + n) >> f.shift;
 }
+
+// Column sum over the rows of a row-major fp32 matrix part[nrows][ld] (per-block
+// partials of a two-level reduction).  Block = 1024 threads = 64 columns x 16 row
+// groups; each lane keeps 4 independent loads in flight.  `red` holds 1024 floats.
+// Result valid in threads 0..63 (column `col` = the caller's column for lane t&63).
+__device__ __forceinline__ float colsum64(const float* __restrict__ part, int nrows, long ld, int col, bool ok,
+                                          float* red) {
+    const int grp = threadIdx.x >> 6;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (ok) {
+        int r = grp;
+        for (; r + 48 < nrows; r += 64) {
+            a0 += part[(long)r * ld + col];
+            a1 += part[(long)(r + 16) * ld + col];
+            a2 += part[(long)(r + 32) * ld + col];
+            a3 += part[(long)(r + 48) * ld + col];
+        }
+        for (; r < nrows; r += 16) a0 += part[(long)r * ld + col];
+    }
+    red[threadIdx.x] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    float s = 0.f;
+    if (threadIdx.x < 64) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s += red[i * 64 + threadIdx.x];
+    }
+    __syncthreads();
+    return s;
+}

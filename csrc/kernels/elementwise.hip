@@ -59,6 +59,7 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ x,
     const long r0 = (long)blockIdx.x * rows_per_blk;
     const long r1 = std::min<long>(rows, r0 + rows_per_blk);
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
     for (long r = r0; r < r1; ++r) {
         float v[8];
         load8(x + r * C + c0, v);
@@ -68,11 +69,12 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ x,
     store8(part + (long)blockIdx.x * C + c0, s);
 }
 template <typename TO>
-__global__ void colsum_final_k(const float* __restrict__ part, int nblk, int C, TO* __restrict__ out, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += part[(long)b * C + c];
+__global__ __launch_bounds__(1024) void colsum_final_k(const float* __restrict__ part, int nblk, int C,
+                                                       TO* __restrict__ out, int accumulate) {
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    float s = colsum64(part, nblk, C, c, c < C, red);
+    if (threadIdx.x >= 64 || c >= C) return;
     if (accumulate) s += to_f(out[c]);
     out[c] = from_f<TO>(s);
 }
@@ -300,7 +302,7 @@ DDL_API int ddl_dropout(int dtype, const void* x, void* y, long n, uint64_t seed
     DDL_RETURN_LAUNCH();
 }
 
-DDL_API int ddl_colsum_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(256, (rows + 63) / 64)); }
+DDL_API int ddl_colsum_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(1024, (rows + 15) / 16)); }
 
 // out[c] (+)= sum_r x[r, c]; `part` needs ddl_colsum_nblk(rows) * C floats.
 DDL_API int ddl_colsum(int dtype, const void* x, long rows, int C, float* part, void* out, int out_dtype,
@@ -311,8 +313,8 @@ DDL_API int ddl_colsum(int dtype, const void* x, long rows, int C, float* part, 
     dim3 g(nblk, (C / 8 + 255) / 256);
     DISPATCH_T(dtype, (colsum_partial_k<bf16_t><<<g, 256, 0, st>>>((const bf16_t*)x, rows, C, rpb, part)),
                (colsum_partial_k<float><<<g, 256, 0, st>>>((const float*)x, rows, C, rpb, part)));
-    if (out_dtype == 1) colsum_final_k<bf16_t><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, (bf16_t*)out, accumulate);
-    else colsum_final_k<float><<<(C + 255) / 256, 256, 0, st>>>(part, nblk, C, (float*)out, accumulate);
+    if (out_dtype == 1) colsum_final_k<bf16_t><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, (bf16_t*)out, accumulate);
+    else colsum_final_k<float><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, (float*)out, accumulate);
     DDL_RETURN_LAUNCH();
 }
 

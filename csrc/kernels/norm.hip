@@ -56,37 +56,16 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_partial_k(const T* __restrict_
     }
 }
 
-// Sum the per-block partials: block = 64 channels x 4 partial-row groups, so
-// each wave reads 64 consecutive floats per partial row (coalesced, independent
-// loads in flight) instead of one thread walking every partial serially.
-__device__ __forceinline__ void sum_partials_64(const float* __restrict__ part, int nblk, int C, int c, double& s,
-                                                double& q, double* red) {
-    const int grp = threadIdx.x >> 6;
-    double a = 0.0, b = 0.0;
-    if (c < C) {
-        for (int blk = grp; blk < nblk; blk += 4) {
-            a += part[(long)blk * 2 * C + c];
-            b += part[(long)blk * 2 * C + C + c];
-        }
-    }
-    red[threadIdx.x] = a;
-    red[256 + threadIdx.x] = b;
-    __syncthreads();
-    const int l = threadIdx.x & 63;
-    s = red[l] + red[64 + l] + red[128 + l] + red[192 + l];
-    q = red[256 + l] + red[320 + l] + red[384 + l] + red[448 + l];
-}
-
 template <typename TP>
-__global__ __launch_bounds__(256) void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+__global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
                                     const TP* __restrict__ gamma, const TP* __restrict__ beta,
                                     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum,
                                     float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                     float* __restrict__ scale, float* __restrict__ shift) {
-    __shared__ double red[512];
+    __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    double s, q;
-    sum_partials_64(part, nblk, C, c, s, q, red);
+    const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
+    const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
     if (threadIdx.x >= 64 || c >= C) return;
     const double mean = s / (double)M;
     double var = q / (double)M - mean * mean;
@@ -189,13 +168,13 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
 }
 
 template <typename TP>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
                                   const TP* __restrict__ gamma, const float* __restrict__ invstd,
                                   TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef) {
-    __shared__ double red[512];
+    __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    double s, q;
-    sum_partials_64(part, nblk, C, c, s, q, red);
+    const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
+    const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
     if (threadIdx.x >= 64 || c >= C) return;
     if (dgamma) dgamma[c] = from_f<TP>((float)q);
     if (dbeta) dbeta[c] = from_f<TP>((float)s);
@@ -348,15 +327,13 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
 }
 
 template <typename TP>
-__global__ void colsum_partials_k(const float* __restrict__ part, int nblk, int H, TP* __restrict__ dg,
-                                  TP* __restrict__ db) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= H) return;
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < nblk; ++i) {
-        a += part[(long)i * 2 * H + c];
-        b += part[(long)i * 2 * H + H + c];
-    }
+__global__ __launch_bounds__(1024) void colsum_partials_k(const float* __restrict__ part, int nblk, int H,
+                                                          TP* __restrict__ dg, TP* __restrict__ db) {
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const float a = colsum64(part, nblk, 2L * H, c, c < H, red);
+    const float b = colsum64(part, nblk, 2L * H, H + c, c < H, red);
+    if (threadIdx.x >= 64 || c >= H) return;
     dg[c] = from_f<TP>(a);
     db[c] = from_f<TP>(b);
 }
@@ -373,7 +350,7 @@ inline int grid_for(long n, int nt = 256, int cap = 4096) {
 
 DDL_API int ddl_bn_stats_nblk(long M, int C) {
     const int rpi = BN_NT / (C / 8);
-    long nblk = std::min<long>(1024, (M + rpi * 8 - 1) / (rpi * 8));
+    long nblk = std::min<long>(512, (M + rpi * 8 - 1) / (rpi * 8));
     return (int)std::max<long>(1, nblk);
 }
 
@@ -387,11 +364,11 @@ DDL_API int ddl_bn_fwd_train(int dtype, const void* x, long M, int C, const void
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (dtype == 1) {
         bn_stats_partial_k<bf16_t><<<nblk, BN_NT, 0, st>>>((const bf16_t*)x, M, C, (int)rpb, part);
-        bn_stats_finalize_k<bf16_t><<<(C + 63) / 64, 256, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
+        bn_stats_finalize_k<bf16_t><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
             (const bf16_t*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
     } else {
         bn_stats_partial_k<float><<<nblk, BN_NT, 0, st>>>((const float*)x, M, C, (int)rpb, part);
-        bn_stats_finalize_k<float><<<(C + 63) / 64, 256, 0, st>>>(part, nblk, C, M, (const float*)gamma,
+        bn_stats_finalize_k<float><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, (const float*)gamma,
             (const float*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
     }
     DDL_RETURN_LAUNCH();
@@ -440,7 +417,7 @@ static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float*
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
-    bn_bwd_finalize_k<T><<<(C + 63) / 64, 256, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef);
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef);
     const long n8 = M * C / 8;
     const int g = grid_for(n8, 256, 8192);
     if (relu) {
@@ -517,7 +494,7 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
         case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
         default: return -1;
     }
-    colsum_partials_k<T><<<(H + 255) / 256, 256, 0, st>>>(part, nblk, H, dg, db);
+    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(part, nblk, H, dg, db);
     return 0;
 }
 

@@ -9,7 +9,25 @@ import torch
 from . import _lib
 from ._lib import I, L, P
 
-_lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, P]})
+_lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, P],
+               "ddl_gemm_big": [P, L, P, L, P, L, I, I, I, P, I, I, P, P],
+               "ddl_gemm_big_supported": [I, I, I, L, L]})
+
+BIG_MIN_TILES = 64          # 256x256 tiles needed before the big kernel beats the 128x128 one
+_force_small = False
+
+
+def set_big_gemm(enabled: bool) -> None:
+    global _force_small
+    _force_small = not enabled
+
+
+def _use_big(mode, C, M, N, K, lda, ldb, splits, conv, row_remap, residual) -> bool:
+    if _force_small or mode != MODE_NT or C.dtype != torch.bfloat16 or splits is not None or conv is not None:
+        return False
+    if row_remap or residual is not None or K % 128 != 0:
+        return False
+    return (-(-M // 256)) * (-(-N // 256)) >= BIG_MIN_TILES
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
 ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4}
@@ -34,6 +52,13 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
          conv: Optional[Sequence[int]] = None, row_remap: bool = False,
          residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _use_big(mode, C, M, N, K, lda, ldb, splits, conv, row_remap, residual):
+        bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
+        rc = _lib.fn("ddl_gemm_big")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, _lib.p(bias),
+                                     bias_bf16, ACT[act], _lib.p(aux), _lib.stream())
+        if rc != 0:
+            raise RuntimeError(f"ddl_gemm_big(M={M}, N={N}, K={K}) failed: {rc}")
+        return C
     out_f32 = 1 if C.dtype == torch.float32 else 0
     s = 1 if row_remap else pick_splits(M, N, K, splits)
     ws = None

@@ -67,7 +67,11 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
-            gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
+            if N % 128 == 0 and M >= 4096:
+                # dgrad as an NT GEMM on the large-tile kernel: W^T is a tiny copy
+                gemm(MODE_NT, dz, N, w.t().contiguous(), N, dx, K, M, K, N)
+            else:
+                gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
             dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             dw = torch.empty(N, K, dtype=w.dtype, device=w.device)

@@ -94,3 +94,25 @@ def test_conv_fwd_bwd(N, H, W, C, K, R, stride, pad):
     yr.backward(g.to(torch.bfloat16).float())
     assert _rel_err(x.grad, xr.grad) < 2e-2
     assert _rel_err(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (4096, 2304, 768), (1000, 3000, 256), (16384, 768, 3072),
+                                   (300, 520, 384)])
+@pytest.mark.parametrize("act", [None, "gelu"])
+def test_big_gemm_nt(M, N, K, act):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _lib
+    torch.manual_seed(4)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    z = torch.empty_like(c) if act else None
+    rc = _lib.fn("ddl_gemm_big")(a.data_ptr(), K, w.data_ptr(), K, c.data_ptr(), N, M, N, K, b.data_ptr(), 1,
+                                 1 if act else 0, _lib.p(z), _lib.stream())
+    assert rc == 0
+    pre = a.float() @ w.float().t() + b.float()
+    ref = torch.nn.functional.gelu(pre) if act else pre
+    assert _rel_err(c, ref) < 1e-2
+    if act:
+        assert _rel_err(z, pre) < 1e-2
