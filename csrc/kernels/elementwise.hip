@@ -265,9 +265,9 @@ __global__ __launch_bounds__(256) void embed_bwd_k(const int64_t* __restrict__ i
     }
 }
 template <typename TO>
-__global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ x, TO* __restrict__ y, long n) {
+__global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ x, TO* __restrict__ y, long n, int acc) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-        y[i] = from_f<TO>(x[i]);
+        y[i] = from_f<TO>(x[i] + (acc ? to_f(y[i]) : 0.f));
 }
 
 }  // namespace
@@ -380,12 +380,12 @@ DDL_API int ddl_embedding_fwd(int dtype, const int64_t* ids, const void* w, void
 }
 // acc must be zeroed (fp32 [V, D]); then cast into dw (dtype) of V*D elements.
 DDL_API int ddl_embedding_bwd(int dtype, const int64_t* ids, const void* dy, float* acc, void* dw, long n_tok, long V,
-                              int D, hipStream_t st) {
+                              int D, int accumulate, hipStream_t st) {
     const long tot = n_tok * D;
     DISPATCH_T(dtype, (embed_bwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>(ids, (const bf16_t*)dy, acc, n_tok, D)),
                (embed_bwd_k<float><<<grid_for(tot), 256, 0, st>>>(ids, (const float*)dy, acc, n_tok, D)));
     const long n = V * D;
-    DISPATCH_T(dtype, (cast_f32_k<bf16_t><<<grid_for(n), 256, 0, st>>>(acc, (bf16_t*)dw, n)),
-               (cast_f32_k<float><<<grid_for(n), 256, 0, st>>>(acc, (float*)dw, n)));
+    DISPATCH_T(dtype, (cast_f32_k<bf16_t><<<grid_for(n), 256, 0, st>>>(acc, (bf16_t*)dw, n, accumulate)),
+               (cast_f32_k<float><<<grid_for(n), 256, 0, st>>>(acc, (float*)dw, n, accumulate)));
     DDL_RETURN_LAUNCH();
 }

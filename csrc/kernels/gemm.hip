@@ -59,6 +59,7 @@ struct Params {
     long split_stride;
     int row_remap;    // conv output rows -> strided output pixels
     const bf16_t* res;  // optional residual added before the activation (same layout as C)
+    int accumulate;     // C += result (gradient accumulation straight into the parameter-grad arena)
     ConvDesc cd;
     int tiles_m, tiles_n;
 };
@@ -374,6 +375,26 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
             }
+            if (p.accumulate) {
+                float o[4] = {0.f, 0.f, 0.f, 0.f};
+                if (p.out_f32) {
+                    const float* c = (const float*)p.C + orow * p.ldc + n;
+                    if (full) load4(c, o);
+                    else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) if (n + r < p.N) o[r] = c[r];
+                    }
+                } else {
+                    const bf16_t* c = (const bf16_t*)p.C + orow * p.ldc + n;
+                    if (full) load4(c, o);
+                    else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) if (n + r < p.N) o[r] = bf2f(c[r]);
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += o[r];
+            }
             if (p.out_f32) {
                 float* c = (float*)p.C + orow * p.ldc + n;
                 if (full) store4(c, v);
@@ -397,7 +418,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
 __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ part, int splits, long split_stride,
                                                      int M, int N, long ldc, void* out, int out_f32,
                                                      const void* bias, int bias_bf16, int act, void* aux,
-                                                     const bf16_t* __restrict__ res) {
+                                                     const bf16_t* __restrict__ res, int accumulate) {
     const long total = (long)M * N;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int m = (int)(i / N), n = (int)(i - (long)m * N);
@@ -410,6 +431,7 @@ __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ p
             if (aux) ((bf16_t*)aux)[(long)m * ldc + n] = f2bf(v);
             v = apply_act(v, act);
         }
+        if (accumulate) v += out_f32 ? ((float*)out)[(long)m * ldc + n] : bf2f(((bf16_t*)out)[(long)m * ldc + n]);
         if (out_f32) ((float*)out)[(long)m * ldc + n] = v;
         else ((bf16_t*)out)[(long)m * ldc + n] = f2bf(v);
     }
@@ -427,12 +449,15 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
     p.splits = splits;
     void* final_out = p.C;
     const int final_f32 = p.out_f32;
+    int acc_final = 0;
     if (splits > 1) {
         p.split_stride = (long)p.M * p.ldc;
         if (!workspace || ws_elems < p.split_stride * splits) return -2;
         if (p.row_remap) return -3;
         p.C = workspace;
         p.out_f32 = 1;
+        acc_final = p.accumulate;
+        p.accumulate = 0;
     }
     dim3 grid(p.tiles_m * p.tiles_n, splits);
     hipLaunchKernelGGL((gemm_k<LA, LB>), grid, dim3(NT), 0, st, p);
@@ -440,7 +465,7 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
         const long total = (long)p.M * p.N;
         const int g = (int)std::min<long>(8192, (total + 255) / 256);
         gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.M, p.N, p.ldc, final_out, final_f32,
-                                          p.bias, p.bias_bf16, p.act, p.aux, p.res);
+                                          p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final);
     }
     return (int)hipGetLastError();
 }
@@ -468,13 +493,14 @@ void fill_conv(ConvDesc& cd, const int* d) {
 DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                      int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
                      float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
-                     hipStream_t st) {
+                     int accumulate, hipStream_t st) {
     Params p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = aux; p.out_f32 = out_f32;
     p.row_remap = row_remap;
     p.res = (const bf16_t*)res;
+    p.accumulate = accumulate;
     if (conv) fill_conv(p.cd, conv);
     if (M <= 0 || N <= 0) return 0;
     switch (mode) {

@@ -42,6 +42,7 @@ struct BigParams {
     int bias_bf16;
     int act;
     bf16_t* aux;
+    int accumulate;
     int tiles_m, tiles_n;
 };
 
@@ -245,6 +246,16 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
                         for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], p.act);
                     }
                     bf16_t* cp = p.C + (long)m * p.ldc + n;
+                    if (p.accumulate) {
+                        float o[4] = {0.f, 0.f, 0.f, 0.f};
+                        if (full) load4(cp, o);
+                        else {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) if (n + r < p.N) o[r] = bf2f(cp[r]);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] += o[r];
+                    }
                     if (full) store4(cp, v);
                     else {
 #pragma unroll
@@ -262,12 +273,13 @@ DDL_API int ddl_gemm_big_supported(int M, int N, int K, long lda, long ldb) {
 
 // C = A . B^T (+bias)(act: 0 none, 1 gelu (aux <- pre-activation), 2 relu, 3 tanh); bf16 in/out
 DDL_API int ddl_gemm_big(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                         const void* bias, int bias_bf16, int act, void* aux, hipStream_t st) {
+                         const void* bias, int bias_bf16, int act, void* aux, int accumulate, hipStream_t st) {
     if (!ddl_gemm_big_supported(M, N, K, lda, ldb)) return -1;
     BigParams p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = (bf16_t*)C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = (bf16_t*)aux;
+    p.accumulate = accumulate;
     p.tiles_m = (M + TB - 1) / TB;
     p.tiles_n = (N + TB - 1) / TB;
     hipLaunchKernelGGL(gemm_big_k, dim3(p.tiles_m * p.tiles_n), dim3(NTH), 0, st, p);

@@ -170,14 +170,15 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
 template <typename TP>
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
                                   const TP* __restrict__ gamma, const float* __restrict__ invstd,
-                                  TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef) {
+                                  TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef,
+                                  int acc) {
     __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
     const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
     if (threadIdx.x >= 64 || c >= C) return;
-    if (dgamma) dgamma[c] = from_f<TP>((float)q);
-    if (dbeta) dbeta[c] = from_f<TP>((float)s);
+    if (dgamma) dgamma[c] = from_f<TP>((float)q + (acc ? to_f(dgamma[c]) : 0.f));
+    if (dbeta) dbeta[c] = from_f<TP>((float)s + (acc ? to_f(dbeta[c]) : 0.f));
     const float g = gamma ? to_f(gamma[c]) : 1.f;
     coef[c] = g * invstd[c];                 // k1
     coef[C + c] = (float)(s / (double)M);    // mean(dz)
@@ -328,14 +329,14 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
 
 template <typename TP>
 __global__ __launch_bounds__(1024) void colsum_partials_k(const float* __restrict__ part, int nblk, int H,
-                                                          TP* __restrict__ dg, TP* __restrict__ db) {
+                                                          TP* __restrict__ dg, TP* __restrict__ db, int acc) {
     __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     const float a = colsum64(part, nblk, 2L * H, c, c < H, red);
     const float b = colsum64(part, nblk, 2L * H, H + c, c < H, red);
     if (threadIdx.x >= 64 || c >= H) return;
-    dg[c] = from_f<TP>(a);
-    db[c] = from_f<TP>(b);
+    dg[c] = from_f<TP>(a + (acc ? to_f(dg[c]) : 0.f));
+    db[c] = from_f<TP>(b + (acc ? to_f(db[c]) : 0.f));
 }
 
 inline int grid_for(long n, int nt = 256, int cap = 4096) {
@@ -410,14 +411,14 @@ DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float*
 template <typename T>
 static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float* mean, const float* invstd,
                             const T* gamma, long M, int C, int relu, float* part, T* dgamma, T* dbeta, float* coef,
-                            T* dx, T* dres, hipStream_t st) {
+                            T* dx, T* dres, int acc, hipStream_t st) {
     const int nblk = ddl_bn_stats_nblk(M, C);
     const int rpi = BN_NT / (C / 8);
     long rpb = (M + nblk - 1) / nblk;
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
-    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef);
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
     const long n8 = M * C / 8;
     const int g = grid_for(n8, 256, 8192);
     if (relu) {
@@ -431,14 +432,14 @@ static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float*
 
 DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* yout, const void* x, const float* mean,
                        const float* invstd, const void* gamma, long M, int C, int relu, float* part, void* dgamma,
-                       void* dbeta, float* coef, void* dx, void* dres, hipStream_t st) {
+                       void* dbeta, float* coef, void* dx, void* dres, int acc_params, hipStream_t st) {
     if (C % 8 || (BN_NT % (C / 8) != 0)) return -1;
     if (dtype == 1)
         bn_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)yout, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M,
-                        C, relu, part, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, st);
+                        C, relu, part, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
     else
         bn_bwd_dispatch((const float*)dy, (const float*)yout, (const float*)x, mean, invstd, (const float*)gamma, M, C,
-                        relu, part, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, st);
+                        relu, part, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st);
     DDL_RETURN_LAUNCH();
 }
 
@@ -481,7 +482,8 @@ DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<
 
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
-                           const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, hipStream_t st) {
+                           const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, int acc,
+                           hipStream_t st) {
     const int nblk = ddl_ln_bwd_nblk(rows);
     const int rpb = (int)((rows + nblk - 1) / nblk);
     switch (H / 256) {
@@ -494,20 +496,20 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
         case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
         default: return -1;
     }
-    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(part, nblk, H, dg, db);
+    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(part, nblk, H, dg, db, acc);
     return 0;
 }
 
 DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res, long res_rows, const void* g,
                        const float* mean, const float* rstd, void* dx, float* part, void* dg, void* db, long rows, int H,
-                       hipStream_t st) {
+                       int acc_params, hipStream_t st) {
     if (!ddl_ln_supported(H)) return -1;
     if (res_rows <= 0) res_rows = rows;
     int rc = dtype == 1
                  ? ln_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
-                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, st)
+                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, st)
                  : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
-                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, st);
+                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, st);
     if (rc) return rc;
     DDL_RETURN_LAUNCH();
 }

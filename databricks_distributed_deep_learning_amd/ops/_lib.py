@@ -110,11 +110,11 @@ _SIGS = {
     "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],
     "ddl_bn_eval_coeffs": [I, I, P, P, P, P, F, P, P, P],
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P],
-    "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, P],
+    "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_ln_supported": [I],
     "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, P],
     "ddl_ln_bwd_nblk": [L],
-    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, P],
+    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P],
     # elementwise.hip
     "ddl_gelu_fwd": [I, P, P, L, P],
     "ddl_gelu_bwd": [I, P, P, P, L, P],
@@ -128,7 +128,7 @@ _SIGS = {
     "ddl_avgpool_fwd": [I, P, P, I, I, I, P],
     "ddl_avgpool_bwd": [I, P, P, I, I, I, P],
     "ddl_embedding_fwd": [I, P, P, P, L, I, P],
-    "ddl_embedding_bwd": [I, P, P, P, P, L, L, I, P],
+    "ddl_embedding_bwd": [I, P, P, P, P, L, L, I, I, P],
     # optim.hip
     "ddl_sgd_step": [I, P, P, I, P, P, P, I, P, F, F, F, I, I, P],
     "ddl_adamw_step": [I, P, P, I, P, P, P, P, I, P, F, F, F, F, F, F, F, P],
@@ -172,3 +172,21 @@ def dcode(t: torch.Tensor) -> int:
 
 def p(t: Optional[torch.Tensor]) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------ gradient sinks
+# When a DataParallel reducer owns a parameter's gradient (a view into the flat
+# gradient arena), the native backward kernels accumulate the weight gradient
+# straight into that view in their epilogue and signal readiness to the reducer,
+# instead of returning a tensor that autograd would add into the arena with an
+# extra elementwise kernel per parameter.
+def grad_sink(param) -> Optional[torch.Tensor]:
+    if param is None:
+        return None
+    return getattr(param, "_ddl_main_grad", None)
+
+
+def grad_ready(param) -> None:
+    cb = getattr(param, "_ddl_grad_ready", None)
+    if cb is not None:
+        cb()

@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ._lib import grad_ready, grad_sink
 from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm
 
 
@@ -77,16 +78,17 @@ def _dgrad(dy, w, x_shape, stride, pad):
     return dx
 
 
-def _wgrad(dy, x, w_shape, stride, pad):
+def _wgrad(dy, x, w_shape, stride, pad, out=None):
     N, H, W_, C = x.shape
     K, R, S, _ = w_shape
     _, P, Q, _ = dy.shape
-    dw = torch.empty(K, R, S, C, dtype=dy.dtype, device=dy.device)
+    acc = out is not None
+    dw = out if acc else torch.empty(K, R, S, C, dtype=dy.dtype, device=dy.device)
     M = N * P * Q
     if R == 1 and S == 1 and stride == 1 and pad == 0:
-        gemm(MODE_TN, dy, K, x, C, dw, C, K, C, M)
+        gemm(MODE_TN, dy, K, x, C, dw, C, K, C, M, accumulate=acc)
     else:
-        gemm(MODE_CONVW, dy, K, x, 0, dw, R * S * C, K, R * S * C, M,
+        gemm(MODE_CONVW, dy, K, x, 0, dw, R * S * C, K, R * S * C, M, accumulate=acc,
              conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q))
     return dw
 
@@ -94,6 +96,7 @@ def _wgrad(dy, x, w_shape, stride, pad):
 class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad):
+        ctx.w_param = w
         x = x.contiguous()
         w = w.contiguous()
         ctx.stride, ctx.pad = stride, pad
@@ -108,7 +111,12 @@ class _Conv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad)
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
+            sink = grad_sink(ctx.w_param)
+            if sink is not None and sink.shape == w.shape:
+                _wgrad(dy, x, w.shape, ctx.stride, ctx.pad, out=sink)
+                grad_ready(ctx.w_param)
+            else:
+                dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
         return dx, dw, None, None
 
 

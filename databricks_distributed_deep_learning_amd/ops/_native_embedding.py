@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import call, dcode, p
+from ._lib import call, dcode, grad_ready, grad_sink, p
 
 
 class _Embedding(torch.autograd.Function):
@@ -14,6 +14,7 @@ class _Embedding(torch.autograd.Function):
         y = torch.empty(*ids.shape, D, dtype=weight.dtype, device=weight.device)
         call("ddl_embedding_fwd", dcode(weight), p(ids), p(weight), p(y), ids.numel(), D)
         ctx.save_for_backward(ids)
+        ctx.w_param = weight
         ctx.wshape = (V, D)
         ctx.wdtype = weight.dtype
         return y
@@ -24,8 +25,12 @@ class _Embedding(torch.autograd.Function):
         V, D = ctx.wshape
         dy = dy.contiguous()
         acc = torch.zeros(V, D, dtype=torch.float32, device=dy.device)
-        dw = torch.empty(V, D, dtype=ctx.wdtype, device=dy.device)
-        call("ddl_embedding_bwd", dcode(dy), p(ids), p(dy), p(acc), p(dw), ids.numel(), V, D)
+        sink = grad_sink(ctx.w_param)
+        dw = sink if sink is not None else torch.empty(V, D, dtype=ctx.wdtype, device=dy.device)
+        call("ddl_embedding_bwd", dcode(dy), p(ids), p(dy), p(acc), p(dw), ids.numel(), V, D, int(sink is not None))
+        if sink is not None:
+            grad_ready(ctx.w_param)
+            return None, None
         return None, dw
 
 

@@ -9,8 +9,8 @@ import torch
 from . import _lib
 from ._lib import I, L, P
 
-_lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, P],
-               "ddl_gemm_big": [P, L, P, L, P, L, I, I, I, P, I, I, P, P],
+_lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P],
+               "ddl_gemm_big": [P, L, P, L, P, L, I, I, I, P, I, I, P, I, P],
                "ddl_gemm_big_supported": [I, I, I, L, L]})
 
 BIG_MIN_TILES = 64          # 256x256 tiles needed before the big kernel beats the 128x128 one
@@ -51,11 +51,11 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          M: int, N: int, K: int, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
          aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
          conv: Optional[Sequence[int]] = None, row_remap: bool = False,
-         residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+         residual: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
     if _use_big(mode, C, M, N, K, lda, ldb, splits, conv, row_remap, residual):
         bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
         rc = _lib.fn("ddl_gemm_big")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, _lib.p(bias),
-                                     bias_bf16, ACT[act], _lib.p(aux), _lib.stream())
+                                     bias_bf16, ACT[act], _lib.p(aux), int(accumulate), _lib.stream())
         if rc != 0:
             raise RuntimeError(f"ddl_gemm_big(M={M}, N={N}, K={K}) failed: {rc}")
         return C
@@ -71,7 +71,7 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
     rc = _lib.fn("ddl_gemm")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
                              _lib.p(bias), bias_bf16, ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws),
                              0 if ws is None else ws.numel(), conv_arr, int(row_remap), _lib.p(residual),
-                             _lib.stream())
+                             int(accumulate), _lib.stream())
     if rc != 0:
         raise RuntimeError(f"ddl_gemm(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
     return C

@@ -14,7 +14,7 @@ from typing import Optional
 
 import torch
 
-from ._lib import call, dcode, p
+from ._lib import call, dcode, grad_ready, grad_sink, p
 from ._native_gemm import MODE_NN, MODE_NT, MODE_TN, gemm
 from . import _native_elementwise as E
 
@@ -29,6 +29,7 @@ def _ok(x, w) -> bool:
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act):
+        ctx.w_param, ctx.b_param = w, b
         K = x.shape[-1]
         N = w.shape[0]
         x2 = x.reshape(-1, K)
@@ -74,11 +75,21 @@ class _Linear(torch.autograd.Function):
                 gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
             dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
-            gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
+            sink = grad_sink(ctx.w_param)
+            if sink is not None:       # accumulate straight into the reducer's gradient arena
+                gemm(MODE_TN, dz, N, x2, K, sink, K, N, K, M, accumulate=True)
+                grad_ready(ctx.w_param)
+            else:
+                dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
+                gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.empty(N, dtype=w.dtype, device=w.device)
-            E.colsum(dz, db)
+            sink = grad_sink(ctx.b_param)
+            if sink is not None:
+                E.colsum(dz, sink, accumulate=True)
+                grad_ready(ctx.b_param)
+            else:
+                db = torch.empty(N, dtype=w.dtype, device=w.device)
+                E.colsum(dz, db)
         return dx, dw, db, None
 
 

@@ -6,7 +6,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import call, dcode, p
+from ._lib import call, dcode, grad_ready, grad_sink, p
 
 
 def _bn_supported(C: int) -> bool:
@@ -31,6 +31,7 @@ class _BatchNormTrain(torch.autograd.Function):
         call("ddl_bn_apply", dt, p(x), p(res), p(stats[2]), p(stats[3]), p(y), x.numel(), C, int(relu))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
+        ctx.params = (weight, bias)
         ctx.save_for_backward(x, y if relu else None, weight, stats)
         return y
 
@@ -46,10 +47,19 @@ class _BatchNormTrain(torch.autograd.Function):
         coef = torch.empty(3 * C, **f32)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        dgamma = torch.empty_like(weight) if weight is not None else None
-        dbeta = torch.empty_like(weight) if weight is not None else None
+        sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
+        direct = sg is not None and sb is not None
+        if direct:
+            dgamma, dbeta = sg, sb
+        else:
+            dgamma = torch.empty_like(weight) if weight is not None else None
+            dbeta = torch.empty_like(weight) if weight is not None else None
         call("ddl_bn_bwd", dcode(x), p(dy), p(y), p(x), p(stats[0]), p(stats[1]), p(weight), M, C, int(ctx.relu),
-             p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres))
+             p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+        if direct:
+            grad_ready(ctx.params[0])
+            grad_ready(ctx.params[1])
+            dgamma = dbeta = None
         return dx, dgamma, dbeta, None, None, None, None, None, dres
 
 
@@ -99,6 +109,7 @@ class _LayerNorm(torch.autograd.Function):
         call("ddl_ln_fwd", dcode(x), p(x), p(res), res_rows, p(weight), p(bias), p(y), p(stats[0]), p(stats[1]),
              rows, H, float(eps))
         ctx.res_shape = residual.shape if residual is not None else None
+        ctx.params = (weight, bias)
         ctx.res_rows = res_rows
         ctx.save_for_backward(x, res, weight, stats)
         return y
@@ -112,10 +123,15 @@ class _LayerNorm(torch.autograd.Function):
         nblk = _lib.fn("ddl_ln_bwd_nblk")(rows)
         part = torch.empty(nblk * 2 * H, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
-        dg = torch.empty_like(weight)
-        db = torch.empty_like(weight)
+        sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
+        direct = sg is not None and sb is not None
+        dg, db = (sg, sb) if direct else (torch.empty_like(weight), torch.empty_like(weight))
         call("ddl_ln_bwd", dcode(x), p(dy), p(x), p(res), ctx.res_rows, p(weight), p(stats[0]), p(stats[1]), p(dx),
-             p(part), p(dg), p(db), rows, H)
+             p(part), p(dg), p(db), rows, H, int(direct))
+        if direct:
+            grad_ready(ctx.params[0])
+            grad_ready(ctx.params[1])
+            dg = db = None
         dres = None
         if ctx.res_shape is not None:
             if ctx.res_rows == rows:

@@ -80,7 +80,11 @@ class DataParallel(nn.Module):
                 self._entry_bucket[ei] = b.index
         self._hooks = []
         for ei, e in enumerate(self.arena.entries):
-            self._hooks.append(e.param.register_post_accumulate_grad_hook(self._make_hook(ei)))
+            hook = self._make_hook(ei)
+            self._hooks.append(e.param.register_post_accumulate_grad_hook(hook))
+            # native backward kernels accumulate straight into the arena view and call this
+            e.param._ddl_main_grad = self.arena.grad[e.offset:e.offset + e.numel].view(e.shape)
+            e.param._ddl_grad_ready = (lambda h=hook, prm=e.param: h(prm))
         self._reset()
 
     # ------------------------------------------------------------------
