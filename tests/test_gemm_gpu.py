@@ -109,7 +109,7 @@ def test_big_gemm_nt(M, N, K, act):
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     z = torch.empty_like(c) if act else None
     rc = _lib.fn("ddl_gemm_big")(a.data_ptr(), K, w.data_ptr(), K, c.data_ptr(), N, M, N, K, b.data_ptr(), 1,
-                                 1 if act else 0, _lib.p(z), _lib.stream())
+                                 1 if act else 0, _lib.p(z), 0, _lib.stream())
     assert rc == 0
     pre = a.float() @ w.float().t() + b.float()
     ref = torch.nn.functional.gelu(pre) if act else pre
