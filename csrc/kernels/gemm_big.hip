@@ -1,13 +1,20 @@
-// Large-tile bf16 GEMM for gfx950: C[M,N] = A[M,K] . B[N,K]^T (+bias)(act), the
-// "NT" shape of every Linear forward (and of dgrad once W^T is materialised).
+// Large-tile bf16 GEMM / implicit-GEMM convolution for gfx950 (kernel families K1/K2/K3/K9/K13).
+//
+//   C[m][n] (+)= sum_k A(m,k) * B(n,k)  (+bias[n]) (+residual) (activation)
+//
+// Same operand-loader vocabulary as gemm.hip (KC: reduction-contiguous, KO:
+// reduction-outer, CONV / CONVW: implicit im2col of an NHWC tensor), so every
+// Linear / conv GEMM of fwd, dgrad and wgrad runs here without transposes.
 //
 // Structure (the CDNA4 256x256 8-phase schedule):
 //   * block tile 256x256, BK = 64, 8 wave64 (512 threads) as 2 (M) x 4 (N);
 //     each wave owns a 128x64 output tile held as four 64x32 quadrants
 //     (8 v_mfma_f32_16x16x32_bf16 accumulators each = 128 accumulator VGPRs);
-//   * operands reach LDS by global_load_lds (LDS-DMA, 16 B per lane, no VGPR
-//     staging); a K-tile is four 16 KB half-tiles (A rows 0-127 / 128-255,
-//     B rows 0-127 / 128-255), two LDS buffers = 128 KB;
+//   * operands reach LDS by global_load_lds (LDS-DMA, 16 B per lane, per-lane
+//     source address -> gathers for free; out-of-range lanes read a 16-byte zero
+//     page, which is how padding pixels, K tails and M/N tails become zeros);
+//     a K-tile is four 16 KB half-tiles (A rows 0-127 / 128-255, B rows 0-127 /
+//     128-255), two LDS buffers = 128 KB;
 //   * every K-tile is computed in 4 phases, one quadrant each:
 //       {ds_read the new fragments, issue one half-tile prefetch,
 //        s_barrier, lgkmcnt(0), 16 MFMA (setprio 1), s_barrier};
@@ -16,12 +23,14 @@
 //   * wave quadrants are interleaved (rows wm*64 and 128+wm*64, cols wn*32 and
 //     128+wn*32) so each phase reads exactly one A half and/or one B half, which
 //     is what lets a half-tile be restaged one phase after its last read;
-//   * LDS images are 16x32 subtiles of 1 KB with the st_16x32 swizzle (byte bit
-//     5 ^= bit 9) applied on the glds SOURCE address and on the ds_read, so the
-//     DMA image stays lane-linear and fragment reads are conflict-free;
-//   * XCD-aware bijective block remap; bias / GELU / ReLU / tanh epilogue from
-//     the fp32 accumulators (GELU also stores the pre-activation for backward).
-// Requirements (checked by the host): K % 128 == 0, lda/ldb % 8 == 0, 16-B aligned.
+//   * LDS images: reduction-contiguous operands as 16x32 subtiles of 1 KB with
+//     the st_16x32 swizzle (byte bit 5 ^= bit 9), read by ds_read_b128;
+//     reduction-outer operands as [64 k][128] rows of 256 B with an XOR chunk
+//     swizzle, read by ds_read_b64_tr_b16 (hardware transpose).  Both swizzles
+//     are applied on the DMA SOURCE address and on the read, so the DMA image
+//     stays lane-linear and every fragment read is conflict-free;
+//   * split-K over blockIdx.y with fp32 partial slabs reduced (with the
+//     epilogue) by a second kernel; XCD-aware bijective block remap.
 #include "ddl_common.h"
 
 namespace {
@@ -29,50 +38,175 @@ namespace {
 constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
 
+enum Layout { KC = 0, KO = 1, CONV = 2, CONVW = 3 };
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4 };
+
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_v4;
+
+struct ConvDesc {
+    int N, H, W, C;
+    int P, Q;
+    int stride, h_off, w_off, h_step, w_step;
+    int R, S;
+    FastDiv fd_PQ, fd_Q, fd_C, fd_S;
+    int OH, OW, ostep, oa, ob;
+};
 
 struct BigParams {
     const bf16_t* A;
     const bf16_t* B;
     long lda, ldb;
-    bf16_t* C;
+    void* C;
     long ldc;
     int M, N, K;
     const void* bias;
     int bias_bf16;
     int act;
     bf16_t* aux;
+    const bf16_t* res;
     int accumulate;
+    int out_f32;
+    int splits, kt_per_split;
+    long split_stride;
+    int row_remap;
+    const bf16_t* zero;       // >= 16 zero bytes
+    ConvDesc cd;
     int tiles_m, tiles_n;
 };
 
 __device__ __forceinline__ int half_off(int buf, int x, int h) { return ((buf * 2 + x) * 2 + h) * HALF; }
+__device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
+__device__ __forceinline__ int swz_ko(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
-__device__ __forceinline__ int swz(int b) { return b ^ (((b >> 9) & 1) << 5); }
-
-// Issue the LDS-DMA of half-tile h of operand x (0 = A, 1 = B) for K-tile kt into buffer buf.
-__device__ __forceinline__ void stage(const BigParams& p, char* smem, int buf, int x, int h, int kt, int r0tile) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const bf16_t* base = x ? p.B : p.A;
-    const long ld = x ? p.ldb : p.lda;
-    const int rows = x ? p.N : p.M;
-    const int lb = swz(l * 16);           // logical byte this lane's DMA slot holds
-    const int r = lb >> 6, c = (lb >> 4) & 3;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int sub = w * 2 + j;       // 16 subtiles of 16 rows x 32 k
-        const int rb = sub >> 1, kb = sub & 1;
-        int row = r0tile + h * 128 + rb * 16 + r;
-        row = row < rows ? row : rows - 1;
-        const bf16_t* g = base + (long)row * ld + (long)kt * BK + kb * 32 + c * 8;
-        __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(smem + half_off(buf, x, h) + sub * 1024), 16, 0, 0);
-    }
+__device__ __forceinline__ void glds(const bf16_t* g, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 0);
 }
 
-__device__ __forceinline__ bf16x8 frag(const char* smem, int buf, int x, int h, int rb, int kb) {
+// pixel decomposition of a GEMM row m (conv): image pointer + top-left input coords
+struct Pix {
+    const bf16_t* img;
+    int hb, wb;
+    bool ok;
+};
+__device__ __forceinline__ Pix decompose(const ConvDesc& cd, const bf16_t* base, int m, int mlimit) {
+    Pix px;
+    px.ok = m < mlimit;
+    const int mm = px.ok ? m : 0;
+    const int n = (int)fdiv((uint32_t)mm, cd.fd_PQ);
+    const int rem = mm - n * cd.P * cd.Q;
+    const int pp = (int)fdiv((uint32_t)rem, cd.fd_Q);
+    const int qq = rem - pp * cd.Q;
+    px.hb = pp * cd.stride + cd.h_off;
+    px.wb = qq * cd.stride + cd.w_off;
+    px.img = base + (long)n * cd.H * cd.W * cd.C;
+    return px;
+}
+__device__ __forceinline__ void tap_of(const ConvDesc& cd, int k, int& dh, int& dw, int& ci) {
+    const int tap = (int)fdiv((uint32_t)k, cd.fd_C);
+    ci = k - tap * cd.C;
+    const int rr = (int)fdiv((uint32_t)tap, cd.fd_S);
+    const int ss = tap - rr * cd.S;
+    dh = rr * cd.h_step;
+    dw = ss * cd.w_step;
+}
+
+// ------------------------------------------------------------------ operand staging
+template <int L, bool IS_A>
+struct Stager {
+    const bf16_t* base;
+    long ld;
+    int rows;        // extent of this operand's M (A) / N (B) side
+    int K;
+    int r0;          // tile origin on the M / N side
+    Pix px[2];       // CONV: this lane's row in half 0 / half 1
+
+    __device__ __forceinline__ void init(const BigParams& p, int origin) {
+        base = IS_A ? p.A : p.B;
+        ld = IS_A ? p.lda : p.ldb;
+        rows = IS_A ? p.M : p.N;
+        K = p.K;
+        r0 = origin;
+        if (L == CONV) {
+            const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+            const int r = swz_kc(l * 16) >> 6;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) px[h] = decompose(p.cd, base, r0 + h * 128 + w * 16 + r, rows);
+        }
+    }
+
+    // half-tile h of K-tile kt; tiles at or past kt_end are all zeros
+    __device__ __forceinline__ void stage(const BigParams& p, char* smem, int buf, int h, int kt, int kt_end) {
+        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        char* hbase = smem + half_off(buf, IS_A ? 0 : 1, h);
+        const bool tile_ok = kt < kt_end;
+        if (L == KC || L == CONV) {
+            const int lb = swz_kc(l * 16);
+            const int r = lb >> 6, c = (lb >> 4) & 3;
+            const int row = r0 + h * 128 + w * 16 + r;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int k = kt * BK + j * 32 + c * 8;
+                const bf16_t* g = p.zero;
+                if (L == KC) {
+                    if (tile_ok && row < rows && k < K) g = base + (long)row * ld + k;
+                } else {
+                    int dh, dw, ci;
+                    tap_of(p.cd, k < K ? k : 0, dh, dw, ci);
+                    const Pix& x = px[h];
+                    const int hh = x.hb + dh, ww = x.wb + dw;
+                    if (tile_ok && x.ok && k < K && (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W)
+                        g = x.img + ((long)hh * p.cd.W + ww) * p.cd.C + ci;
+                }
+                glds(g, hbase + (w * 2 + j) * 1024);
+            }
+        } else {
+            const int pc = l & 15;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int krow = (w * 2 + j) * 4 + (l >> 4);
+                const int c = pc ^ swz_ko(krow);
+                const int col = r0 + h * 128 + 8 * c;
+                const int k = kt * BK + krow;
+                const bf16_t* g = p.zero;
+                if (L == KO) {
+                    if (tile_ok && k < K && col < rows) g = base + (long)k * ld + col;
+                } else {   // CONVW: reduction rows are output pixels, columns are (tap, channel)
+                    if (tile_ok && k < K && col < rows) {
+                        int dh, dw, ci;
+                        tap_of(p.cd, col, dh, dw, ci);
+                        const Pix x = decompose(p.cd, base, k, K);
+                        const int hh = x.hb + dh, ww = x.wb + dw;
+                        if ((unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W)
+                            g = x.img + ((long)hh * p.cd.W + ww) * p.cd.C + ci;
+                    }
+                }
+                glds(g, hbase + (w * 2 + j) * 1024);
+            }
+        }
+    }
+};
+
+// fragment: operand rows rbase..rbase+15 of half h, k = 32 kk + 8 (lane>>4) + 0..7
+template <int L>
+__device__ __forceinline__ bf16x8 frag(const char* hbase, int rbase, int kk) {
     const int l = threadIdx.x & 63;
-    const int pb = swz((l & 15) * 64 + (l >> 4) * 16);
-    return *reinterpret_cast<const bf16x8*>(smem + half_off(buf, x, h) + (rb * 2 + kb) * 1024 + pb);
+    if (L == KC || L == CONV) {
+        const int pb = swz_kc((l & 15) * 64 + (l >> 4) * 16);
+        return *reinterpret_cast<const bf16x8*>(hbase + ((rbase >> 4) * 2 + kk) * 1024 + pb);
+    } else {
+        const int g = l >> 4, q = (l >> 2) & 3, pq = l & 3;
+        const int col = rbase + 4 * pq;
+        const int chunk = col >> 3;
+        const int ra = kk * 32 + 8 * g + q, rb = ra + 4;
+        const char* pa = hbase + ra * 256 + ((chunk ^ swz_ko(ra)) << 4) + (pq & 1) * 8;
+        const char* pb = hbase + rb * 256 + ((chunk ^ swz_ko(rb)) << 4) + (pq & 1) * 8;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pa);
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pb);
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, r);
+    }
 }
 
 #define BARRIER() __builtin_amdgcn_s_barrier()
@@ -82,13 +216,89 @@ __device__ __forceinline__ bf16x8 frag(const char* smem, int buf, int x, int h, 
 
 __device__ __forceinline__ float act_fn(float v, int act) {
     switch (act) {
-        case 1: return gelu_erf(v);
-        case 2: return fmaxf(v, 0.f);
-        case 3: return tanhf(v);
+        case ACT_GELU: return gelu_erf(v);
+        case ACT_RELU: return fmaxf(v, 0.f);
+        case ACT_TANH: return tanhf(v);
         default: return v;
     }
 }
 
+__device__ __forceinline__ long out_row(const BigParams& p, int m) {
+    if (!p.row_remap) return m;
+    const ConvDesc& cd = p.cd;
+    const int n = (int)fdiv((uint32_t)m, cd.fd_PQ);
+    const int rem = m - n * cd.P * cd.Q;
+    const int pp = (int)fdiv((uint32_t)rem, cd.fd_Q);
+    const int qq = rem - pp * cd.Q;
+    return ((long)n * cd.OH + pp * cd.ostep + cd.oa) * cd.OW + qq * cd.ostep + cd.ob;
+}
+
+template <typename T>
+__device__ __forceinline__ void load4g(const T* ptr, bool full, int nvalid, float* o) {
+    if (full) load4(ptr, o);
+    else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = r < nvalid ? to_f(ptr[r]) : 0.f;
+    }
+}
+template <typename T>
+__device__ __forceinline__ void store4g(T* ptr, bool full, int nvalid, const float* v) {
+    if (full) store4(ptr, v);
+    else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) if (r < nvalid) ptr[r] = from_f<T>(v[r]);
+    }
+}
+
+// bias / residual / activation / accumulate and the final store of 4 columns
+__device__ __forceinline__ void epilogue4(const BigParams& p, long orow, int n, float* v) {
+    const bool full = n + 3 < p.N;
+    const int nv = p.N - n;
+    if (p.bias) {
+        float bv[4];
+        if (p.bias_bf16) load4g((const bf16_t*)p.bias + n, full, nv, bv);
+        else load4g((const float*)p.bias + n, full, nv, bv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bv[r];
+    }
+    if (p.res) {
+        float rv[4];
+        load4g(p.res + orow * p.ldc + n, full, nv, rv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += rv[r];
+    }
+    if (p.act == ACT_DGELU) {
+        float z[4];
+        load4g(p.aux + orow * p.ldc + n, full, nv, z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= gelu_erf_grad(z[r]);
+    } else if (p.act != ACT_NONE) {
+        if (p.aux) store4g(p.aux + orow * p.ldc + n, full, nv, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], p.act);
+    }
+    if (p.out_f32) {
+        float* cp = (float*)p.C + orow * p.ldc + n;
+        if (p.accumulate) {
+            float o[4];
+            load4g(cp, full, nv, o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += o[r];
+        }
+        store4g(cp, full, nv, v);
+    } else {
+        bf16_t* cp = (bf16_t*)p.C + orow * p.ldc + n;
+        if (p.accumulate) {
+            float o[4];
+            load4g(cp, full, nv, o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += o[r];
+        }
+        store4g(cp, full, nv, v);
+    }
+}
+
+template <int LA, int LB>
 __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
     const int nwg = p.tiles_m * p.tiles_n;
@@ -99,7 +309,16 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
     const int m0 = tm * TB, n0 = tn * TB;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = w >> 2, wn = w & 3;
-    const int nK = p.K / BK;
+    const int split = blockIdx.y;
+    const int nK_total = (p.K + BK - 1) / BK;
+    const int kt0 = split * p.kt_per_split;
+    const int kt_end = min(nK_total, kt0 + p.kt_per_split);
+    const int nK = kt_end - kt0;              // may be odd: the pair loop reads one zero tile
+
+    Stager<LA, true> sa;
+    Stager<LB, false> sb;
+    sa.init(p, m0);
+    sb.init(p, n0);
 
     f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -112,18 +331,19 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
                 for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
-
     auto readA = [&](int buf, int qm) {
+        const char* hb = smem + half_off(buf, 0, qm);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag(smem, buf, 0, qm, wm * 4 + i, kk);
+            for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag<LA>(hb, wm * 64 + i * 16, kk);
     };
     auto readB = [&](int buf, int qn, bf16x8 (&fb)[2][2]) {
+        const char* hb = smem + half_off(buf, 1, qn);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag(smem, buf, 1, qn, wn * 2 + j, kk);
+            for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag<LB>(hb, wn * 32 + j * 16, kk);
     };
     auto mma = [&](int qm, int qn, bf16x8 (&fb)[2][2]) {
         __builtin_amdgcn_s_setprio(1);
@@ -138,78 +358,82 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
         __builtin_amdgcn_s_setprio(0);
     };
 
-    // ---------------- prologue: E <- K-tile 0 (all halves), O <- K-tile 1 (A0, B0, B1)
-    stage(p, smem, 0, 0, 0, 0, m0);
-    stage(p, smem, 0, 1, 0, 0, n0);
-    stage(p, smem, 0, 1, 1, 0, n0);
-    stage(p, smem, 0, 0, 1, 0, m0);
-    stage(p, smem, 1, 0, 0, 1, m0);
-    stage(p, smem, 1, 1, 0, 1, n0);
-    stage(p, smem, 1, 1, 1, 1, n0);
-    VM6();
-    BARRIER();
-
-    for (int it = 0; it < nK / 2; ++it) {
-        const int kE = 2 * it, kO = kE + 1;
-        const bool stE = kE + 2 < nK, stO = kO + 2 < nK;
-        // ---- phase 1: E, quadrant (0,0)
-        readA(0, 0);
-        readB(0, 0, fb0);
-        stage(p, smem, 1, 0, 1, kO, m0);
-        BARRIER(); LGKM0();
-        mma(0, 0, fb0);
+    if (nK > 0) {
+        // prologue: E <- tile kt0 (all halves), O <- tile kt0+1 (A0, B0, B1)
+        sa.stage(p, smem, 0, 0, kt0, kt_end);
+        sb.stage(p, smem, 0, 0, kt0, kt_end);
+        sb.stage(p, smem, 0, 1, kt0, kt_end);
+        sa.stage(p, smem, 0, 1, kt0, kt_end);
+        sa.stage(p, smem, 1, 0, kt0 + 1, kt_end);
+        sb.stage(p, smem, 1, 0, kt0 + 1, kt_end);
+        sb.stage(p, smem, 1, 1, kt0 + 1, kt_end);
+        VM6();
         BARRIER();
-        // ---- phase 2: E, (0,1)
-        readB(0, 1, fb1);
-        if (stE) stage(p, smem, 0, 0, 0, kE + 2, m0);
-        BARRIER(); LGKM0();
-        mma(0, 1, fb1);
-        BARRIER();
-        // ---- phase 3: E, (1,1)
-        readA(0, 1);
-        if (stE) stage(p, smem, 0, 1, 0, kE + 2, n0);
-        BARRIER(); LGKM0();
-        mma(1, 1, fb1);
-        BARRIER();
-        // ---- phase 4: E, (1,0); retire O(kO)
-        if (stE) { stage(p, smem, 0, 1, 1, kE + 2, n0); VM6(); } else { VM0(); }
-        BARRIER();
-        mma(1, 0, fb0);
-        BARRIER();
-        // ---- phase 5: O, (0,0)
-        readA(1, 0);
-        readB(1, 0, fb0);
-        if (stE) stage(p, smem, 0, 0, 1, kE + 2, m0);
-        BARRIER(); LGKM0();
-        mma(0, 0, fb0);
-        BARRIER();
-        // ---- phase 6: O, (0,1)
-        readB(1, 1, fb1);
-        if (stO) stage(p, smem, 1, 0, 0, kO + 2, m0);
-        BARRIER(); LGKM0();
-        mma(0, 1, fb1);
-        BARRIER();
-        // ---- phase 7: O, (1,1)
-        readA(1, 1);
-        if (stO) stage(p, smem, 1, 1, 0, kO + 2, n0);
-        BARRIER(); LGKM0();
-        mma(1, 1, fb1);
-        BARRIER();
-        // ---- phase 8: O, (1,0); retire E(kE+2)
-        if (stO) { stage(p, smem, 1, 1, 1, kO + 2, n0); VM6(); } else { VM0(); }
-        BARRIER();
-        mma(1, 0, fb0);
-        BARRIER();
+        const int iters = (nK + 1) / 2;
+        for (int it = 0; it < iters; ++it) {
+            const int kE = kt0 + 2 * it, kO = kE + 1;
+            const bool more = it + 1 < iters;
+            // phase 1: E (0,0)
+            readA(0, 0);
+            readB(0, 0, fb0);
+            sa.stage(p, smem, 1, 1, kO, kt_end);
+            BARRIER(); LGKM0();
+            mma(0, 0, fb0);
+            BARRIER();
+            // phase 2: E (0,1)
+            readB(0, 1, fb1);
+            if (more) sa.stage(p, smem, 0, 0, kE + 2, kt_end);
+            BARRIER(); LGKM0();
+            mma(0, 1, fb1);
+            BARRIER();
+            // phase 3: E (1,1)
+            readA(0, 1);
+            if (more) sb.stage(p, smem, 0, 0, kE + 2, kt_end);
+            BARRIER(); LGKM0();
+            mma(1, 1, fb1);
+            BARRIER();
+            // phase 4: E (1,0); retire O(kO)
+            if (more) { sb.stage(p, smem, 0, 1, kE + 2, kt_end); VM6(); } else { VM0(); }
+            BARRIER();
+            mma(1, 0, fb0);
+            BARRIER();
+            // phase 5: O (0,0)
+            readA(1, 0);
+            readB(1, 0, fb0);
+            if (more) sa.stage(p, smem, 0, 1, kE + 2, kt_end);
+            BARRIER(); LGKM0();
+            mma(0, 0, fb0);
+            BARRIER();
+            // phase 6: O (0,1)
+            readB(1, 1, fb1);
+            if (more) sa.stage(p, smem, 1, 0, kO + 2, kt_end);
+            BARRIER(); LGKM0();
+            mma(0, 1, fb1);
+            BARRIER();
+            // phase 7: O (1,1)
+            readA(1, 1);
+            if (more) sb.stage(p, smem, 1, 0, kO + 2, kt_end);
+            BARRIER(); LGKM0();
+            mma(1, 1, fb1);
+            BARRIER();
+            // phase 8: O (1,0); retire E(kE+2)
+            if (more) { sb.stage(p, smem, 1, 1, kO + 2, kt_end); VM6(); } else { VM0(); }
+            BARRIER();
+            mma(1, 0, fb0);
+            BARRIER();
+        }
     }
 
     // ---------------- epilogue: lane holds C[m][n..n+3]
     const int g = lane >> 4;
+    const bool partial = p.splits > 1;
 #pragma unroll
     for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int m = m0 + qm * 128 + wm * 64 + i * 16 + (lane & 15);
             if (m >= p.M) continue;
+            const long orow = partial ? (long)m : out_row(p, m);
 #pragma unroll
             for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
@@ -218,70 +442,94 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
                     if (n >= p.N) continue;
                     float v[4] = {acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
                                   acc[qm][qn][i][j][3]};
-                    const bool full = n + 3 < p.N;
-                    if (p.bias) {
-                        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-                        if (full) {
-                            if (p.bias_bf16) load4((const bf16_t*)p.bias + n, bv);
-                            else load4((const float*)p.bias + n, bv);
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (n + r < p.N)
-                                    bv[r] = p.bias_bf16 ? bf2f(((const bf16_t*)p.bias)[n + r]) : ((const float*)p.bias)[n + r];
-                        }
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] += bv[r];
+                    if (partial) {
+                        store4g((float*)p.C + split * p.split_stride + orow * p.ldc + n, n + 3 < p.N, p.N - n, v);
+                        continue;
                     }
-                    if (p.act) {
-                        if (p.aux) {
-                            bf16_t* ap = p.aux + (long)m * p.ldc + n;
-                            if (full) store4(ap, v);
-                            else {
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) if (n + r < p.N) ap[r] = f2bf(v[r]);
-                            }
-                        }
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], p.act);
-                    }
-                    bf16_t* cp = p.C + (long)m * p.ldc + n;
-                    if (p.accumulate) {
-                        float o[4] = {0.f, 0.f, 0.f, 0.f};
-                        if (full) load4(cp, o);
-                        else {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) if (n + r < p.N) o[r] = bf2f(cp[r]);
-                        }
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] += o[r];
-                    }
-                    if (full) store4(cp, v);
-                    else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) if (n + r < p.N) cp[r] = f2bf(v[r]);
-                    }
+                    epilogue4(p, orow, n, v);
                 }
         }
 }
 
-}  // namespace
-
-DDL_API int ddl_gemm_big_supported(int M, int N, int K, long lda, long ldb) {
-    return K > 0 && K % 128 == 0 && lda % 8 == 0 && ldb % 8 == 0 && M > 0 && N > 0;
+// Split-K: sum fp32 partial slabs + the epilogue; 4 consecutive columns per thread.
+__global__ __launch_bounds__(256) void big_reduce_k(BigParams p, const float* __restrict__ part) {
+    const long n4 = ((long)p.N + 3) / 4;
+    const long total = (long)p.M * n4;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int m = (int)(i / n4);
+        const int n = (int)(i - (long)m * n4) * 4;
+        const bool full = n + 3 < p.N;
+        const int nv = p.N - n;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < p.splits; ++s) {
+            float t[4];
+            load4g(part + s * p.split_stride + (long)m * p.ldc + n, full, nv, t);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += t[r];
+        }
+        epilogue4(p, out_row(p, m), n, v);
+    }
 }
 
-// C = A . B^T (+bias)(act: 0 none, 1 gelu (aux <- pre-activation), 2 relu, 3 tanh); bf16 in/out
-DDL_API int ddl_gemm_big(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                         const void* bias, int bias_bf16, int act, void* aux, int accumulate, hipStream_t st) {
-    if (!ddl_gemm_big_supported(M, N, K, lda, ldb)) return -1;
+void fill_conv(ConvDesc& cd, const int* d) {
+    cd.N = d[0]; cd.H = d[1]; cd.W = d[2]; cd.C = d[3]; cd.P = d[4]; cd.Q = d[5];
+    cd.stride = d[6]; cd.h_off = d[7]; cd.w_off = d[8]; cd.h_step = d[9]; cd.w_step = d[10];
+    cd.R = d[11]; cd.S = d[12]; cd.OH = d[13]; cd.OW = d[14]; cd.ostep = d[15]; cd.oa = d[16]; cd.ob = d[17];
+    cd.fd_PQ = make_fastdiv((uint32_t)(cd.P * cd.Q));
+    cd.fd_Q = make_fastdiv((uint32_t)cd.Q);
+    cd.fd_C = make_fastdiv((uint32_t)cd.C);
+    cd.fd_S = make_fastdiv((uint32_t)std::max(1, cd.S));
+}
+
+template <int LA, int LB>
+int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st) {
+    p.tiles_m = (p.M + TB - 1) / TB;
+    p.tiles_n = (p.N + TB - 1) / TB;
+    const int nk = (p.K + BK - 1) / BK;
+    if (splits < 1) splits = 1;
+    if (splits > nk) splits = nk > 0 ? nk : 1;
+    p.kt_per_split = nk > 0 ? (nk + splits - 1) / splits : 1;
+    splits = nk > 0 ? (nk + p.kt_per_split - 1) / p.kt_per_split : 1;
+    p.splits = splits;
+    if (splits > 1) {
+        p.split_stride = (long)p.M * p.ldc;
+        if (!ws || ws_elems < p.split_stride * splits) return -2;
+    }
+    BigParams kp = p;
+    if (splits > 1) kp.C = ws;
+    hipLaunchKernelGGL((gemm_big_k<LA, LB>), dim3(p.tiles_m * p.tiles_n, splits), dim3(NTH), 0, st, kp);
+    if (splits > 1) {
+        const long total = (long)p.M * ((p.N + 3) / 4);
+        const int g = (int)std::min<long>(16384, (total + 255) / 256);
+        big_reduce_k<<<g, 256, 0, st>>>(p, ws);
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// mode: 0 = A KC, B KC (NT)   1 = A KC, B KO (NN)   2 = A KO, B KO (TN)
+//       3 = A CONV, B KC      4 = A KO, B CONVW
+// Requirements: K % 8 == 0, leading dims % 8 == 0 (16-B chunks), zero points at >= 16 zero bytes.
+DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
+                          int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
+                          float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
+                          int accumulate, const void* zero, hipStream_t st) {
+    if (M <= 0 || N <= 0) return 0;
+    if (K % 8 || !zero) return -1;
     BigParams p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
-    p.C = (bf16_t*)C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+    p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = (bf16_t*)aux;
-    p.accumulate = accumulate;
-    p.tiles_m = (M + TB - 1) / TB;
-    p.tiles_n = (N + TB - 1) / TB;
-    hipLaunchKernelGGL(gemm_big_k, dim3(p.tiles_m * p.tiles_n), dim3(NTH), 0, st, p);
-    return (int)hipGetLastError();
+    p.res = (const bf16_t*)res; p.accumulate = accumulate; p.out_f32 = out_f32;
+    p.row_remap = row_remap; p.zero = (const bf16_t*)zero;
+    if (conv) fill_conv(p.cd, conv);
+    switch (mode) {
+        case 0: return launch_big<KC, KC>(p, workspace, ws_elems, splits, st);
+        case 1: return launch_big<KC, KO>(p, workspace, ws_elems, splits, st);
+        case 2: return launch_big<KO, KO>(p, workspace, ws_elems, splits, st);
+        case 3: return launch_big<CONV, KC>(p, workspace, ws_elems, splits, st);
+        case 4: return launch_big<KO, CONVW>(p, workspace, ws_elems, splits, st);
+        default: return -1;
+    }
 }

@@ -45,10 +45,7 @@ def _dgrad(dy, w, x_shape, stride, pad):
     _, P, Q, _ = dy.shape
     if R == 1 and S == 1 and stride == 1 and pad == 0:
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
-        if K % 128 == 0:   # NT on the large-tile kernel with W^T (a [C, K] copy, tiny)
-            gemm(MODE_NT, dy, K, w.reshape(K, C).t().contiguous(), K, dx, C, N * H * W_, C, K)
-        else:
-            gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K)
+        gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K)
         return dx
     if stride == 1:
         wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()       # [C, R, S, K]

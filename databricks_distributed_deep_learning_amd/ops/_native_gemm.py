@@ -10,30 +10,48 @@ from . import _lib
 from ._lib import I, L, P
 
 _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P],
-               "ddl_gemm_big": [P, L, P, L, P, L, I, I, I, P, I, I, P, I, P],
-               "ddl_gemm_big_supported": [I, I, I, L, L]})
-
-BIG_MIN_TILES = 64          # 256x256 tiles needed before the big kernel beats the 128x128 one
-_force_small = False
-
-
-def set_big_gemm(enabled: bool) -> None:
-    global _force_small
-    _force_small = not enabled
-
-
-def _use_big(mode, C, M, N, K, lda, ldb, splits, conv, row_remap, residual) -> bool:
-    if _force_small or mode != MODE_NT or C.dtype != torch.bfloat16 or splits is not None or conv is not None:
-        return False
-    if row_remap or residual is not None or K % 128 != 0:
-        return False
-    return (-(-M // 256)) * (-(-N // 256)) >= BIG_MIN_TILES
+               "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
 ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4}
 BM = BN = 128
 BK = 64
 NUM_CU = 256
+_force_small = False
+_zero_pages = {}
+
+
+def set_big_gemm(enabled: bool) -> None:
+    """Route GEMMs to the 256x256 8-phase kernel (True, default) or the 128x128 one."""
+    global _force_small
+    _force_small = not enabled
+
+
+def _zero_page(device) -> torch.Tensor:
+    z = _zero_pages.get(device)
+    if z is None:
+        z = torch.zeros(128, dtype=torch.bfloat16, device=device)
+        _zero_pages[device] = z
+    return z
+
+
+def use_big(mode: int, M: int, N: int, K: int) -> bool:
+    """256x256 tiles pay off when neither output side is narrow (tile waste) and
+    there is enough work; reduction-outer (wgrad) shapes use split-K instead."""
+    if _force_small or K % 8 or K < 128 or min(M, N) < 192:
+        return False
+    tiles = (-(-M // 256)) * (-(-N // 256))
+    if mode in (MODE_TN, MODE_CONVW):
+        return K >= 1024
+    return tiles >= 48
+
+
+def big_splits(M: int, N: int, K: int) -> int:
+    tiles = (-(-M // 256)) * (-(-N // 256))
+    nk = -(-K // BK)
+    if tiles >= 200:
+        return 1
+    return max(1, min(-(-NUM_CU // tiles), nk // 4))
 
 
 def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
@@ -52,22 +70,26 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
          conv: Optional[Sequence[int]] = None, row_remap: bool = False,
          residual: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
-    if _use_big(mode, C, M, N, K, lda, ldb, splits, conv, row_remap, residual):
-        bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
-        rc = _lib.fn("ddl_gemm_big")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, _lib.p(bias),
-                                     bias_bf16, ACT[act], _lib.p(aux), int(accumulate), _lib.stream())
-        if rc != 0:
-            raise RuntimeError(f"ddl_gemm_big(M={M}, N={N}, K={K}) failed: {rc}")
-        return C
-    out_f32 = 1 if C.dtype == torch.float32 else 0
-    s = 1 if row_remap else pick_splits(M, N, K, splits)
-    ws = None
-    if s > 1:
-        ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device)
     conv_arr = None
     if conv is not None:
         conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
+    out_f32 = 1 if C.dtype == torch.float32 else 0
+    if splits is None and use_big(mode, M, N, K):
+        s = 1 if row_remap else big_splits(M, N, K)
+        ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device) if s > 1 else None
+        rc = _lib.fn("ddl_gemm_big2")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
+                                      _lib.p(bias), bias_bf16, ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws),
+                                      0 if ws is None else ws.numel(), conv_arr, int(row_remap),
+                                      _lib.p(residual), int(accumulate), _zero_page(C.device).data_ptr(),
+                                      _lib.stream())
+        if rc != 0:
+            raise RuntimeError(f"ddl_gemm_big2(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
+        return C
+    s = 1 if row_remap else pick_splits(M, N, K, splits)
+    ws = None
+    if s > 1:
+        ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device)
     rc = _lib.fn("ddl_gemm")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
                              _lib.p(bias), bias_bf16, ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws),
                              0 if ws is None else ws.numel(), conv_arr, int(row_remap), _lib.p(residual),

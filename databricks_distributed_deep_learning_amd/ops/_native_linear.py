@@ -68,11 +68,7 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
-            if N % 128 == 0 and M >= 4096:
-                # dgrad as an NT GEMM on the large-tile kernel: W^T is a tiny copy
-                gemm(MODE_NT, dz, N, w.t().contiguous(), N, dx, K, M, K, N)
-            else:
-                gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
+            gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
             dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
