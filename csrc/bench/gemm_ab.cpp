@@ -1,0 +1,52 @@
+// Stand-alone A/B timing of GEMM kernel variants (no torch): hipEvent timing of
+// ddl_gemm_big2 (NT) against an alternative object linked in as ddl_gemm_big.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+extern "C" int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M,
+                             int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
+                             int splits, void* ws, long ws_elems, const int* conv, int row_remap, const void* res,
+                             int accumulate, const void* zero, hipStream_t st);
+extern "C" int ddl_gemm_big(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                            const void* bias, int bias_bf16, int act, void* aux, int accumulate, hipStream_t st);
+
+int main() {
+    const int shapes[][3] = {{16384, 2304, 768}, {16384, 768, 768}, {16384, 3072, 768}, {16384, 768, 3072},
+                             {4096, 4096, 4096}, {8192, 8192, 8192}};
+    void *A, *B, *C, *Z;
+    hipMalloc(&A, 8192L * 8192 * 2);
+    hipMalloc(&B, 8192L * 8192 * 2);
+    hipMalloc(&C, 8192L * 8192 * 2);
+    hipMalloc(&Z, 256);
+    hipMemset(A, 0x3c, 8192L * 8192 * 2);
+    hipMemset(B, 0x3c, 8192L * 8192 * 2);
+    hipMemset(Z, 0, 256);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (auto& s : shapes) {
+        const int M = s[0], N = s[1], K = s[2];
+        for (int v = 0; v < 2; ++v) {
+            auto run = [&] {
+                if (v == 0)
+                    ddl_gemm_big(A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 0);
+                else
+                    ddl_gemm_big2(0, A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 1, nullptr, 0, nullptr,
+                                  0, nullptr, 0, Z, 0);
+            };
+            for (int i = 0; i < 5; ++i) run();
+            hipEventRecord(e0, 0);
+            const int it = 50;
+            for (int i = 0; i < it; ++i) run();
+            hipEventRecord(e1, 0);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            ms /= it;
+            printf("%s M=%d N=%d K=%d  %.4f ms  %.1f TF\n", v == 0 ? "v1" : "v2", M, N, K, ms,
+                   2.0 * M * N * K / ms / 1e9);
+        }
+    }
+    return 0;
+}

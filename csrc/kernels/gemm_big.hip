@@ -35,6 +35,7 @@
 
 namespace {
 
+constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
 constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
 
@@ -112,14 +113,21 @@ __device__ __forceinline__ void tap_of(const ConvDesc& cd, int k, int& dh, int& 
 }
 
 // ------------------------------------------------------------------ operand staging
-template <int L, bool IS_A>
+// Per-lane source pointers are computed once (init) so a stage costs a 64-bit
+// add and a select per DMA: the non-MFMA segment between barriers is on the
+// critical path of the 8-phase schedule.  Out-of-range lanes point at the zero
+// page with a zero stride.
+template <int L, bool IS_A, bool KTAIL>
 struct Stager {
     const bf16_t* base;
     long ld;
     int rows;        // extent of this operand's M (A) / N (B) side
     int K;
     int r0;          // tile origin on the M / N side
+    const bf16_t* lp[2];   // KC / KO: lane pointer for half 0 / 1 at K-tile 0, sub j = 0
+    bool lok[2];
     Pix px[2];       // CONV: this lane's row in half 0 / half 1
+    int kcol;        // KC/CONV: lane's k offset inside a subtile (8 c); KO/CONVW: unused
 
     __device__ __forceinline__ void init(const BigParams& p, int origin) {
         base = IS_A ? p.A : p.B;
@@ -127,40 +135,82 @@ struct Stager {
         rows = IS_A ? p.M : p.N;
         K = p.K;
         r0 = origin;
-        if (L == CONV) {
-            const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-            const int r = swz_kc(l * 16) >> 6;
+        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        if (L == KC || L == CONV) {
+            const int lb = swz_kc(l * 16);
+            const int r = lb >> 6;
+            kcol = ((lb >> 4) & 3) * 8;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) px[h] = decompose(p.cd, base, r0 + h * 128 + w * 16 + r, rows);
+            for (int h = 0; h < 2; ++h) {
+                const int row = r0 + h * 128 + w * 16 + r;
+                if (L == KC) {
+                    // rows past the edge re-read the last row: their results are never stored
+                    lok[h] = row < rows;
+                    lp[h] = base + (long)(lok[h] ? row : rows - 1) * ld + kcol;
+                } else {
+                    px[h] = decompose(p.cd, base, row, rows);
+                    // padding / out-of-range rows: coordinates that fail every bounds check
+                    if (!px[h].ok) px[h].hb = -(1 << 20);
+                    lp[h] = px[h].img + ((long)px[h].hb * p.cd.W + px[h].wb) * p.cd.C + kcol;
+                }
+            }
+        } else if (L == KO) {
+            const int krow = (w * 2) * 4 + (l >> 4);      // sub j = 0; j = 1 adds 4 rows
+            const int c = (l & 15) ^ swz_ko(krow);         // same swizzle for krow + 4 (bits 0,1,3 unchanged)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int col = r0 + h * 128 + 8 * c;
+                lok[h] = col < rows;
+                lp[h] = base + (long)krow * ld + (lok[h] ? col : ((rows - 1) & ~7));
+            }
         }
     }
 
-    // half-tile h of K-tile kt; tiles at or past kt_end are all zeros
-    __device__ __forceinline__ void stage(const BigParams& p, char* smem, int buf, int h, int kt, int kt_end) {
+    // half-tile h of K-tile kt (kt < kt_end: the caller never stages padding
+    // tiles).  Without KTAIL the KC / KO paths are a 64-bit add of a uniform
+    // offset per DMA; the K-tail variant swaps lanes past K onto the zero page.
+    __device__ __forceinline__ void stage(const BigParams& p, char* smem, int buf, int h, int kt) {
         const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
         char* hbase = smem + half_off(buf, IS_A ? 0 : 1, h);
-        const bool tile_ok = kt < kt_end;
-        if (L == KC || L == CONV) {
-            const int lb = swz_kc(l * 16);
-            const int r = lb >> 6, c = (lb >> 4) & 3;
-            const int row = r0 + h * 128 + w * 16 + r;
+        const bool ktail = KTAIL && (kt + 1) * BK > K;       // uniform: partial last tile
+        if (L == KC) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const int k = kt * BK + j * 32 + c * 8;
-                const bf16_t* g = p.zero;
-                if (L == KC) {
-                    if (tile_ok && row < rows && k < K) g = base + (long)row * ld + k;
-                } else {
-                    int dh, dw, ci;
-                    tap_of(p.cd, k < K ? k : 0, dh, dw, ci);
-                    const Pix& x = px[h];
-                    const int hh = x.hb + dh, ww = x.wb + dw;
-                    if (tile_ok && x.ok && k < K && (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W)
-                        g = x.img + ((long)hh * p.cd.W + ww) * p.cd.C + ci;
-                }
+                const int off = kt * BK + j * 32;
+                const bf16_t* g = lp[h] + off;
+                if (ktail) g = (off + kcol < K) ? g : p.zero;
                 glds(g, hbase + (w * 2 + j) * 1024);
             }
-        } else {
+        } else if (L == KO) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16_t* g = lp[h] + (long)(kt * BK + j * 4) * ld;
+                if (ktail) g = (kt * BK + j * 4 + (w * 2) * 4 + (l >> 4) < K) ? g : p.zero;
+                glds(g, hbase + (w * 2 + j) * 1024);
+            }
+        } else if (L == CONV) {
+            const Pix& x = px[h];
+            if (!KTAIL) {
+                // C % 64 == 0: the whole K-tile lies in one (r, s) tap -> uniform offset
+                int dh, dw, ci;
+                tap_of(p.cd, kt * BK, dh, dw, ci);
+                const long toff = ((long)dh * p.cd.W + dw) * p.cd.C + ci;
+                const bool ok = (unsigned)(x.hb + dh) < (unsigned)p.cd.H && (unsigned)(x.wb + dw) < (unsigned)p.cd.W;
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    glds(ok ? lp[h] + toff + j * 32 : p.zero, hbase + (w * 2 + j) * 1024);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int k = kt * BK + j * 32 + kcol;
+                    int dh, dw, ci;
+                    tap_of(p.cd, k < K ? k : 0, dh, dw, ci);
+                    const int hh = x.hb + dh, ww = x.wb + dw;
+                    const bool ok = k < K && (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W;
+                    glds(ok ? x.img + ((long)hh * p.cd.W + ww) * p.cd.C + ci : p.zero, hbase + (w * 2 + j) * 1024);
+                }
+            }
+        } else {   // CONVW: reduction rows are output pixels, columns are (tap, channel)
             const int pc = l & 15;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -169,17 +219,13 @@ struct Stager {
                 const int col = r0 + h * 128 + 8 * c;
                 const int k = kt * BK + krow;
                 const bf16_t* g = p.zero;
-                if (L == KO) {
-                    if (tile_ok && k < K && col < rows) g = base + (long)k * ld + col;
-                } else {   // CONVW: reduction rows are output pixels, columns are (tap, channel)
-                    if (tile_ok && k < K && col < rows) {
-                        int dh, dw, ci;
-                        tap_of(p.cd, col, dh, dw, ci);
-                        const Pix x = decompose(p.cd, base, k, K);
-                        const int hh = x.hb + dh, ww = x.wb + dw;
-                        if ((unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W)
-                            g = x.img + ((long)hh * p.cd.W + ww) * p.cd.C + ci;
-                    }
+                if (k < K && col < rows) {
+                    int dh, dw, ci;
+                    tap_of(p.cd, col, dh, dw, ci);
+                    const Pix x = decompose(p.cd, base, k, K);
+                    const int hh = x.hb + dh, ww = x.wb + dw;
+                    if ((unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W)
+                        g = x.img + ((long)hh * p.cd.W + ww) * p.cd.C + ci;
                 }
                 glds(g, hbase + (w * 2 + j) * 1024);
             }
@@ -298,7 +344,7 @@ __device__ __forceinline__ void epilogue4(const BigParams& p, long orow, int n, 
     }
 }
 
-template <int LA, int LB>
+template <int LA, int LB, bool KTAIL>
 __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
     const int nwg = p.tiles_m * p.tiles_n;
@@ -313,10 +359,10 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
     const int nK_total = (p.K + BK - 1) / BK;
     const int kt0 = split * p.kt_per_split;
     const int kt_end = min(nK_total, kt0 + p.kt_per_split);
-    const int nK = kt_end - kt0;              // may be odd: the pair loop reads one zero tile
+    const int nK = kt_end - kt0;              // may be odd: the last pair then skips its O half
 
-    Stager<LA, true> sa;
-    Stager<LB, false> sb;
+    Stager<LA, true, KTAIL> sa;
+    Stager<LB, false, KTAIL> sb;
     sa.init(p, m0);
     sb.init(p, n0);
 
@@ -358,97 +404,131 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
         __builtin_amdgcn_s_setprio(0);
     };
 
+    // phases 1-4: the four quarter-products of the E buffer (tile kE); stO1
+    // stages the last O half of tile kE+1, more stages tile kE+2 into E
+    auto phasesE = [&](int kE, bool stO1, bool more) {
+        // phase 1: E (0,0)
+        readA(0, 0);
+        readB(0, 0, fb0);
+        if (stO1) sa.stage(p, smem, 1, 1, kE + 1);
+        BARRIER(); LGKM0();
+        mma(0, 0, fb0);
+        BARRIER();
+        // phase 2: E (0,1)
+        readB(0, 1, fb1);
+        if (more) sa.stage(p, smem, 0, 0, kE + 2);
+        BARRIER(); LGKM0();
+        mma(0, 1, fb1);
+        BARRIER();
+        // phase 3: E (1,1)
+        readA(0, 1);
+        if (more) sb.stage(p, smem, 0, 0, kE + 2);
+        BARRIER(); LGKM0();
+        mma(1, 1, fb1);
+        BARRIER();
+        // phase 4: E (1,0); retire O(kE+1)
+        if (more) { sb.stage(p, smem, 0, 1, kE + 2); VM6(); } else { VM0(); }
+        BARRIER();
+        mma(1, 0, fb0);
+        BARRIER();
+    };
+
     if (nK > 0) {
         // prologue: E <- tile kt0 (all halves), O <- tile kt0+1 (A0, B0, B1)
-        sa.stage(p, smem, 0, 0, kt0, kt_end);
-        sb.stage(p, smem, 0, 0, kt0, kt_end);
-        sb.stage(p, smem, 0, 1, kt0, kt_end);
-        sa.stage(p, smem, 0, 1, kt0, kt_end);
-        sa.stage(p, smem, 1, 0, kt0 + 1, kt_end);
-        sb.stage(p, smem, 1, 0, kt0 + 1, kt_end);
-        sb.stage(p, smem, 1, 1, kt0 + 1, kt_end);
-        VM6();
+        sa.stage(p, smem, 0, 0, kt0);
+        sb.stage(p, smem, 0, 0, kt0);
+        sb.stage(p, smem, 0, 1, kt0);
+        sa.stage(p, smem, 0, 1, kt0);
+        if (nK > 1) {
+            sa.stage(p, smem, 1, 0, kt0 + 1);
+            sb.stage(p, smem, 1, 0, kt0 + 1);
+            sb.stage(p, smem, 1, 1, kt0 + 1);
+            VM6();
+        } else {
+            VM0();
+        }
         BARRIER();
-        const int iters = (nK + 1) / 2;
-        for (int it = 0; it < iters; ++it) {
+        const int pairs = nK / 2;
+        for (int it = 0; it < pairs; ++it) {
             const int kE = kt0 + 2 * it, kO = kE + 1;
-            const bool more = it + 1 < iters;
-            // phase 1: E (0,0)
-            readA(0, 0);
-            readB(0, 0, fb0);
-            sa.stage(p, smem, 1, 1, kO, kt_end);
-            BARRIER(); LGKM0();
-            mma(0, 0, fb0);
-            BARRIER();
-            // phase 2: E (0,1)
-            readB(0, 1, fb1);
-            if (more) sa.stage(p, smem, 0, 0, kE + 2, kt_end);
-            BARRIER(); LGKM0();
-            mma(0, 1, fb1);
-            BARRIER();
-            // phase 3: E (1,1)
-            readA(0, 1);
-            if (more) sb.stage(p, smem, 0, 0, kE + 2, kt_end);
-            BARRIER(); LGKM0();
-            mma(1, 1, fb1);
-            BARRIER();
-            // phase 4: E (1,0); retire O(kO)
-            if (more) { sb.stage(p, smem, 0, 1, kE + 2, kt_end); VM6(); } else { VM0(); }
-            BARRIER();
-            mma(1, 0, fb0);
-            BARRIER();
+            const bool more = kE + 2 < kt_end;
+            const bool moreO = kO + 2 < kt_end;
+            phasesE(kE, true, more);
             // phase 5: O (0,0)
             readA(1, 0);
             readB(1, 0, fb0);
-            if (more) sa.stage(p, smem, 0, 1, kE + 2, kt_end);
+            if (more) sa.stage(p, smem, 0, 1, kE + 2);
             BARRIER(); LGKM0();
             mma(0, 0, fb0);
             BARRIER();
             // phase 6: O (0,1)
             readB(1, 1, fb1);
-            if (more) sa.stage(p, smem, 1, 0, kO + 2, kt_end);
+            if (moreO) sa.stage(p, smem, 1, 0, kO + 2);
             BARRIER(); LGKM0();
             mma(0, 1, fb1);
             BARRIER();
             // phase 7: O (1,1)
             readA(1, 1);
-            if (more) sb.stage(p, smem, 1, 0, kO + 2, kt_end);
+            if (moreO) sb.stage(p, smem, 1, 0, kO + 2);
             BARRIER(); LGKM0();
             mma(1, 1, fb1);
             BARRIER();
             // phase 8: O (1,0); retire E(kE+2)
-            if (more) { sb.stage(p, smem, 1, 1, kO + 2, kt_end); VM6(); } else { VM0(); }
+            if (moreO) { sb.stage(p, smem, 1, 1, kO + 2); VM6(); } else { VM0(); }
             BARRIER();
             mma(1, 0, fb0);
             BARRIER();
         }
+        // odd tile count: the last E tile (fully landed: phase 8 waited vmcnt(0))
+        if (nK & 1) phasesE(kt_end - 1, false, false);
     }
 
-    // ---------------- epilogue: lane holds C[m][n..n+3]
+    // ---------------- epilogue
+    // The accumulators go through LDS one 128x128 quarter at a time (fp32, rows
+    // padded to 132 floats: the 16 rows a ds_write_b128 group touches land on
+    // distinct bank quads).  Each thread then owns 8 consecutive columns of a
+    // row, so the bias / residual / activation / store code exists once (not 32
+    // unrolled copies -- the unrolled form cost ~10 us per tile in I-cache
+    // misses) and global stores are row-contiguous.
+    float* ep = reinterpret_cast<float*>(smem);
     const int g = lane >> 4;
     const bool partial = p.splits > 1;
+    auto put = [&](f32x4 (&a)[4][2]) {
 #pragma unroll
-    for (int qm = 0; qm < 2; ++qm)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int m = m0 + qm * 128 + wm * 64 + i * 16 + (lane & 15);
-            if (m >= p.M) continue;
-            const long orow = partial ? (long)m : out_row(p, m);
+            for (int j = 0; j < 2; ++j)
+                *reinterpret_cast<f32x4*>(ep + (wm * 64 + i * 16 + (lane & 15)) * EP_LD + wn * 32 + j * 16 + 4 * g) =
+                    a[i][j];
+    };
 #pragma unroll
-            for (int qn = 0; qn < 2; ++qn)
+    for (int q = 0; q < 4; ++q) {
+        __syncthreads();
+        put(acc[q >> 1][q & 1]);
+        __syncthreads();
+        const int mq = m0 + (q >> 1) * 128, nq = n0 + (q & 1) * 128;
+#pragma unroll 1
+        for (int it = 0; it < (128 * 16) / NTH; ++it) {
+            const int idx = it * NTH + threadIdx.x;
+            const int r = idx >> 4, c = (idx & 15) * 8;
+            const int m = mq + r, n = nq + c;
+            if (m >= p.M || n >= p.N) continue;
+            float v[8];
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + r * EP_LD + c);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + r * EP_LD + c + 4);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int n = n0 + qn * 128 + wn * 32 + j * 16 + 4 * g;
-                    if (n >= p.N) continue;
-                    float v[4] = {acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
-                                  acc[qm][qn][i][j][3]};
-                    if (partial) {
-                        store4g((float*)p.C + split * p.split_stride + orow * p.ldc + n, n + 3 < p.N, p.N - n, v);
-                        continue;
-                    }
-                    epilogue4(p, orow, n, v);
-                }
+            for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
+            if (partial) {
+                float* dst = (float*)p.C + split * p.split_stride + (long)m * p.ldc + n;
+                store4g(dst, n + 3 < p.N, p.N - n, v);
+                if (n + 4 < p.N) store4g(dst + 4, n + 7 < p.N, p.N - n - 4, v + 4);
+                continue;
+            }
+            const long orow = out_row(p, m);
+            epilogue4(p, orow, n, v);
+            if (n + 4 < p.N) epilogue4(p, orow, n + 4, v + 4);
         }
+    }
 }
 
 // Split-K: sum fp32 partial slabs + the epilogue; 4 consecutive columns per thread.
@@ -497,7 +577,13 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     }
     BigParams kp = p;
     if (splits > 1) kp.C = ws;
-    hipLaunchKernelGGL((gemm_big_k<LA, LB>), dim3(p.tiles_m * p.tiles_n, splits), dim3(NTH), 0, st, kp);
+    // KTAIL: per-chunk K checks; also selects the per-chunk tap decomposition for
+    // convolutions whose channel count is not a multiple of 64
+    const bool ktail = (p.K % BK) != 0 || ((LA == CONV || LB == CONVW) && (p.cd.C % BK) != 0);
+    if (ktail)
+        hipLaunchKernelGGL((gemm_big_k<LA, LB, true>), dim3(p.tiles_m * p.tiles_n, splits), dim3(NTH), 0, st, kp);
+    else
+        hipLaunchKernelGGL((gemm_big_k<LA, LB, false>), dim3(p.tiles_m * p.tiles_n, splits), dim3(NTH), 0, st, kp);
     if (splits > 1) {
         const long total = (long)p.M * ((p.N + 3) / 4);
         const int g = (int)std::min<long>(16384, (total + 255) / 256);
@@ -529,7 +615,6 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
         case 1: return launch_big<KC, KO>(p, workspace, ws_elems, splits, st);
         case 2: return launch_big<KO, KO>(p, workspace, ws_elems, splits, st);
         case 3: return launch_big<CONV, KC>(p, workspace, ws_elems, splits, st);
-        case 4: return launch_big<KO, CONVW>(p, workspace, ws_elems, splits, st);
-        default: return -1;
+        default: return -1;   // conv wgrad (CONVW) stays on the 128x128 kernel (gemm.hip)
     }
 }

@@ -38,7 +38,7 @@ def _zero_page(device) -> torch.Tensor:
 def use_big(mode: int, M: int, N: int, K: int) -> bool:
     """256x256 tiles pay off when neither output side is narrow (tile waste) and
     there is enough work; reduction-outer (wgrad) shapes use split-K instead."""
-    if _force_small or K % 8 or K < 128 or min(M, N) < 192:
+    if _force_small or K % 8 or K < 128 or min(M, N) < 192 or mode == MODE_CONVW:
         return False
     tiles = (-(-M // 256)) * (-(-N // 256))
     if mode in (MODE_TN, MODE_CONVW):
