@@ -73,6 +73,7 @@ def bench_gemm(results):
 
 def bench_conv(results, batch=256):
     from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
     dev = torch.device("cuda")
     convs = [  # Cin, Cout, k, stride, H
         (3, 64, 7, 2, 224), (64, 64, 1, 1, 56), (64, 64, 3, 1, 56), (64, 256, 1, 1, 56), (256, 64, 1, 1, 56),
@@ -94,15 +95,21 @@ def bench_conv(results, batch=256):
         wp = F.pad(w, (0, (8 - cin % 8) % 8)) if cin % 8 else w
         fl = 2.0 * batch * P * P * cout * k * k * cin
         r = {"op": "conv", "cin": cin, "cout": cout, "k": k, "stride": s, "H": H, "batch": batch}
-        r["fwd_ours_ms"] = timeit(lambda: NC._fwd(xp, wp, s, pad))
-        r["fwd_miopen_ms"] = timeit(lambda: F.conv2d(xn, wn, stride=s, padding=pad))
+        ops = {"fwd": lambda: NC._fwd(xp, wp, s, pad),
+               "wgrad": lambda: NC._wgrad(dy, xp, wp.shape, s, pad)}
+        ref = {"fwd": lambda: F.conv2d(xn, wn, stride=s, padding=pad),
+               "wgrad": lambda: torch.ops.aten.convolution_backward(
+                   dyn, xn, wn, None, [s, s], [pad, pad], [1, 1], False, [0, 0], 1, [False, True, False])}
         if cin % 8 == 0:
-            r["dgrad_ours_ms"] = timeit(lambda: NC._dgrad(dy, w, x.shape, s, pad))
-            r["dgrad_miopen_ms"] = timeit(lambda: torch.ops.aten.convolution_backward(
-                dyn, xn, wn, None, [s, s], [pad, pad], [1, 1], False, [0, 0], 1, [True, False, False]))
-        r["wgrad_ours_ms"] = timeit(lambda: NC._wgrad(dy, xp, wp.shape, s, pad))
-        r["wgrad_miopen_ms"] = timeit(lambda: torch.ops.aten.convolution_backward(
-            dyn, xn, wn, None, [s, s], [pad, pad], [1, 1], False, [0, 0], 1, [False, True, False]))
+            ops["dgrad"] = lambda: NC._dgrad(dy, w, x.shape, s, pad)
+            ref["dgrad"] = lambda: torch.ops.aten.convolution_backward(
+                dyn, xn, wn, None, [s, s], [pad, pad], [1, 1], False, [0, 0], 1, [True, False, False])
+        for op, fn in ops.items():
+            for kind in ("big", "small"):
+                with NG.force_kernel(kind):
+                    r[f"{op}_{kind}_ms"] = timeit(fn)
+            r[f"{op}_tuned_ms"] = timeit(fn)
+            r[f"{op}_miopen_ms"] = timeit(ref[op])
         for kk in list(r):
             if kk.endswith("_ms"):
                 r[kk] = round(r[kk], 4)

@@ -1,7 +1,9 @@
 """Thin wrapper over ``ddl_gemm`` (csrc/kernels/gemm.hip): modes, split-K policy, workspace."""
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -25,6 +27,20 @@ def set_big_gemm(enabled: bool) -> None:
     """Route GEMMs to the 256x256 8-phase kernel (True, default) or the 128x128 one."""
     global _force_small
     _force_small = not enabled
+
+
+_forced: Optional[str] = None
+
+
+@contextlib.contextmanager
+def force_kernel(kind: Optional[str]):
+    """Route every GEMM inside the block to "big" / "small" (tests, A/B benchmarks)."""
+    global _forced
+    prev, _forced = _forced, kind
+    try:
+        yield
+    finally:
+        _forced = prev
 
 
 def _zero_page(device) -> torch.Tensor:
@@ -65,35 +81,117 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
     return max(1, min(-(-2 * NUM_CU // tiles), nk // 8))
 
 
+def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr,
+            row_remap, residual, accumulate) -> None:
+    bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
+    out_f32 = 1 if C.dtype == torch.float32 else 0
+    ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device) if s > 1 else None
+    args = (mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, _lib.p(bias), bias_bf16,
+            ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws), 0 if ws is None else ws.numel(), conv_arr,
+            int(row_remap), _lib.p(residual), int(accumulate))
+    if kind == "big":
+        rc = _lib.fn("ddl_gemm_big2")(*args, _zero_page(C.device).data_ptr(), _lib.stream())
+    else:
+        rc = _lib.fn("ddl_gemm")(*args, _lib.stream())
+    if rc != 0:
+        raise RuntimeError(f"ddl_gemm[{kind}](mode={mode}, M={M}, N={N}, K={K}, splits={s}) failed: {rc}")
+
+
+def _big_allowed(mode: int, K: int, lda: int = 8, ldb: int = 8) -> bool:
+    # 16-byte LDS-DMA rows: K and both leading dimensions in whole 8-element chunks
+    return not _force_small and mode != MODE_CONVW and K % 8 == 0 and K >= 64 and lda % 8 == 0 and ldb % 8 == 0
+
+
+def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):
+    """(kernel, splits) variants worth timing for one GEMM shape."""
+    out = []
+    if _big_allowed(mode, K, lda, ldb):
+        out.append(("big", 1))
+        bs = big_splits(M, N, K)
+        if bs > 1 and not row_remap:
+            out.append(("big", bs))
+    out.append(("small", 1))
+    ps = pick_splits(M, N, K)
+    if ps > 1 and not row_remap:
+        out.append(("small", ps))
+    return out
+
+
+def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):
+    if use_big(mode, M, N, K) and _big_allowed(mode, K, lda, ldb):
+        return ("big", 1 if row_remap else big_splits(M, N, K))
+    return ("small", 1 if row_remap else pick_splits(M, N, K))
+
+
+# Measured kernel choice per GEMM signature (like cudnn.benchmark): the first call
+# of a shape times every candidate into scratch outputs and caches the fastest;
+# the bench's warmup steps absorb this.  DDL_GEMM_TUNE=0 uses the static heuristic.
+_tuned: dict = {}
+_TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
+
+
+def tuned_choices() -> dict:
+    return dict(_tuned)
+
+
+def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap, residual):
+    cands = _candidates(mode, M, N, K, row_remap, lda, ldb)
+    if len(cands) == 1:
+        return cands[0]
+    Cs = torch.empty_like(C)
+    aux_s = aux
+    if aux is not None and act in ("gelu", "relu", "tanh"):   # aux is an output for these
+        aux_s = torch.empty_like(aux)
+    best, best_t = None, float("inf")
+    for kind, s in cands:
+        run = lambda: _launch(kind, s, mode, A, lda, B, ldb, Cs, ldc, M, N, K, bias, act, aux_s,  # noqa: E731
+                              conv_arr, row_remap, residual, False)
+        run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            run()
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1)
+        if t < best_t:
+            best, best_t = (kind, s), t
+    return best
+
+
 def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
          M: int, N: int, K: int, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
          aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
          conv: Optional[Sequence[int]] = None, row_remap: bool = False,
-         residual: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+         residual: Optional[torch.Tensor] = None, accumulate: bool = False,
+         kernel: Optional[str] = None) -> torch.Tensor:
+    """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256) or "small" (128x128)."""
     conv_arr = None
     if conv is not None:
         conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
-    bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
-    out_f32 = 1 if C.dtype == torch.float32 else 0
-    if splits is None and use_big(mode, M, N, K):
-        s = 1 if row_remap else big_splits(M, N, K)
-        ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device) if s > 1 else None
-        rc = _lib.fn("ddl_gemm_big2")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
-                                      _lib.p(bias), bias_bf16, ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws),
-                                      0 if ws is None else ws.numel(), conv_arr, int(row_remap),
-                                      _lib.p(residual), int(accumulate), _zero_page(C.device).data_ptr(),
-                                      _lib.stream())
-        if rc != 0:
-            raise RuntimeError(f"ddl_gemm_big2(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
-        return C
-    s = 1 if row_remap else pick_splits(M, N, K, splits)
-    ws = None
-    if s > 1:
-        ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device)
-    rc = _lib.fn("ddl_gemm")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
-                             _lib.p(bias), bias_bf16, ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws),
-                             0 if ws is None else ws.numel(), conv_arr, int(row_remap), _lib.p(residual),
-                             int(accumulate), _lib.stream())
-    if rc != 0:
-        raise RuntimeError(f"ddl_gemm(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
+    kernel = kernel or _forced
+    if kernel is not None:
+        if kernel == "big" and not _big_allowed(mode, K, lda, ldb):
+            kernel = "small"              # no 256x256 variant for these
+        if kernel == "big":
+            choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
+        else:
+            choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
+    elif splits is not None:                       # explicit request: 128x128 kernel with that split
+        choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
+    elif _TUNE and not _force_small and C.is_cuda:
+        key = (mode, M, N, K, lda, ldb, ldc, tuple(conv) if conv is not None else None, bool(row_remap),
+               act, C.dtype, bias is not None)
+        choice = _tuned.get(key)
+        if choice is None:
+            if torch.cuda.is_current_stream_capturing():   # cannot time inside a graph capture
+                choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
+            else:
+                choice = _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
+                               residual)
+                _tuned[key] = choice
+    else:
+        choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
+    _launch(choice[0], choice[1], mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
+            residual, accumulate)
     return C

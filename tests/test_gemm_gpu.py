@@ -20,10 +20,16 @@ def _rel_err(a, b):
 SHAPES = [(128, 128, 64), (256, 384, 768), (77, 200, 136), (1000, 2304, 768), (130, 8, 72), (16, 1000, 2048)]
 
 
+@pytest.mark.parametrize("kernel", ["big", "small"])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm_modes(M, N, K):
+def test_gemm_modes(M, N, K, kernel):
     dev = gpu_device()
-    from databricks_distributed_deep_learning_amd.ops._native_gemm import MODE_NN, MODE_NT, MODE_TN, gemm
+    from databricks_distributed_deep_learning_amd.ops._native_gemm import MODE_NN, MODE_NT, MODE_TN, force_kernel
+    from databricks_distributed_deep_learning_amd.ops._native_gemm import gemm as _gemm
+
+    def gemm(*a, **k):
+        with force_kernel(kernel):
+            return _gemm(*a, **k)
     torch.manual_seed(0)
     a = torch.randn(M, K, device=dev).to(torch.bfloat16)
     w = torch.randn(N, K, device=dev).to(torch.bfloat16)
@@ -78,9 +84,17 @@ CONVS = [  # N, H, W, C, K, R, stride, pad
 ]
 
 
+@pytest.mark.parametrize("kernel", [None, "big", "small"])
 @pytest.mark.parametrize("N,H,W,C,K,R,stride,pad", CONVS)
-def test_conv_fwd_bwd(N, H, W, C, K, R, stride, pad):
+def test_conv_fwd_bwd(N, H, W, C, K, R, stride, pad, kernel):
     dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_conv
+    from databricks_distributed_deep_learning_amd.ops._native_gemm import force_kernel
+    with force_kernel(kernel):
+        _conv_case(dev, N, H, W, C, K, R, stride, pad)
+
+
+def _conv_case(dev, N, H, W, C, K, R, stride, pad):
     from databricks_distributed_deep_learning_amd.ops import _native_conv
     from databricks_distributed_deep_learning_amd.ops.conv import conv2d_reference
     torch.manual_seed(2)
@@ -112,23 +126,17 @@ def test_big_gemm_modes(mode, M, N, K):
     if mode == 0:      # C[M,N] = a w^T + b, gelu (aux = pre-activation)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         z = torch.empty_like(c)
-        NG.gemm(0, a, K, w, K, c, N, M, N, K, bias=b, act="gelu", aux=z, splits=None) if NG.use_big(0, M, N, K) else None
-        if not NG.use_big(0, M, N, K):
-            pytest.skip("shape below the big-kernel threshold")
+        NG.gemm(0, a, K, w, K, c, N, M, N, K, bias=b, act="gelu", aux=z, kernel="big")
         pre = a.float() @ w.float().t() + b.float()
         assert _rel_err(c, torch.nn.functional.gelu(pre)) < 1e-2 and _rel_err(z, pre) < 1e-2
     elif mode == 1:    # dx[M,K] = dy[M,N] w[N,K]
         dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
         dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
-        if not NG.use_big(1, M, K, N):
-            pytest.skip("shape below the big-kernel threshold")
-        NG.gemm(1, dy, N, w, K, dx, K, M, K, N)
+        NG.gemm(1, dy, N, w, K, dx, K, M, K, N, kernel="big")
         assert _rel_err(dx, dy.float() @ w.float()) < 1e-2
     else:              # dW[N,K] (+)= dy^T a, split-K; accumulate into an existing grad
         dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
-        if not NG.use_big(2, N, K, M):
-            pytest.skip("shape below the big-kernel threshold")
         dw = torch.randn(N, K, device=dev).to(torch.bfloat16)
         base = dw.float().clone()
-        NG.gemm(2, dy, N, a, K, dw, K, N, K, M, accumulate=True)
+        NG.gemm(2, dy, N, a, K, dw, K, N, K, M, accumulate=True, kernel="big")
         assert _rel_err(dw, base + dy.float().t() @ a.float()) < 1e-2
