@@ -88,7 +88,7 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
     newest = max(os.path.getmtime(o) for o in objs)
     if todo or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest:
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp",
-               "-L/opt/rocm/lib", "-Wl,--no-as-needed", "-lamdhip64"]
+               "-L/opt/rocm/lib", "-Wl,--no-as-needed", "-lamdhip64", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

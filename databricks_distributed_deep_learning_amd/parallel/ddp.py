@@ -19,7 +19,12 @@ Design (MI355X-first, not a DDP re-implementation):
   communication; with ``accumulate_fp32`` the micro-step gradients are summed
   into an fp32 arena so bf16 accumulation error does not grow with grad_accum;
 * the 1/world average is folded into the optimizer (``grad_scale``) instead of
-  an extra pass over the buckets.
+  an extra pass over the buckets;
+* ``comm="native"`` (default on GPU + RCCL) issues the bucket all-reduces
+  through the C++ engine in ``csrc/runtime/comm.cpp`` (its own RCCL
+  communicator and high-priority HIP stream, event-ordered after the producing
+  kernels, one stream wait before the optimizer); ``comm="torch"`` uses
+  ``torch.distributed.all_reduce(async_op=True)`` (gloo on CPU).
 """
 from __future__ import annotations
 
@@ -59,7 +64,8 @@ class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, arena: Optional[ParamArena] = None,
                  bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast_buffers: bool = False,
-                 accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True):
+                 accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True,
+                 comm: str = "auto"):
         super().__init__()
         self.module = module
         self.arena = arena if arena is not None else ParamArena(list(module.named_parameters()))
@@ -73,6 +79,16 @@ class DataParallel(nn.Module):
         self._acc_active = False
         if broadcast_init and self.world > 1:
             ddist.broadcast_tensors([self.arena.flat] + [b for b in module.buffers()])
+        self.native = None
+        if not isinstance(comm, str):        # an engine object (all_reduce / wait), e.g. for tests
+            self.native = comm
+        elif comm == "native" or (comm == "auto" and self.world > 1):
+            from .comm import NativeComm, native_available
+            if native_available() and self.arena.flat.is_cuda:
+                self.native = NativeComm(process_group)
+            elif comm == "native":
+                raise RuntimeError("comm='native' needs CUDA tensors, the native library and the nccl backend")
+        self.comm = "native" if self.native is not None else "torch"
         self.buckets = self._build_buckets(bucket_mb, first_bucket_mb)
         self._entry_bucket = {}
         for b in self.buckets:
@@ -142,8 +158,13 @@ class DataParallel(nn.Module):
             return
         b.launched = True
         b.payload = self._payload(b)
-        if self.world > 1:
-            b.handle = dist.all_reduce(b.payload, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self.native is not None or self.world > 1:
+            if self.native is not None:
+                # payload is the arena slice / fp32 accumulator / a converted copy held
+                # in b.payload until finish() -- alive until the comm stream is drained
+                self.native.all_reduce(b.payload)
+            else:
+                b.handle = dist.all_reduce(b.payload, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     # ------------------------------------------------------------------
     def forward(self, *args, **kwargs):
@@ -177,6 +198,8 @@ class DataParallel(nn.Module):
         for b in self.buckets:
             if b.handle is not None:
                 b.handle.wait()
+        if self.native is not None:
+            self.native.wait()
         if self._acc_active:
             out = self._acc32
         elif self.reduce_dtype != self.arena.dtype:

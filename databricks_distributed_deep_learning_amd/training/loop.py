@@ -59,7 +59,7 @@ class Trainer:
         rd = {"auto": None, "fp32": torch.float32, "bf16": torch.bfloat16}[cfg.grad_reduce_dtype]
         self.ddp = DataParallel(model, self.arena, bucket_mb=cfg.bucket_mb, first_bucket_mb=cfg.first_bucket_mb,
                                 reduce_dtype=rd, broadcast_buffers=cfg.broadcast_buffers,
-                                accumulate_fp32=accumulate_fp32)
+                                accumulate_fp32=accumulate_fp32, comm=cfg.comm)
         self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg)
         self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
         if cfg.batch_size <= 0:
@@ -166,6 +166,7 @@ class Trainer:
             "samples_per_sec": self.samples_per_step * steps / t_max if t_max > 0 else 0.0,
             "final_loss": last_loss, "native": ops.native_mode(),
             "buckets_mb": [round(b, 2) for b in self.ddp.bucket_sizes_mb()],
+            "comm": self.ddp.comm,
         }
         summary.update(memory_stats(self.device))
         if c.checkpoint_dir and not c.checkpoint_every:

@@ -33,7 +33,22 @@ def _data(n=8):
     return torch.randn(n, 10, generator=g), torch.randint(0, 3, (n,), generator=g)
 
 
-def _ddp_equivalence(accum):
+class _GlooEngine:
+    """Stand-in for the native RCCL engine (same all_reduce/wait contract) on gloo."""
+
+    def __init__(self):
+        self.calls, self.waits = [], 0
+
+    def all_reduce(self, t):
+        import torch.distributed as dist
+        self.calls.append(t.numel())
+        dist.all_reduce(t)
+
+    def wait(self):
+        self.waits += 1
+
+
+def _ddp_equivalence(accum, engine=False):
     import torch.distributed as dist
     from databricks_distributed_deep_learning_amd.optim import FlatSGD, ParamArena
     from databricks_distributed_deep_learning_amd.parallel import DataParallel
@@ -49,7 +64,8 @@ def _ddp_equivalence(accum):
     # DP: each rank gets its shard, split further into `accum` micro-batches
     m = _tiny_model()
     arena = ParamArena(list(m.named_parameters()))
-    ddp = DataParallel(m, arena, bucket_mb=0.0005, first_bucket_mb=0.0002)
+    eng = _GlooEngine() if engine else "auto"
+    ddp = DataParallel(m, arena, bucket_mb=0.0005, first_bucket_mb=0.0002, comm=eng)
     opt = FlatSGD(arena, lr=0.1, momentum=0.0)
     xs, ys = x[rank::world], y[rank::world]
     ddp.zero_grad()
@@ -61,7 +77,10 @@ def _ddp_equivalence(accum):
     g = ddp.finish()
     opt.step(g, grad_scale=1.0 / (world * accum))
     err = max((a - b).abs().max().item() for a, b in zip(m.parameters(), ref.parameters()))
-    return {"err": err, "nbuckets": len(ddp.buckets)}
+    out = {"err": err, "nbuckets": len(ddp.buckets), "comm": ddp.comm}
+    if engine:
+        out.update(engine_calls=len(eng.calls), engine_waits=eng.waits)
+    return out
 
 
 def _hvd_equivalence():
@@ -133,6 +152,16 @@ def test_ddp_matches_single_process_large_batch(accum):
     out = Distributor(num_processes=2, use_gpu=False).run(_ddp_equivalence, accum)
     assert out["err"] < 1e-6, out
     assert out["nbuckets"] > 1
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_ddp_engine_contract(accum):
+    """The reducer drives a comm engine (the native RCCL engine's contract): one
+    all_reduce per bucket, none on no_sync micro-steps, one wait per step."""
+    out = Distributor(num_processes=2, use_gpu=False).run(_ddp_equivalence, accum, True)
+    assert out["err"] < 1e-6, out
+    assert out["comm"] == "native"
+    assert out["engine_calls"] == out["nbuckets"] and out["engine_waits"] == 1, out
 
 
 def test_ddp_broadcasts_rank0_params():
