@@ -98,10 +98,12 @@ __global__ void bn_eval_coeffs_k(int C, const TP* __restrict__ gamma, const TP* 
     shift[c] = bb - rm[c] * g * inv;
 }
 
+// RELU + mask: one bit per element (byte i covers elements 8i..8i+7) records
+// y > 0, so the backward never re-reads y (16x less traffic than the bf16 output)
 template <typename T, bool RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
                                                   const float* __restrict__ scale, const float* __restrict__ shift,
-                                                  T* __restrict__ y, long n8, int C) {
+                                                  T* __restrict__ y, uint8_t* __restrict__ mask, long n8, int C) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
         const int c0 = (int)((i * 8) % C);
         float v[8], sc[8], sh[8];
@@ -110,20 +112,26 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, const
         load8(shift + c0, sh);
         float r[8];
         if (RES) load8(res + i * 8, r);
+        uint32_t bits = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float t = v[j] * sc[j] + sh[j];
             if (RES) t += r[j];
-            if (RELU) t = fmaxf(t, 0.f);
+            if (RELU) {
+                // the bit must agree with the stored (rounded) output
+                t = fmaxf(t, 0.f);
+                bits |= (to_f(from_f<T>(t)) > 0.f ? 1u : 0u) << j;
+            }
             v[j] = t;
         }
         store8(y + i * 8, v);
+        if (RELU && mask) mask[i] = (uint8_t)bits;
     }
 }
 
 // ------------------------------------------------------------------ BN backward
 template <typename T, bool RELU>
-__global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ dy, const T* __restrict__ yout,
+__global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                           const T* __restrict__ x, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, long M, int C,
                                                           int rows_per_blk, float* __restrict__ part) {
@@ -139,13 +147,13 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
     for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
 #pragma unroll 2
     for (long r = r0 + rr; r < r1; r += rpi) {
-        float g[8], xv[8], yo[8];
+        float g[8], xv[8];
         load8(dy + r * C + cg * 8, g);
         load8(x + r * C + cg * 8, xv);
-        if (RELU) load8(yout + r * C + cg * 8, yo);
+        const uint32_t bits = RELU ? mask[r * tpr + cg] : 0xffu;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float dz = RELU ? (yo[j] > 0.f ? g[j] : 0.f) : g[j];
+            const float dz = ((bits >> j) & 1u) ? g[j] : 0.f;
             a[j] += dz;
             b[j] += dz * (xv[j] - mu[j]) * is[j];
         }
@@ -186,16 +194,16 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restric
 }
 
 template <typename T, bool RELU, bool DRES>
-__global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ dy, const T* __restrict__ yout,
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                       const T* __restrict__ x, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd, const float* __restrict__ coef,
                                                       T* __restrict__ dx, T* __restrict__ dres, long n8, int C) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
         const int c0 = (int)((i * 8) % C);
-        float g[8], xv[8], yo[8], mu[8], is[8], k1[8], mb[8], mg[8];
+        float g[8], xv[8], mu[8], is[8], k1[8], mb[8], mg[8];
         load8(dy + i * 8, g);
         load8(x + i * 8, xv);
-        if (RELU) load8(yout + i * 8, yo);
+        const uint32_t bits = RELU ? mask[i] : 0xffu;
         load8(mean + c0, mu);
         load8(invstd + c0, is);
         load8(coef + c0, k1);
@@ -204,7 +212,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ dy, 
         float o[8], dz[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            dz[j] = RELU ? (yo[j] > 0.f ? g[j] : 0.f) : g[j];
+            dz[j] = ((bits >> j) & 1u) ? g[j] : 0.f;
             const float xh = (xv[j] - mu[j]) * is[j];
             o[j] = k1[j] * (dz[j] - mb[j] - xh * mg[j]);
         }
@@ -387,29 +395,30 @@ DDL_API int ddl_bn_eval_coeffs(int dtype, int C, const void* gamma, const void* 
 }
 
 template <typename T>
-static void bn_apply_dispatch(const T* x, const T* res, const float* sc, const float* sh, T* y, long n, int C, int relu,
-                              hipStream_t st) {
+static void bn_apply_dispatch(const T* x, const T* res, const float* sc, const float* sh, T* y, uint8_t* mask, long n,
+                              int C, int relu, hipStream_t st) {
     const long n8 = n / 8;
     const int g = grid_for(n8, 256, 8192);
     if (res) {
-        if (relu) bn_apply_k<T, true, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
-        else bn_apply_k<T, true, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
+        if (relu) bn_apply_k<T, true, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, mask, n8, C);
+        else bn_apply_k<T, true, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, mask, n8, C);
     } else {
-        if (relu) bn_apply_k<T, false, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
-        else bn_apply_k<T, false, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, n8, C);
+        if (relu) bn_apply_k<T, false, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, mask, n8, C);
+        else bn_apply_k<T, false, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, mask, n8, C);
     }
 }
 
 DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float* scale, const float* shift, void* y,
-                         long n, int C, int relu, hipStream_t st) {
+                         long n, int C, int relu, void* mask, hipStream_t st) {
     if (n % 8 || C % 8) return -1;
-    if (dtype == 1) bn_apply_dispatch((const bf16_t*)x, (const bf16_t*)res, scale, shift, (bf16_t*)y, n, C, relu, st);
-    else bn_apply_dispatch((const float*)x, (const float*)res, scale, shift, (float*)y, n, C, relu, st);
+    uint8_t* mk = (uint8_t*)mask;
+    if (dtype == 1) bn_apply_dispatch((const bf16_t*)x, (const bf16_t*)res, scale, shift, (bf16_t*)y, mk, n, C, relu, st);
+    else bn_apply_dispatch((const float*)x, (const float*)res, scale, shift, (float*)y, mk, n, C, relu, st);
     DDL_RETURN_LAUNCH();
 }
 
 template <typename T>
-static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float* mean, const float* invstd,
+static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const float* mean, const float* invstd,
                             const T* gamma, long M, int C, int relu, float* part, T* dgamma, T* dbeta, float* coef,
                             T* dx, T* dres, int acc, hipStream_t st) {
     const int nblk = ddl_bn_stats_nblk(M, C);
@@ -430,15 +439,17 @@ static void bn_bwd_dispatch(const T* dy, const T* yout, const T* x, const float*
     }
 }
 
-DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* yout, const void* x, const float* mean,
+// relu: `mask` is the bit mask written by ddl_bn_apply (required when relu != 0)
+DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* mask, const void* x, const float* mean,
                        const float* invstd, const void* gamma, long M, int C, int relu, float* part, void* dgamma,
                        void* dbeta, float* coef, void* dx, void* dres, int acc_params, hipStream_t st) {
-    if (C % 8 || (BN_NT % (C / 8) != 0)) return -1;
+    if (C % 8 || (BN_NT % (C / 8) != 0) || (relu && !mask)) return -1;
+    const uint8_t* yout = (const uint8_t*)mask;
     if (dtype == 1)
-        bn_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)yout, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M,
+        bn_bwd_dispatch((const bf16_t*)dy, yout, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M,
                         C, relu, part, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
     else
-        bn_bwd_dispatch((const float*)dy, (const float*)yout, (const float*)x, mean, invstd, (const float*)gamma, M, C,
+        bn_bwd_dispatch((const float*)dy, yout, (const float*)x, mean, invstd, (const float*)gamma, M, C,
                         relu, part, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st);
     DDL_RETURN_LAUNCH();
 }

@@ -28,16 +28,18 @@ class _BatchNormTrain(torch.autograd.Function):
              float(momentum), float(eps), p(part), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
         res = residual.contiguous() if residual is not None else None
         y = torch.empty_like(x)
-        call("ddl_bn_apply", dt, p(x), p(res), p(stats[2]), p(stats[3]), p(y), x.numel(), C, int(relu))
+        # ReLU: 1 bit per element for the backward instead of re-reading y
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if relu else None
+        call("ddl_bn_apply", dt, p(x), p(res), p(stats[2]), p(stats[3]), p(y), x.numel(), C, int(relu), p(mask))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.params = (weight, bias)
-        ctx.save_for_backward(x, y if relu else None, weight, stats)
+        ctx.save_for_backward(x, mask, weight, stats)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, stats = ctx.saved_tensors
+        x, mask, weight, stats = ctx.saved_tensors
         dy = dy.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -54,7 +56,7 @@ class _BatchNormTrain(torch.autograd.Function):
         else:
             dgamma = torch.empty_like(weight) if weight is not None else None
             dbeta = torch.empty_like(weight) if weight is not None else None
-        call("ddl_bn_bwd", dcode(x), p(dy), p(y), p(x), p(stats[0]), p(stats[1]), p(weight), M, C, int(ctx.relu),
+        call("ddl_bn_bwd", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M, C, int(ctx.relu),
              p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
         if direct:
             grad_ready(ctx.params[0])
@@ -75,7 +77,7 @@ class _BatchNormEval(torch.autograd.Function):
              p(coeff[0]), p(coeff[1]))
         y = torch.empty_like(x)
         res = residual.contiguous() if residual is not None else None
-        call("ddl_bn_apply", dcode(x), p(x), p(res), p(coeff[0]), p(coeff[1]), p(y), x.numel(), C, int(relu))
+        call("ddl_bn_apply", dcode(x), p(x), p(res), p(coeff[0]), p(coeff[1]), p(y), x.numel(), C, int(relu), None)
         return y
 
 
