@@ -49,9 +49,12 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
     ap.add_argument("--bert-batch", type=int, default=0, help="BERT-base per-GPU batch (default 128)")
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"])
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--cuda-graph", action="store_true")
     args = ap.parse_args()
+    # the first step times GEMM kernel candidates per shape (ops/_native_gemm.py);
+    # it must never land inside the timed region
+    args.warmup = max(1, args.warmup)
 
     import torch
     from databricks_distributed_deep_learning_amd.parallel import dist as ddist

@@ -3,8 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstring>
+#include <cstdint>
 
 extern "C" int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M,
+                             int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
+                             int splits, void* ws, long ws_elems, const int* conv, int row_remap, const void* res,
+                             int accumulate, const void* zero, hipStream_t st);
+extern "C" int ddl_gemm_big3(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M,
                              int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
                              int splits, void* ws, long ws_elems, const int* conv, int row_remap, const void* res,
                              int accumulate, const void* zero, hipStream_t st);
@@ -19,20 +25,34 @@ int main() {
     hipMalloc(&B, 8192L * 8192 * 2);
     hipMalloc(&C, 8192L * 8192 * 2);
     hipMalloc(&Z, 256);
-    hipMemset(A, 0x3c, 8192L * 8192 * 2);
-    hipMemset(B, 0x3c, 8192L * 8192 * 2);
+    {   // uniform random bf16 in [-1, 1) (constant operands read high)
+        std::vector<uint16_t> h(8192L * 8192);
+        uint32_t s = 12345;
+        for (auto& v : h) {
+            s = s * 1664525u + 1013904223u;
+            const float f = ((s >> 8) * (1.0f / 16777216.0f)) * 2.f - 1.f;
+            uint32_t u;
+            memcpy(&u, &f, 4);
+            v = (uint16_t)(u >> 16);
+        }
+        hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+        hipMemcpy(B, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    }
     hipMemset(Z, 0, 256);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     for (auto& s : shapes) {
         const int M = s[0], N = s[1], K = s[2];
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < 3; ++v) {
             auto run = [&] {
                 if (v == 0)
                     ddl_gemm_big(A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 0);
-                else
+                else if (v == 1)
                     ddl_gemm_big2(0, A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 1, nullptr, 0, nullptr,
+                                  0, nullptr, 0, Z, 0);
+                else
+                    ddl_gemm_big3(0, A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 1, nullptr, 0, nullptr,
                                   0, nullptr, 0, Z, 0);
             };
             for (int i = 0; i < 5; ++i) run();
@@ -44,7 +64,7 @@ int main() {
             float ms;
             hipEventElapsedTime(&ms, e0, e1);
             ms /= it;
-            printf("%s M=%d N=%d K=%d  %.4f ms  %.1f TF\n", v == 0 ? "v1" : "v2", M, N, K, ms,
+            printf("%s M=%d N=%d K=%d  %.4f ms  %.1f TF\n", v == 0 ? "v1" : v == 1 ? "v2" : "v2-stagger", M, N, K, ms,
                    2.0 * M * N * K / ms / 1e9);
         }
     }

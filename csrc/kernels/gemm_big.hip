@@ -35,6 +35,12 @@
 
 namespace {
 
+#ifndef DDL_STAGGER
+#define DDL_STAGGER 1
+#endif
+#ifndef DDL_GROUP_M
+#define DDL_GROUP_M 8      // tile rows per L2 group (tile order inside an XCD's share)
+#endif
 constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
 constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
@@ -256,6 +262,15 @@ __device__ __forceinline__ bf16x8 frag(const char* hbase, int rbase, int kk) {
 }
 
 #define BARRIER() __builtin_amdgcn_s_barrier()
+// End of a read phase.  With the staggered wave groups a half-tile may be
+// restaged by the other group in the very next phase, so this wave's fragment
+// reads must have completed BEFORE it arrives at the barrier (WAR); the wait
+// costs nothing visible because the other group is in its MFMA cluster.
+#if DDL_STAGGER
+#define READS_DONE_BARRIER() do { LGKM0(); BARRIER(); } while (0)
+#else
+#define READS_DONE_BARRIER() do { BARRIER(); LGKM0(); } while (0)
+#endif
 #define LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 #define VM6() asm volatile("s_waitcnt vmcnt(6)" ::: "memory")
 #define VM0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
@@ -351,7 +366,14 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
     const int bid = blockIdx.x;
     const int xcd = bid & 7, qn_ = nwg >> 3, rn = nwg & 7;
     const int wg = (xcd < rn ? xcd * (qn_ + 1) : rn * (qn_ + 1) + (xcd - rn) * qn_) + (bid >> 3);
-    const int tm = wg / p.tiles_n, tn = wg - tm * p.tiles_n;
+    // grouped order: consecutive tiles (the ones an XCD runs together) cover a
+    // GROUP_M x k block of tiles instead of one long row, so the A and B panels
+    // they stream stay L2-resident at large M, N
+    const int per_group = DDL_GROUP_M * p.tiles_n;
+    const int grp = wg / per_group, first_m = grp * DDL_GROUP_M;
+    const int gsz = min(p.tiles_m - first_m, DDL_GROUP_M);
+    const int wl = wg - grp * per_group;
+    const int tm = first_m + wl % gsz, tn = wl / gsz;
     const int m0 = tm * TB, n0 = tn * TB;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = w >> 2, wn = w & 3;
@@ -411,19 +433,19 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
         readA(0, 0);
         readB(0, 0, fb0);
         if (stO1) sa.stage(p, smem, 1, 1, kE + 1);
-        BARRIER(); LGKM0();
+        READS_DONE_BARRIER();
         mma(0, 0, fb0);
         BARRIER();
         // phase 2: E (0,1)
         readB(0, 1, fb1);
         if (more) sa.stage(p, smem, 0, 0, kE + 2);
-        BARRIER(); LGKM0();
+        READS_DONE_BARRIER();
         mma(0, 1, fb1);
         BARRIER();
         // phase 3: E (1,1)
         readA(0, 1);
         if (more) sb.stage(p, smem, 0, 0, kE + 2);
-        BARRIER(); LGKM0();
+        READS_DONE_BARRIER();
         mma(1, 1, fb1);
         BARRIER();
         // phase 4: E (1,0); retire O(kE+1)
@@ -448,6 +470,11 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
             VM0();
         }
         BARRIER();
+#if DDL_STAGGER
+        // wave groups wm=0/1 run one barrier apart: one group's MFMA cluster
+        // overlaps the other's LDS reads / DMA issue on the same SIMD
+        if (wm == 1) BARRIER();
+#endif
         const int pairs = nK / 2;
         for (int it = 0; it < pairs; ++it) {
             const int kE = kt0 + 2 * it, kO = kE + 1;
@@ -458,19 +485,19 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
             readA(1, 0);
             readB(1, 0, fb0);
             if (more) sa.stage(p, smem, 0, 1, kE + 2);
-            BARRIER(); LGKM0();
+            READS_DONE_BARRIER();
             mma(0, 0, fb0);
             BARRIER();
             // phase 6: O (0,1)
             readB(1, 1, fb1);
             if (moreO) sa.stage(p, smem, 1, 0, kO + 2);
-            BARRIER(); LGKM0();
+            READS_DONE_BARRIER();
             mma(0, 1, fb1);
             BARRIER();
             // phase 7: O (1,1)
             readA(1, 1);
             if (moreO) sb.stage(p, smem, 1, 0, kO + 2);
-            BARRIER(); LGKM0();
+            READS_DONE_BARRIER();
             mma(1, 1, fb1);
             BARRIER();
             // phase 8: O (1,0); retire E(kE+2)
@@ -481,6 +508,9 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
         }
         // odd tile count: the last E tile (fully landed: phase 8 waited vmcnt(0))
         if (nK & 1) phasesE(kt_end - 1, false, false);
+#if DDL_STAGGER
+        if (wm == 0) BARRIER();
+#endif
     }
 
     // ---------------- epilogue

@@ -44,7 +44,7 @@ class TrainConfig:
     lr_warmup_steps: int = 0
     # ---- distributed ------------------------------------------------------
     backend: str = "auto"            # auto|nccl|gloo  (nccl == RCCL on ROCm)
-    bucket_mb: float = 64.0          # gradient bucket size for the reducer
+    bucket_mb: float = 25.0          # gradient bucket size for the reducer (xGMI ring: few-MB latency floor)
     first_bucket_mb: float = 4.0     # small first bucket so comm starts early
     comm: str = "auto"               # gradient all-reduce engine: auto|native (C++ RCCL engine)|torch
     grad_reduce_dtype: str = "auto"  # auto|fp32|bf16  all-reduce payload dtype

@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import json
 import os
 from typing import Optional, Sequence
 
@@ -103,17 +104,15 @@ def _big_allowed(mode: int, K: int, lda: int = 8, ldb: int = 8) -> bool:
 
 
 def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):
-    """(kernel, splits) variants worth timing for one GEMM shape."""
+    """(kernel, splits) variants worth timing for one GEMM shape: each kernel at
+    no split, its heuristic split and half of it (split-K trades parallelism
+    against fp32 partial-slab traffic, which the heuristic cannot price)."""
     out = []
     if _big_allowed(mode, K, lda, ldb):
-        out.append(("big", 1))
-        bs = big_splits(M, N, K)
-        if bs > 1 and not row_remap:
-            out.append(("big", bs))
-    out.append(("small", 1))
-    ps = pick_splits(M, N, K)
-    if ps > 1 and not row_remap:
-        out.append(("small", ps))
+        bs = 1 if row_remap else big_splits(M, N, K)
+        out += [("big", s) for s in sorted({1, max(1, bs // 2), bs})]
+    ps = 1 if row_remap else pick_splits(M, N, K)
+    out += [("small", s) for s in sorted({1, max(1, ps // 2), ps})]
     return out
 
 
@@ -128,6 +127,34 @@ def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb
 # the bench's warmup steps absorb this.  DDL_GEMM_TUNE=0 uses the static heuristic.
 _tuned: dict = {}
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
+# optional persistent cache (JSON): later processes skip the timing runs
+_CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
+
+
+def _load_cache() -> None:
+    if not _CACHE_PATH or not os.path.exists(_CACHE_PATH):
+        return
+    try:
+        with open(_CACHE_PATH) as f:
+            for k, v in json.load(f).items():
+                _tuned[k] = tuple(v)
+    except (OSError, ValueError):
+        pass
+
+
+def _save_cache() -> None:
+    if not _CACHE_PATH:
+        return
+    tmp = f"{_CACHE_PATH}.{os.getpid()}.tmp"
+    try:
+        with open(tmp, "w") as f:
+            json.dump({k: list(v) for k, v in _tuned.items()}, f)
+        os.replace(tmp, _CACHE_PATH)
+    except OSError:
+        pass
+
+
+_load_cache()
 
 
 def tuned_choices() -> dict:
@@ -180,8 +207,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
     elif splits is not None:                       # explicit request: 128x128 kernel with that split
         choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
     elif _TUNE and not _force_small and C.is_cuda:
-        key = (mode, M, N, K, lda, ldb, ldc, tuple(conv) if conv is not None else None, bool(row_remap),
-               act, C.dtype, bias is not None)
+        key = f"{mode}|{M}|{N}|{K}|{lda}|{ldb}|{ldc}|{tuple(conv) if conv is not None else ''}|{int(row_remap)}|" \
+              f"{act}|{C.dtype}|{int(bias is not None)}"
         choice = _tuned.get(key)
         if choice is None:
             if torch.cuda.is_current_stream_capturing():   # cannot time inside a graph capture
@@ -190,6 +217,7 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
                 choice = _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
                                residual)
                 _tuned[key] = choice
+                _save_cache()
     else:
         choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
     _launch(choice[0], choice[1], mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,

@@ -8,7 +8,8 @@ Design (MI355X-first, not a DDP re-implementation):
   memory itself;
 * bucket boundaries: a small first bucket (``first_bucket_mb``, default 4 MB) so
   the first RCCL ring starts while most of backward is still running, then
-  large buckets (``bucket_mb``, default 64 MB) — an 8-GPU xGMI ring is
+  ``bucket_mb`` buckets (default 25 MB: the last bucket's all-reduce is the
+  exposed part, so it must stay small; bigger ones buy nothing) — an 8-GPU xGMI ring is
   per-link bound (~153 GB/s/link, 7 links), so few large messages that let RCCL
   spread channels over all links beat many small latency-bound ones;
 * readiness: ``register_post_accumulate_grad_hook`` per parameter counts down a
@@ -62,7 +63,7 @@ class DataParallel(nn.Module):
     """
 
     def __init__(self, module: nn.Module, arena: Optional[ParamArena] = None,
-                 bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
+                 bucket_mb: float = 25.0, first_bucket_mb: float = 4.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast_buffers: bool = False,
                  accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True,
                  comm: str = "auto"):
