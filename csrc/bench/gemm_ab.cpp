@@ -21,6 +21,7 @@ int main() {
     const int shapes[][3] = {{16384, 2304, 768}, {16384, 768, 768}, {16384, 3072, 768}, {16384, 768, 3072},
                              {4096, 4096, 4096}, {8192, 8192, 8192}};
     void *A, *B, *C, *Z;
+    (void)ddl_gemm_big;
     hipMalloc(&A, 8192L * 8192 * 2);
     hipMalloc(&B, 8192L * 8192 * 2);
     hipMalloc(&C, 8192L * 8192 * 2);
@@ -42,18 +43,26 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (auto& s : shapes) {
-        const int M = s[0], N = s[1], K = s[2];
-        for (int v = 0; v < 3; ++v) {
+    // mode 0 NT: C[M,N] = A[M,K] B[N,K]^T; mode 1 NN: A[M,K], B[K,N] (KO); mode 2 TN: A[K,M] (KO), B[K,N] (KO)
+    struct Case { int mode, M, N, K, splits; };
+    const Case cases[] = {
+        {0, 16384, 2304, 768, 1}, {0, 16384, 768, 768, 1}, {0, 16384, 3072, 768, 1}, {0, 16384, 768, 3072, 1},
+        {0, 4096, 4096, 4096, 1}, {0, 8192, 8192, 8192, 1},
+        {1, 16384, 768, 2304, 1}, {1, 16384, 768, 768, 1}, {1, 16384, 3072, 768, 1}, {1, 16384, 768, 3072, 1},
+        {1, 4096, 4096, 4096, 1},
+        {2, 2304, 768, 16384, 4}, {2, 768, 768, 16384, 8}, {2, 3072, 768, 16384, 4}, {2, 768, 3072, 16384, 4},
+        {2, 4096, 4096, 4096, 1}};
+    float* ws;
+    hipMalloc(&ws, 8L * 4096 * 4096 * 4);
+    for (const Case& c : cases) {
+        const int M = c.M, N = c.N, K = c.K;
+        const long lda = c.mode == 2 ? M : K;
+        const long ldb = c.mode == 0 ? K : N;
+        for (int v = 1; v < 3; ++v) {
             auto run = [&] {
-                if (v == 0)
-                    ddl_gemm_big(A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 0);
-                else if (v == 1)
-                    ddl_gemm_big2(0, A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 1, nullptr, 0, nullptr,
-                                  0, nullptr, 0, Z, 0);
-                else
-                    ddl_gemm_big3(0, A, K, B, K, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 1, nullptr, 0, nullptr,
-                                  0, nullptr, 0, Z, 0);
+                auto f = v == 1 ? ddl_gemm_big2 : ddl_gemm_big3;
+                f(c.mode, A, lda, B, ldb, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, c.splits, ws, 8L * 4096 * 4096,
+                  nullptr, 0, nullptr, 0, Z, 0);
             };
             for (int i = 0; i < 5; ++i) run();
             hipEventRecord(e0, 0);
@@ -64,8 +73,8 @@ int main() {
             float ms;
             hipEventElapsedTime(&ms, e0, e1);
             ms /= it;
-            printf("%s M=%d N=%d K=%d  %.4f ms  %.1f TF\n", v == 0 ? "v1" : v == 1 ? "v2" : "v2-stagger", M, N, K, ms,
-                   2.0 * M * N * K / ms / 1e9);
+            printf("%s mode=%d M=%d N=%d K=%d splits=%d  %.4f ms  %.1f TF\n", v == 1 ? "old" : "new", c.mode, M, N, K,
+                   c.splits, ms, 2.0 * M * N * K / ms / 1e9);
         }
     }
     return 0;
