@@ -33,7 +33,7 @@ def run_one(model: str, args, world: int):
     else:
         cfg = get_preset("bert_base_ddp", batch_size=args.bert_batch or 128, dropout=0.1)
     cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
-                      bucket_mb=args.bucket_mb, cuda_graph=args.cuda_graph)
+                      bucket_mb=args.bucket_mb, cuda_graph=args.cuda_graph, backend=args.backend)
     tr = Trainer(cfg)
     s = tr.run()
     del tr
@@ -51,6 +51,8 @@ def main() -> int:
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--cuda-graph", action="store_true")
+    ap.add_argument("--backend", default=os.environ.get("DDL_BACKEND", "auto"),
+                    help="process-group backend (auto = RCCL on GPU); gloo only for 1-GPU multi-rank rehearsals")
     args = ap.parse_args()
     # the first step times GEMM kernel candidates per shape (ops/_native_gemm.py);
     # it must never land inside the timed region
@@ -62,7 +64,7 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    ddist.init("auto")
+    ddist.init(args.backend)
     results = {}
     order = ["resnet50", "bert_base"] if args.model == "both" else [args.model]
     for m in order:
@@ -94,6 +96,7 @@ def main() -> int:
             "optimizer": head["optimizer"],
             "parallelism": f"dp{world}",
             "native_kernels": head["native"],
+            "grad_comm": head.get("comm"),
         },
     }
     if "bert_base" in results and is_r50:

@@ -76,6 +76,8 @@ def init(backend: str = "auto", timeout_s: float = 600.0, use_gpu: Optional[bool
     if is_initialized():
         return
     backend = resolve_backend(backend, use_gpu)
+    if use_gpu is None:
+        use_gpu = gpu_available()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(_free_port()))
     os.environ.setdefault("RANK", "0")
@@ -90,7 +92,9 @@ def init(backend: str = "auto", timeout_s: float = 600.0, use_gpu: Optional[bool
         _DEVICE = torch.device("cuda", lr)
         kw["device_id"] = _DEVICE
     else:
-        _DEVICE = torch.device("cuda", local_rank()) if (use_gpu and gpu_available()) else torch.device("cpu")
+        # gloo with GPU tensors (e.g. several ranks sharing one GPU in a rehearsal)
+        _DEVICE = torch.device("cuda", local_rank() % max(1, torch.cuda.device_count())) \
+            if (use_gpu and gpu_available()) else torch.device("cpu")
     dist.init_process_group(backend=backend, init_method="env://",
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
