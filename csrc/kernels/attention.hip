@@ -228,18 +228,29 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
 }
 
 // delta[b,h,q] = sum_d dO[q][d] * O[q][d]
+// delta[b,h,q] = sum_d dO * O.  8 lanes per (b, s, h) row, 16-B loads, a 3-step
+// xor-shuffle reduction: a pure streaming pass over dO and O.
 __global__ __launch_bounds__(256) void attn_delta_k(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out,
                                                     float* __restrict__ delta, int B, int S, int H) {
-    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);   // (b, s, h) flattened as (b*S + s)*H + h
-    if (row >= (long)B * S * H) return;
-    const int lane = threadIdx.x & 63;
-    const float a = bf2f(dout[row * D + lane]) * bf2f(out[row * D + lane]);
-    const float s = wave_sum(a);
-    if (lane == 0) {
+    const long row = ((long)blockIdx.x * 256 + threadIdx.x) >> 3;   // (b*S + s)*H + h
+    const int part = threadIdx.x & 7;
+    const bool ok = row < (long)B * S * H;
+    float a = 0.f;
+    if (ok) {
+        float x[8], y[8];
+        load8(dout + row * D + part * 8, x);
+        load8(out + row * D + part * 8, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a += x[j] * y[j];
+    }
+    a += __shfl_xor(a, 1);
+    a += __shfl_xor(a, 2);
+    a += __shfl_xor(a, 4);
+    if (ok && part == 0) {
         const long bs = row / H;
         const int h = (int)(row - bs * H);
         const long b = bs / S, q = bs - b * S;
-        delta[(b * H + h) * S + q] = s;
+        delta[(b * H + h) * S + q] = a;
     }
 }
 
@@ -450,7 +461,7 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
                          float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop, uint64_t seed,
                          hipStream_t st) {
     const long rows = (long)B * S * H;
-    attn_delta_k<<<(int)((rows + 3) / 4), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
+    attn_delta_k<<<(int)((rows * 8 + 255) / 256), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
     dim3 grid((S + TK - 1) / TK, B * H);
     attn_bwd_dkv_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B,
                                          S, H, scale, p_drop, seed);

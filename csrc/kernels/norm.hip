@@ -489,7 +489,7 @@ DDL_API int ddl_ln_fwd(int dtype, const void* x, const void* res, long res_rows,
     DDL_RETURN_LAUNCH();
 }
 
-DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(1024, (rows + 31) / 32)); }
+DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(1024, (rows + 15) / 16)); }
 
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
