@@ -76,8 +76,12 @@ __device__ __forceinline__ int swz_ko(int r) { return 2 * ((r & 3) | (((r >> 3) 
 
 // ------------------------------------------------------------------ loaders
 // Each thread stages 4 chunks (16 B) of each operand per K-step.
-template <int L, bool IS_A>
+template <int L, bool IS_A, int ROWS = 128>
 struct Loader {
+    // ROWS = 64 (narrow B tile): KC rows (t>>3) + 32 i for i < 2; KO/CONVW chunk c = t&7
+    // and k-rows (t>>3) + 32 i.  The LDS images keep the 128-row layouts (only
+    // the first 64 rows / columns are filled), so fragment reads are unchanged.
+    static constexpr int NCH = ROWS / 32;   // 16-B chunks per thread
     // KC / CONV: thread -> chunk c = t&7, rows (t>>3) + 32 i
     // KO / CONVW: thread -> chunk c = t&15, k-rows (t>>4) + 16 i
     const bf16_t* base;
@@ -117,7 +121,7 @@ struct Loader {
         }
         if (L == CONVW) {
             const ConvDesc& cd = p.cd;
-            const int col = r0 + 8 * (t & 15);
+            const int col = r0 + 8 * (ROWS == 128 ? (t & 15) : (t & 7));
             colok = col < rows_total;
             const int cc = colok ? col : 0;
             const int tap = (int)fdiv((uint32_t)cc, cd.fd_C);
@@ -134,16 +138,17 @@ struct Loader {
             const int c = t & 7;
             const int k = k0 + 8 * c;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < NCH; ++i) {
                 const int r = r0 + (t >> 3) + 32 * i;
                 const bool ok = r < rows_total && k < K;
                 v[i] = sel(ok, ldg16(ok ? base + (long)r * ld + k : base), z);
             }
         } else if (L == KO) {
-            const int col = r0 + 8 * (t & 15);
+            const int col = r0 + 8 * (ROWS == 128 ? (t & 15) : (t & 7));
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int k = k0 + (t >> 4) + 16 * i;
+                const int k = k0 + (ROWS == 128 ? (t >> 4) + 16 * i : (t >> 3) + 32 * (i & 1));
+                if (ROWS != 128 && i >= 2) break;
                 const bool ok = k < K && col < rows_total;
                 v[i] = sel(ok, ldg16(ok ? base + (long)k * ld + col : base), z);
             }
@@ -166,7 +171,8 @@ struct Loader {
             const ConvDesc& cd = p.cd;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int m = k0 + (t >> 4) + 16 * i;
+                if (ROWS != 128 && i >= 2) break;
+                const int m = k0 + (ROWS == 128 ? (t >> 4) + 16 * i : (t >> 3) + 32 * i);
                 bool ok = colok && m < K;
                 const int mm = ok ? m : 0;
                 const int n = (int)fdiv((uint32_t)mm, cd.fd_PQ);
@@ -186,15 +192,22 @@ struct Loader {
         if (L == KC || L == CONV) {
             const int c = t & 7;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < NCH; ++i) {
                 const int r = (t >> 3) + 32 * i;
                 *reinterpret_cast<uint4*>(lds + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = v[i];
             }
-        } else {
+        } else if (ROWS == 128) {
             const int c = t & 15;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = (t >> 4) + 16 * i;
+                *reinterpret_cast<uint4*>(lds + r * 256 + ((c ^ swz_ko(r)) << 4)) = v[i];
+            }
+        } else {
+            const int c = t & 7;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = (t >> 3) + 32 * i;
                 *reinterpret_cast<uint4*>(lds + r * 256 + ((c ^ swz_ko(r)) << 4)) = v[i];
             }
         }
@@ -246,8 +259,10 @@ __device__ __forceinline__ long out_row(const Params& p, int m) {
     return ((long)n * cd.OH + pp * cd.ostep + cd.oa) * cd.OW + qq * cd.ostep + cd.ob;
 }
 
-template <int LA, int LB>
+template <int LA, int LB, int BNT>
 __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
+    constexpr int WN = BNT / 2;        // wave tile N extent (64 or 32)
+    constexpr int NJ = WN / 16;        // MFMA column tiles per wave
     __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
     // ---- XCD-aware bijective tile remap
     const int nwg = p.tiles_m * p.tiles_n;
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
     const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
     const int wg = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
     const int tm = wg / p.tiles_n, tn = wg - tm * p.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = tm * BM, n0 = tn * BNT;
     const int split = blockIdx.y;
 
     const int nk_total = (p.K + BK - 1) / BK;
@@ -263,18 +278,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
     const int kt1 = min(nk_total, kt0 + p.kt_per_split);
 
     Loader<LA, true> la;
-    Loader<LB, false> lb;
+    Loader<LB, false, BNT> lb;
     la.init(p, m0);
     lb.init(p, n0);
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = w & 1, wn = w >> 1;
 
-    f32x4 acc[4][4];
+    f32x4 acc[4][NJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     if (kt0 < kt1) {
         uint4 ra[4], rb[4];
@@ -294,15 +309,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
             }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                bf16x8 af[4], bfr[4];
+                bf16x8 af[4], bfr[NJ];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) af[i] = read_frag<LA>(sa, wm * 64 + i * 16, kk);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bfr[j] = read_frag<LB>(sb, wn * 64 + j * 16, kk);
+                for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<LB>(sb, wn * WN + j * 16, kk);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
             }
             if (more) {
@@ -322,8 +337,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
         if (m >= p.M) continue;
         const long orow = out_row(p, m);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = n0 + wn * 64 + j * 16 + 4 * g;
+        for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WN + j * 16 + 4 * g;
             if (n >= p.N) continue;
             float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
             const bool full = n + 3 < p.N;
@@ -437,10 +452,10 @@ __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ p
     }
 }
 
-template <int LA, int LB>
+template <int LA, int LB, int BNT = 128>
 int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t st) {
     p.tiles_m = (p.M + BM - 1) / BM;
-    p.tiles_n = (p.N + BN - 1) / BN;
+    p.tiles_n = (p.N + BNT - 1) / BNT;
     const int nk = (p.K + BK - 1) / BK;
     if (splits < 1) splits = 1;
     if (splits > nk) splits = nk > 0 ? nk : 1;
@@ -460,7 +475,7 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
         p.accumulate = 0;
     }
     dim3 grid(p.tiles_m * p.tiles_n, splits);
-    hipLaunchKernelGGL((gemm_k<LA, LB>), grid, dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_k<LA, LB, BNT>), grid, dim3(NT), 0, st, p);
     if (splits > 1) {
         const long total = (long)p.M * p.N;
         const int g = (int)std::min<long>(8192, (total + 255) / 256);
@@ -490,10 +505,10 @@ void fill_conv(ConvDesc& cd, const int* d) {
 //       3 = A CONV, B KC (conv fwd / dgrad by implicit GEMM; conv desc required)
 //       4 = A KO, B CONVW (conv wgrad; conv desc required)
 // act: 0 none, 1 gelu (aux <- pre-activation if aux), 2 relu, 3 tanh, 4 dgelu (v *= gelu'(aux))
-DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
-                     int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
-                     float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
-                     int accumulate, hipStream_t st) {
+static int gemm_entry(int narrow, int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
+                      int M, int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
+                      int splits, float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
+                      int accumulate, hipStream_t st) {
     Params p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
@@ -503,6 +518,16 @@ DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb,
     p.accumulate = accumulate;
     if (conv) fill_conv(p.cd, conv);
     if (M <= 0 || N <= 0) return 0;
+    if (narrow) {   // 128 x 64 tiles: outputs with 64 (or 64 + k*128) columns waste no MFMA work
+        switch (mode) {
+            case 0: return launch<KC, KC, 64>(p, workspace, ws_elems, splits, st);
+            case 1: return launch<KC, KO, 64>(p, workspace, ws_elems, splits, st);
+            case 2: return launch<KO, KO, 64>(p, workspace, ws_elems, splits, st);
+            case 3: return launch<CONV, KC, 64>(p, workspace, ws_elems, splits, st);
+            case 4: return launch<KO, CONVW, 64>(p, workspace, ws_elems, splits, st);
+            default: return -1;
+        }
+    }
     switch (mode) {
         case 0: return launch<KC, KC>(p, workspace, ws_elems, splits, st);
         case 1: return launch<KC, KO>(p, workspace, ws_elems, splits, st);
@@ -511,4 +536,22 @@ DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb,
         case 4: return launch<KO, CONVW>(p, workspace, ws_elems, splits, st);
         default: return -1;
     }
+}
+
+
+
+DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
+                     int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
+                     float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
+                     int accumulate, hipStream_t st) {
+    return gemm_entry(0, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, bias_bf16, act, aux, out_f32, splits, workspace,
+                      ws_elems, conv, row_remap, res, accumulate, st);
+}
+
+DDL_API int ddl_gemm_n64(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
+                         int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
+                         float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
+                         int accumulate, hipStream_t st) {
+    return gemm_entry(1, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, bias_bf16, act, aux, out_f32, splits, workspace,
+                      ws_elems, conv, row_remap, res, accumulate, st);
 }

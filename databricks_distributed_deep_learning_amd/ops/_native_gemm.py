@@ -13,6 +13,7 @@ from . import _lib
 from ._lib import I, L, P
 
 _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P],
+               "ddl_gemm_n64": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P],
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -92,6 +93,8 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
             int(row_remap), _lib.p(residual), int(accumulate))
     if kind == "big":
         rc = _lib.fn("ddl_gemm_big2")(*args, _zero_page(C.device).data_ptr(), _lib.stream())
+    elif kind == "narrow":
+        rc = _lib.fn("ddl_gemm_n64")(*args, _lib.stream())
     else:
         rc = _lib.fn("ddl_gemm")(*args, _lib.stream())
     if rc != 0:
@@ -113,6 +116,9 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
         out += [("big", s) for s in sorted({1, max(1, bs // 2), bs})]
     ps = 1 if row_remap else pick_splits(M, N, K)
     out += [("small", s) for s in sorted({1, max(1, ps // 2), ps})]
+    if N <= 192 or N % 128 == 64:     # 128x64 tiles: no half-empty column tile
+        ns = 1 if row_remap else pick_splits(M, 2 * N, K)   # 128x64 tiles = 128x128 tiles on 2N
+        out += [("narrow", s) for s in sorted({1, max(1, ns // 2), ns})]
     return out
 
 
@@ -192,7 +198,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          conv: Optional[Sequence[int]] = None, row_remap: bool = False,
          residual: Optional[torch.Tensor] = None, accumulate: bool = False,
          kernel: Optional[str] = None) -> torch.Tensor:
-    """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256) or "small" (128x128)."""
+    """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128) or
+    "narrow" (128x64)."""
     conv_arr = None
     if conv is not None:
         conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
@@ -202,6 +209,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
             kernel = "small"              # no 256x256 variant for these
         if kernel == "big":
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
+        elif kernel == "narrow":
+            choice = ("narrow", 1 if row_remap else pick_splits(M, 2 * N, K, splits))
         else:
             choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
     elif splits is not None:                       # explicit request: 128x128 kernel with that split

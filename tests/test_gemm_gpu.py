@@ -20,7 +20,7 @@ def _rel_err(a, b):
 SHAPES = [(128, 128, 64), (256, 384, 768), (77, 200, 136), (1000, 2304, 768), (130, 8, 72), (16, 1000, 2048)]
 
 
-@pytest.mark.parametrize("kernel", ["big", "small"])
+@pytest.mark.parametrize("kernel", ["big", "small", "narrow"])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_modes(M, N, K, kernel):
     dev = gpu_device()
@@ -84,7 +84,7 @@ CONVS = [  # N, H, W, C, K, R, stride, pad
 ]
 
 
-@pytest.mark.parametrize("kernel", [None, "big", "small"])
+@pytest.mark.parametrize("kernel", [None, "big", "small", "narrow"])
 @pytest.mark.parametrize("N,H,W,C,K,R,stride,pad", CONVS)
 def test_conv_fwd_bwd(N, H, W, C, K, R, stride, pad, kernel):
     dev = gpu_device()
