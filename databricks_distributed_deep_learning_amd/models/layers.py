@@ -26,8 +26,8 @@ class Conv2d(nn.Module):
         std = math.sqrt(2.0 / (cout * k * k))
         nn.init.normal_(self.weight, 0.0, std)
 
-    def forward(self, x):
-        return ops.conv2d(x, self.weight, self.stride, self.padding)
+    def forward(self, x, grad_residual=None):
+        return ops.conv2d(x, self.weight, self.stride, self.padding, grad_residual=grad_residual)
 
     def extra_repr(self):
         return f"{self.cin}, {self.cout}, k={self.k}, stride={self.stride}, padding={self.padding}"
@@ -49,11 +49,12 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, residual_grad_to=None):
         if self.training:
             self.num_batches_tracked.add_(1)
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var,
-                              self.training, self.momentum, self.eps, self.relu, residual)
+                              self.training, self.momentum, self.eps, self.relu, residual,
+                              residual_grad_to=residual_grad_to)
 
     def _apply(self, fn, recurse=True):
         # keep running stats in fp32 when the module is cast to bf16

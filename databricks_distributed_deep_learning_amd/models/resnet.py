@@ -13,13 +13,22 @@ not installed) around the fused ops:
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type, Union
 
 import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops.bridge import GradBridge
 from .layers import BatchNorm2d, Conv2d, Linear
+
+
+_BRIDGE = os.environ.get("DDL_GRAD_BRIDGE", "1") != "0"
+
+
+def _bridge(x: torch.Tensor, training: bool):
+    return GradBridge() if (_BRIDGE and training and torch.is_grad_enabled() and x.requires_grad) else None
 
 
 class BasicBlock(nn.Module):
@@ -35,7 +44,11 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        if self.downsample is None:
+            br = _bridge(x, self.training)
+            out = self.bn1(self.conv1(x, grad_residual=br))
+            return self.bn2(self.conv2(out), residual=x, residual_grad_to=br)
+        identity = self.downsample(x)
         out = self.bn1(self.conv1(x))
         return self.bn2(self.conv2(out), residual=identity)
 
@@ -55,7 +68,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        if self.downsample is None:
+            # identity block: the residual gradient is added inside conv1's dgrad epilogue
+            br = _bridge(x, self.training)
+            out = self.bn1(self.conv1(x, grad_residual=br))
+            out = self.bn2(self.conv2(out))
+            return self.bn3(self.conv3(out), residual=x, residual_grad_to=br)
+        identity = self.downsample(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), residual=identity)

@@ -39,20 +39,24 @@ def _fwd(x, w, stride, pad, bias=None, act=None, residual=None):
     return y
 
 
-def _dgrad(dy, w, x_shape, stride, pad):
+def _dgrad(dy, w, x_shape, stride, pad, residual=None):
+    """dx (+ ``residual``, added in the GEMM epilogue; stride-1 paths only)."""
     N, H, W_, C = x_shape
     K, R, S, _ = w.shape
     _, P, Q, _ = dy.shape
     if R == 1 and S == 1 and stride == 1 and pad == 0:
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
-        gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K)
+        gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K, residual=residual)
         return dx
     if stride == 1:
         wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()       # [C, R, S, K]
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
         gemm(MODE_CONV, dy, 0, wt, R * S * K, dx, C, N * H * W_, C, R * S * K,
-             conv=_desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_))
+             conv=_desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_),
+             residual=residual)
         return dx
+    if residual is not None:
+        return _dgrad(dy, w, x_shape, stride, pad).add_(residual)
     # stride s: output-parity classes (a, b); taps r = a+pad (mod s)
     classes = []
     empty = False
@@ -95,8 +99,9 @@ def _wgrad(dy, x, w_shape, stride, pad, out=None):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad):
+    def forward(ctx, x, w, stride, pad, bridge=None):
         ctx.w_param = w
+        ctx.bridge = bridge
         x = x.contiguous()
         w = w.contiguous()
         ctx.stride, ctx.pad = stride, pad
@@ -109,7 +114,10 @@ class _Conv(torch.autograd.Function):
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad)
+            res = ctx.bridge.take() if ctx.bridge is not None else None
+            if res is not None:
+                res = res.contiguous().view(x.shape)
+            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad, residual=res)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
             if sink is not None and sink.shape == w.shape:
@@ -117,21 +125,23 @@ class _Conv(torch.autograd.Function):
                 grad_ready(ctx.w_param)
             else:
                 dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def conv2d(x, w, stride, padding):
+def conv2d(x, w, stride, padding, bridge=None):
+    from .bridge import join
     from .conv import conv2d_reference
-    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
-        return conv2d_reference(x, w, stride, padding)
     C = x.shape[-1]
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[0] % 8 or C % 8:
+        # the bridge attaches to the caller's tensor (before any channel padding)
+        x, bridge = join(x, bridge), None
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[0] % 8:
+        return conv2d_reference(x, w, stride, padding)
     if C % 8:
         c8 = (C + 7) // 8 * 8
         x = F.pad(x, (0, c8 - C))
         w = F.pad(w, (0, c8 - C))
-    if w.shape[0] % 8:
-        return conv2d_reference(x, w, stride, padding)
-    return _Conv.apply(x, w, stride, padding)
+    return _Conv.apply(x, w, stride, padding, bridge)
 
 
 def conv2d_bias_act(x, w, b, stride, padding, relu=False, residual=None):

@@ -15,7 +15,8 @@ def _bn_supported(C: int) -> bool:
 
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual, bridge=None):
+        ctx.bridge = bridge
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -62,7 +63,10 @@ class _BatchNormTrain(torch.autograd.Function):
             grad_ready(ctx.params[0])
             grad_ready(ctx.params[1])
             dgamma = dbeta = None
-        return dx, dgamma, dbeta, None, None, None, None, None, dres
+        if dres is not None and ctx.bridge is not None:
+            ctx.bridge.put(dres)            # summed into the consumer's dgrad epilogue
+            dres = None
+        return dx, dgamma, dbeta, None, None, None, None, None, dres, None
 
 
 class _BatchNormEval(torch.autograd.Function):
@@ -81,7 +85,7 @@ class _BatchNormEval(torch.autograd.Function):
         return y
 
 
-def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual):
+def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual, bridge=None):
     from .norm import batch_norm_reference
     C = x.shape[-1]
     if not _bn_supported(C) or x.dtype not in (torch.bfloat16, torch.float32):
@@ -90,7 +94,8 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, e
     if weight is not None and weight.dtype != x.dtype:
         weight, bias = weight.to(x.dtype), bias.to(x.dtype)
     if training:
-        return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual)
+        return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
+                                     bridge)
     if torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)):
         # eval-mode BN with gradients (frozen-statistics fine-tuning): reference path
         return batch_norm_reference(x, weight, bias, running_mean, running_var, False, momentum, eps, relu,

@@ -1,0 +1,54 @@
+"""Residual-gradient bridge: fold the residual branch's gradient into a GEMM epilogue.
+
+In a ResNet identity block the block input ``x`` feeds both ``conv1`` and the
+residual add of the last BatchNorm, so autograd would sum two full-size
+gradients with an extra elementwise kernel (read 2, write 1).  With a bridge the
+last BN's backward *hands* its residual gradient to the bridge instead of
+returning it, and ``conv1``'s backward adds it in the dgrad GEMM epilogue
+(``residual=``) -- the sum costs one extra read inside a kernel that runs anyway.
+
+Ordering is guaranteed by data dependence: ``conv1``'s backward needs the
+gradient of its output, which only exists after the last BN's backward ran.
+A consumer that finds the bridge empty adds nothing (the producer then returned
+the gradient to autograd as usual), so mixing native and reference ops stays
+correct.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+class GradBridge:
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad: Optional[torch.Tensor] = None
+
+    def put(self, g: torch.Tensor) -> None:
+        if self.grad is not None:
+            raise RuntimeError("GradBridge: gradient already pending (bridge reused within one backward?)")
+        self.grad = g
+
+    def take(self) -> Optional[torch.Tensor]:
+        g, self.grad = self.grad, None
+        return g
+
+
+class _BridgeJoin(torch.autograd.Function):
+    """Identity in forward; adds the bridged gradient in backward (reference-op consumers)."""
+
+    @staticmethod
+    def forward(ctx, x, bridge):
+        ctx.bridge = bridge
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        r = ctx.bridge.take()
+        return (g if r is None else g + r.view_as(g)), None
+
+
+def join(x: torch.Tensor, bridge: Optional[GradBridge]) -> torch.Tensor:
+    return x if bridge is None else _BridgeJoin.apply(x, bridge)

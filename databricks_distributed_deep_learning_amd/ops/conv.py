@@ -24,11 +24,15 @@ def conv2d_reference(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding:
     return y.permute(0, 2, 3, 1).contiguous()
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0) -> torch.Tensor:
+def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0,
+           grad_residual=None) -> torch.Tensor:
+    """``grad_residual``: a :class:`ops.bridge.GradBridge` whose pending gradient is
+    added to this conv's input gradient (fused into the dgrad GEMM epilogue)."""
     if _lib.use_native(x):
         from . import _native_conv
-        return _native_conv.conv2d(x, w, stride, padding)
-    return conv2d_reference(x, w, stride, padding)
+        return _native_conv.conv2d(x, w, stride, padding, grad_residual)
+    from .bridge import join
+    return conv2d_reference(join(x, grad_residual), w, stride, padding)
 
 
 def out_hw(h: int, w: int, k: int, stride: int, padding: int):
