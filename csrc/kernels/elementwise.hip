@@ -389,3 +389,36 @@ DDL_API int ddl_embedding_bwd(int dtype, const int64_t* ids, const void* dy, flo
                (cast_f32_k<float><<<grid_for(n), 256, 0, st>>>(acc, (float*)dw, n, accumulate)));
     DDL_RETURN_LAUNCH();
 }
+
+// ------------------------------------------------------------------ conv dgrad weight layout
+// out[c][r'][s'][k] = w[k][rmap[r']][smap[s']][c]  (bf16): the transposed (and for
+// stride-1 dgrad: spatially flipped; for a stride-s parity class: tap-subset)
+// weight the implicit-GEMM dgrad reads as its KC operand.  One launch replaces
+// the index / flip / permute / contiguous chain (4-6 small ATen kernels per conv).
+struct TapMap {
+    int r[8], s[8];
+};
+__global__ __launch_bounds__(256) void conv_w_dgrad_k(const bf16_t* __restrict__ w, bf16_t* __restrict__ out, int K,
+                                                      int R, int S, int C, int Rp, int Sp, TapMap tm) {
+    const long total = (long)C * Rp * Sp * K;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int k = (int)(i % K);
+        long t = i / K;
+        const int sp = (int)(t % Sp);
+        t /= Sp;
+        const int rp = (int)(t % Rp);
+        const int c = (int)(t / Rp);
+        out[i] = w[(((long)k * R + tm.r[rp]) * S + tm.s[sp]) * C + c];
+    }
+}
+
+DDL_API int ddl_conv_w_dgrad(const void* w, void* out, int K, int R, int S, int C, int Rp, int Sp, const int* rmap,
+                             const int* smap, hipStream_t st) {
+    if (Rp > 8 || Sp > 8 || Rp < 1 || Sp < 1) return -1;
+    TapMap tm{};
+    for (int i = 0; i < Rp; ++i) tm.r[i] = rmap[i];
+    for (int i = 0; i < Sp; ++i) tm.s[i] = smap[i];
+    const long total = (long)C * Rp * Sp * K;
+    conv_w_dgrad_k<<<grid_for(total), 256, 0, st>>>((const bf16_t*)w, (bf16_t*)out, K, R, S, C, Rp, Sp, tm);
+    DDL_RETURN_LAUNCH();
+}

@@ -48,10 +48,26 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        self._nbt_pending = 0
+
+    def _flush_nbt(self):
+        if self._nbt_pending:
+            self.num_batches_tracked.add_(self._nbt_pending)
+            self._nbt_pending = 0
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        self._flush_nbt()
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        self._nbt_pending = 0
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     def forward(self, x, residual: Optional[torch.Tensor] = None, residual_grad_to=None):
         if self.training:
-            self.num_batches_tracked.add_(1)
+            # counted on the host (one tiny kernel per BN per step otherwise); folded into
+            # the buffer whenever the state dict is read
+            self._nbt_pending += 1
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var,
                               self.training, self.momentum, self.eps, self.relu, residual,
                               residual_grad_to=residual_grad_to)

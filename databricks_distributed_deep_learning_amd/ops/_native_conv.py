@@ -13,9 +13,12 @@ to 8 channels so every gathered chunk is one 16-byte load.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
+from . import _lib
 from ._lib import grad_ready, grad_sink
 from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm
 
@@ -39,6 +42,19 @@ def _fwd(x, w, stride, pad, bias=None, act=None, residual=None):
     return y
 
 
+def _w_dgrad(w, rs, ss):
+    """[C, len(rs), len(ss), K] = w[:, rs][:, :, ss] transposed, in one native launch."""
+    K, R, S, C = w.shape
+    out = torch.empty(C, len(rs), len(ss), K, dtype=w.dtype, device=w.device)
+    ra = (ctypes.c_int * len(rs))(*rs)
+    sa = (ctypes.c_int * len(ss))(*ss)
+    rc = _lib.fn("ddl_conv_w_dgrad")(w.data_ptr(), out.data_ptr(), K, R, S, C, len(rs), len(ss), ra, sa,
+                                     _lib.stream())
+    if rc != 0:
+        raise RuntimeError(f"ddl_conv_w_dgrad failed: {rc}")
+    return out
+
+
 def _dgrad(dy, w, x_shape, stride, pad, residual=None):
     """dx (+ ``residual``, added in the GEMM epilogue; stride-1 paths only)."""
     N, H, W_, C = x_shape
@@ -49,7 +65,7 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
         gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K, residual=residual)
         return dx
     if stride == 1:
-        wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()       # [C, R, S, K]
+        wt = _w_dgrad(w, list(range(R - 1, -1, -1)), list(range(S - 1, -1, -1)))   # flipped [C, R, S, K]
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
         gemm(MODE_CONV, dy, 0, wt, R * S * K, dx, C, N * H * W_, C, R * S * K,
              conv=_desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_),
@@ -72,7 +88,7 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
             classes.append((a, b, rs, ss, Ho, Wo))
     dx = (torch.zeros if empty else torch.empty)(N, H, W_, C, dtype=dy.dtype, device=dy.device)
     for a, b, rs, ss, Ho, Wo in classes:
-        wc = w[:, rs][:, :, ss].permute(3, 1, 2, 0).contiguous()   # [C, R', S', K]
+        wc = _w_dgrad(w, rs, ss)                                     # [C, R', S', K]
         h_off = (a + pad - rs[0]) // stride
         w_off = (b + pad - ss[0]) // stride
         Rp, Sp = len(rs), len(ss)
