@@ -91,16 +91,21 @@ class NativeComm:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         path = rccl_path().encode()
         uid = ctypes.create_string_buffer(128)
+        payload = None
         if self.rank == 0:
             rc = _fn("ddl_comm_unique_id")(path, uid)
-            if rc != 0:
-                raise CommError(f"ddl_comm_unique_id failed: {_err()}")
-        obj = [uid.raw if self.rank == 0 else None]
+            payload = uid.raw if rc == 0 else f"ddl_comm_unique_id failed: {_err()}"
+        # rank 0 always broadcasts (the id or its error) so no rank is left waiting
+        obj = [payload]
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast_object_list(obj, src=src, group=group)
+        if isinstance(obj[0], str):
+            raise CommError(obj[0])
         self._h = _fn("ddl_comm_create")(path, obj[0], self.world, self.rank, self.device.index)
-        if not self._h:
-            raise CommError(f"ddl_comm_create failed: {_err()}")
+        ok = torch.tensor([1 if self._h else 0], device=self.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if not self._h or int(ok.item()) == 0:
+            raise CommError(f"ddl_comm_create failed on some rank: {_err() if not self._h else 'peer'}")
 
     # ------------------------------------------------------------------
     def _check(self, rc: int, what: str) -> None:

@@ -84,9 +84,17 @@ class DataParallel(nn.Module):
         if not isinstance(comm, str):        # an engine object (all_reduce / wait), e.g. for tests
             self.native = comm
         elif comm == "native" or (comm == "auto" and self.world > 1):
-            from .comm import NativeComm, native_available
+            from .comm import CommError, NativeComm, native_available
             if native_available() and self.arena.flat.is_cuda:
-                self.native = NativeComm(process_group)
+                try:
+                    self.native = NativeComm(process_group)
+                except CommError as e:
+                    if comm == "native":
+                        raise
+                    # every rank reaches the same outcome (same library, same RCCL), so
+                    # falling back keeps the collective sequence identical across ranks
+                    import warnings
+                    warnings.warn(f"native RCCL engine unavailable ({e}); using torch.distributed")
             elif comm == "native":
                 raise RuntimeError("comm='native' needs CUDA tensors, the native library and the nccl backend")
         self.comm = "native" if self.native is not None else "torch"
