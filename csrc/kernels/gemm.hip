@@ -58,6 +58,8 @@ struct Params {
     int splits, kt_per_split;
     long split_stride;
     int row_remap;    // conv output rows -> strided output pixels
+    int trans_out;    // store C^T: element (m, n) at C[n * ldc + m] (narrow-Cout weight gradients)
+    long ldw;         // split-K slab row stride
     const bf16_t* res;  // optional residual added before the activation (same layout as C)
     int accumulate;     // C += result (gradient accumulation straight into the parameter-grad arena)
     ConvDesc cd;
@@ -343,11 +345,27 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
             float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
             const bool full = n + 3 < p.N;
             if (p.out_f32 && p.splits > 1) {
-                float* c = (float*)p.C + split * p.split_stride + orow * p.ldc + n;
+                float* c = (float*)p.C + split * p.split_stride + orow * p.ldw + n;
                 if (full) store4(c, v);
                 else {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) if (n + r < p.N) c[r] = v[r];
+                }
+                continue;
+            }
+            if (p.trans_out) {   // plain (or accumulating) transposed store; no other epilogue ops
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (n + r >= p.N) continue;
+                    const long o = (long)(n + r) * p.ldc + m;
+                    float t = v[r];
+                    if (p.out_f32) {
+                        if (p.accumulate) t += ((float*)p.C)[o];
+                        ((float*)p.C)[o] = t;
+                    } else {
+                        if (p.accumulate) t += bf2f(((bf16_t*)p.C)[o]);
+                        ((bf16_t*)p.C)[o] = f2bf(t);
+                    }
                 }
                 continue;
             }
@@ -431,14 +449,23 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
 
 // Sum split-K fp32 partials, apply the epilogue, write bf16/fp32.
 __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ part, int splits, long split_stride,
-                                                     int M, int N, long ldc, void* out, int out_f32,
+                                                     long ldw, int M, int N, long ldc, void* out, int out_f32,
                                                      const void* bias, int bias_bf16, int act, void* aux,
-                                                     const bf16_t* __restrict__ res, int accumulate) {
+                                                     const bf16_t* __restrict__ res, int accumulate, int trans) {
     const long total = (long)M * N;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int m = (int)(i / N), n = (int)(i - (long)m * N);
+        // transposed output: walk the output contiguously (n major) so the stores coalesce
+        const int m = trans ? (int)(i % M) : (int)(i / N);
+        const int n = trans ? (int)(i / M) : (int)(i - (long)m * N);
         float v = 0.f;
-        for (int s = 0; s < splits; ++s) v += part[s * split_stride + (long)m * ldc + n];
+        for (int s = 0; s < splits; ++s) v += part[s * split_stride + (long)m * ldw + n];
+        if (trans) {
+            const long o = (long)n * ldc + m;
+            if (accumulate) v += out_f32 ? ((float*)out)[o] : bf2f(((bf16_t*)out)[o]);
+            if (out_f32) ((float*)out)[o] = v;
+            else ((bf16_t*)out)[o] = f2bf(v);
+            continue;
+        }
         if (bias) v += bias_bf16 ? bf2f(((const bf16_t*)bias)[n]) : ((const float*)bias)[n];
         if (res) v += bf2f(res[(long)m * ldc + n]);
         if (act == ACT_DGELU) v *= gelu_erf_grad(bf2f(((const bf16_t*)aux)[(long)m * ldc + n]));
@@ -465,8 +492,9 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
     void* final_out = p.C;
     const int final_f32 = p.out_f32;
     int acc_final = 0;
+    p.ldw = p.trans_out ? p.N : p.ldc;
     if (splits > 1) {
-        p.split_stride = (long)p.M * p.ldc;
+        p.split_stride = (long)p.M * p.ldw;
         if (!workspace || ws_elems < p.split_stride * splits) return -2;
         if (p.row_remap) return -3;
         p.C = workspace;
@@ -479,8 +507,9 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
     if (splits > 1) {
         const long total = (long)p.M * p.N;
         const int g = (int)std::min<long>(8192, (total + 255) / 256);
-        gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.M, p.N, p.ldc, final_out, final_f32,
-                                          p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final);
+        gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out,
+                                          final_f32, p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final,
+                                          p.trans_out);
     }
     return (int)hipGetLastError();
 }
@@ -504,6 +533,9 @@ void fill_conv(ConvDesc& cd, const int* d) {
 //       2 = A KO, B KO   (dW = dy^T x, Linear wgrad)
 //       3 = A CONV, B KC (conv fwd / dgrad by implicit GEMM; conv desc required)
 //       4 = A KO, B CONVW (conv wgrad; conv desc required)
+//       5 = A CONVW, B KO (conv wgrad computed as dW^T: the im2col side on M, so a
+//           64-channel output is the N side and fits the 128x64 tile)
+//       | 16 = store C^T (element (m, n) at C[n * ldc + m]); no bias/act/residual
 // act: 0 none, 1 gelu (aux <- pre-activation if aux), 2 relu, 3 tanh, 4 dgelu (v *= gelu'(aux))
 static int gemm_entry(int narrow, int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                       int M, int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
@@ -514,6 +546,9 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = aux; p.out_f32 = out_f32;
     p.row_remap = row_remap;
+    p.trans_out = (mode & 16) ? 1 : 0;
+    mode &= 15;
+    if (p.trans_out && (bias || act || res || row_remap)) return -5;
     p.res = (const bf16_t*)res;
     p.accumulate = accumulate;
     if (conv) fill_conv(p.cd, conv);
@@ -525,6 +560,7 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
             case 2: return launch<KO, KO, 64>(p, workspace, ws_elems, splits, st);
             case 3: return launch<CONV, KC, 64>(p, workspace, ws_elems, splits, st);
             case 4: return launch<KO, CONVW, 64>(p, workspace, ws_elems, splits, st);
+            case 5: return launch<CONVW, KO, 64>(p, workspace, ws_elems, splits, st);
             default: return -1;
         }
     }
@@ -534,6 +570,7 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
         case 2: return launch<KO, KO>(p, workspace, ws_elems, splits, st);
         case 3: return launch<CONV, KC>(p, workspace, ws_elems, splits, st);
         case 4: return launch<KO, CONVW>(p, workspace, ws_elems, splits, st);
+        case 5: return launch<CONVW, KO>(p, workspace, ws_elems, splits, st);
         default: return -1;
     }
 }

@@ -17,6 +17,8 @@ _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
+MODE_CONVW_A = 5      # conv wgrad with the im2col operand on the M side (computes dW^T)
+TRANS_OUT = 16        # flag: the kernel stores C^T
 ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4}
 BM = BN = 128
 BK = 64
@@ -85,9 +87,16 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
 
 def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr,
             row_remap, residual, accumulate) -> None:
+    if kind.startswith("t"):
+        # weight-gradient GEMMs computed transposed (operands swapped, C^T stored): a
+        # 64-wide output-channel side lands on the tile's N extent (128x64 tiles)
+        kind = kind[1:]
+        mode = (MODE_CONVW_A if mode == MODE_CONVW else MODE_TN) | TRANS_OUT
+        A, lda, B, ldb, M, N = B, ldb, A, lda, N, M
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
     out_f32 = 1 if C.dtype == torch.float32 else 0
-    ws = torch.empty(s * M * ldc, dtype=torch.float32, device=C.device) if s > 1 else None
+    ws = torch.empty(s * M * (N if mode & TRANS_OUT else ldc), dtype=torch.float32, device=C.device) \
+        if s > 1 else None
     args = (mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, _lib.p(bias), bias_bf16,
             ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws), 0 if ws is None else ws.numel(), conv_arr,
             int(row_remap), _lib.p(residual), int(accumulate))
@@ -106,7 +115,7 @@ def _big_allowed(mode: int, K: int, lda: int = 8, ldb: int = 8) -> bool:
     return not _force_small and mode != MODE_CONVW and K % 8 == 0 and K >= 64 and lda % 8 == 0 and ldb % 8 == 0
 
 
-def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):
+def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int, plain: bool = False):
     """(kernel, splits) variants worth timing for one GEMM shape: each kernel at
     no split, its heuristic split and half of it (split-K trades parallelism
     against fp32 partial-slab traffic, which the heuristic cannot price)."""
@@ -119,6 +128,9 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
     if N <= 192 or N % 128 == 64:     # 128x64 tiles: no half-empty column tile
         ns = 1 if row_remap else pick_splits(M, 2 * N, K)   # 128x64 tiles = 128x128 tiles on 2N
         out += [("narrow", s) for s in sorted({1, max(1, ns // 2), ns})]
+    if mode in (MODE_TN, MODE_CONVW) and plain and (M <= 192 or M % 128 == 64):
+        ts = pick_splits(N, 2 * M, K)     # transposed: N' = M (output channels) on 64-wide tiles
+        out += [("tnarrow", s) for s in sorted({1, max(1, ts // 2), ts})]
     return out
 
 
@@ -168,7 +180,8 @@ def tuned_choices() -> dict:
 
 
 def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap, residual):
-    cands = _candidates(mode, M, N, K, row_remap, lda, ldb)
+    plain = bias is None and act is None and residual is None and aux is None and not row_remap
+    cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain)
     if len(cands) == 1:
         return cands[0]
     Cs = torch.empty_like(C)
@@ -211,6 +224,11 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
         elif kernel == "narrow":
             choice = ("narrow", 1 if row_remap else pick_splits(M, 2 * N, K, splits))
+        elif kernel == "tnarrow" and mode in (MODE_TN, MODE_CONVW) and bias is None and act is None \
+                and residual is None and not row_remap:
+            choice = ("tnarrow", pick_splits(N, 2 * M, K, splits))
+        elif kernel == "tnarrow":
+            choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
         else:
             choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
     elif splits is not None:                       # explicit request: 128x128 kernel with that split

@@ -140,3 +140,39 @@ def test_big_gemm_modes(mode, M, N, K):
         base = dw.float().clone()
         NG.gemm(2, dy, N, a, K, dw, K, N, K, M, accumulate=True, kernel="big")
         assert _rel_err(dw, base + dy.float().t() @ a.float()) < 1e-2
+
+
+@pytest.mark.parametrize("splits", [None, 1, 3])
+@pytest.mark.parametrize("M,N,K", [(64, 576, 3000), (64, 256, 4096), (128, 1152, 777 * 8), (40, 72, 520)])
+def test_transposed_weight_gradient(M, N, K, splits):
+    """dW computed as (x^T dy)^T with the 64-channel side on the 128x64 tile's N extent
+    (kernel "tnarrow": operands swapped, C^T stored, accumulate into an existing grad)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    torch.manual_seed(7)
+    dy = torch.randn(K, M, device=dev).to(torch.bfloat16)     # [pixels, Cout]
+    x = torch.randn(K, N, device=dev).to(torch.bfloat16)      # [pixels, Cin]
+    base = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    dw = base.clone()
+    NG.gemm(NG.MODE_TN, dy, M, x, N, dw, N, M, N, K, accumulate=True, kernel="tnarrow", splits=splits)
+    assert _rel_err(dw, base.float() + dy.float().t() @ x.float()) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C,K,R,stride,pad", [(4, 20, 20, 64, 64, 3, 1, 1), (2, 30, 30, 8, 64, 7, 2, 3),
+                                                    (4, 14, 14, 128, 64, 3, 2, 1)])
+def test_conv_wgrad_transposed(N, H, W, C, K, R, stride, pad):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    from databricks_distributed_deep_learning_amd.ops._native_gemm import force_kernel
+    from databricks_distributed_deep_learning_amd.ops.conv import conv2d_reference
+    torch.manual_seed(8)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(K, R, R, C, device=dev).to(torch.bfloat16)
+    P = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, P, P, K, device=dev).to(torch.bfloat16)
+    xr = x.float().requires_grad_(False)
+    wr = w.float().requires_grad_(True)
+    conv2d_reference(xr, wr, stride, pad).backward(dy.float())
+    with force_kernel("tnarrow"):
+        dw = NC._wgrad(dy, x, w.shape, stride, pad)
+    assert _rel_err(dw, wr.grad) < 1e-2
