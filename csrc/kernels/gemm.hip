@@ -59,6 +59,8 @@ struct Params {
     long split_stride;
     int row_remap;    // conv output rows -> strided output pixels
     int trans_out;    // store C^T: element (m, n) at C[n * ldc + m] (narrow-Cout weight gradients)
+    float* colstats;  // BN statistics of the (bf16-rounded) output: per 128-row tile,
+                      // [tile_m][0..N) column sums and [tile_m][N..2N) sums of squares
     long ldw;         // split-K slab row stride
     const bf16_t* res;  // optional residual added before the activation (same layout as C)
     int accumulate;     // C += result (gradient accumulation straight into the parameter-grad arena)
@@ -333,6 +335,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
 
     // ---- epilogue: lane holds C[m][n..n+3]
     const int g = lane >> 4;
+    float st_s[NJ][4], st_q[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -442,6 +449,46 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) if (n + r < p.N) c[r] = f2bf(v[r]);
                 }
+                if (p.colstats) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float q = n + r < p.N ? bf2f(f2bf(v[r])) : 0.f;   // what BN will read
+                        st_s[j][r] += q;
+                        st_q[j][r] += q * q;
+                    }
+                }
+            }
+        }
+    }
+    if (p.colstats) {
+        // rows of this wave: reduce over the 16 lanes that share a column group,
+        // then over the two M-waves through LDS (the tile buffers are free here)
+        float* red = reinterpret_cast<float*>(smem);     // [2][BNT] sums, squares
+        __syncthreads();
+        for (int t = threadIdx.x; t < 2 * BNT; t += NT) red[t] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float a = st_s[j][r], b = st_q[j][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    a += __shfl_xor(a, o);
+                    b += __shfl_xor(b, o);
+                }
+                if ((lane & 15) == 0) {
+                    const int col = wn * WN + j * 16 + 4 * g + r;
+                    atomicAdd(&red[col], a);
+                    atomicAdd(&red[BNT + col], b);
+                }
+            }
+        __syncthreads();
+        for (int t = threadIdx.x; t < BNT; t += NT) {
+            const int n = n0 + t;
+            if (n < p.N) {
+                p.colstats[(long)tm * 2 * p.N + n] = red[t];
+                p.colstats[(long)tm * 2 * p.N + p.N + n] = red[BNT + t];
             }
         }
     }
@@ -540,7 +587,7 @@ void fill_conv(ConvDesc& cd, const int* d) {
 static int gemm_entry(int narrow, int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
                       int M, int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
                       int splits, float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
-                      int accumulate, hipStream_t st) {
+                      int accumulate, float* colstats, hipStream_t st) {
     Params p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
@@ -549,6 +596,8 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
     p.trans_out = (mode & 16) ? 1 : 0;
     mode &= 15;
     if (p.trans_out && (bias || act || res || row_remap)) return -5;
+    p.colstats = colstats;
+    if (colstats && (p.trans_out || out_f32 || accumulate || (splits > 1) || bias || act || res)) return -6;
     p.res = (const bf16_t*)res;
     p.accumulate = accumulate;
     if (conv) fill_conv(p.cd, conv);
@@ -577,18 +626,19 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
 
 
 
+// colstats (nullable): BN statistics partials of the output, one row pair per 128-row tile
 DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                      int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
                      float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
-                     int accumulate, hipStream_t st) {
+                     int accumulate, float* colstats, hipStream_t st) {
     return gemm_entry(0, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, bias_bf16, act, aux, out_f32, splits, workspace,
-                      ws_elems, conv, row_remap, res, accumulate, st);
+                      ws_elems, conv, row_remap, res, accumulate, colstats, st);
 }
 
 DDL_API int ddl_gemm_n64(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                          int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
                          float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
-                         int accumulate, hipStream_t st) {
+                         int accumulate, float* colstats, hipStream_t st) {
     return gemm_entry(1, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, bias_bf16, act, aux, out_f32, splits, workspace,
-                      ws_elems, conv, row_remap, res, accumulate, st);
+                      ws_elems, conv, row_remap, res, accumulate, colstats, st);
 }

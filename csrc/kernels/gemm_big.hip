@@ -78,6 +78,7 @@ struct BigParams {
     long split_stride;
     int row_remap;
     const bf16_t* zero;       // >= 16 zero bytes
+    float* colstats;          // BN statistics partials of the bf16 output: [tile_m][2][N]
     ConvDesc cd;
     int tiles_m, tiles_n;
 };
@@ -531,6 +532,12 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
                 *reinterpret_cast<f32x4*>(ep + (wm * 64 + i * 16 + (lane & 15)) * EP_LD + wn * 32 + j * 16 + 4 * g) =
                     a[i][j];
     };
+    // BN statistics: this thread always owns the same 8 columns (idx & 15) of a quarter
+    float st_s[2][8], st_q[2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) st_s[a][e] = st_q[a][e] = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         __syncthreads();
@@ -548,6 +555,14 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
             const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + r * EP_LD + c + 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[4 + e] = hi[e]; }
+            if (p.colstats) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float t = n + e < p.N ? bf2f(f2bf(v[e])) : 0.f;   // what BN will read
+                    st_s[q & 1][e] += t;
+                    st_q[q & 1][e] += t * t;
+                }
+            }
             if (partial) {
                 float* dst = (float*)p.C + split * p.split_stride + (long)m * p.ldc + n;
                 store4g(dst, n + 3 < p.N, p.N - n, v);
@@ -557,6 +572,39 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
             const long orow = out_row(p, m);
             epilogue4(p, orow, n, v);
             if (n + 4 < p.N) epilogue4(p, orow, n + 4, v + 4);
+        }
+    }
+    if (p.colstats) {
+        // lanes l, l^16, l^32, l^48 own the same columns; then 8 waves through LDS
+        float* red = reinterpret_cast<float*>(smem + 96 * 1024);   // [8 waves][256 cols][2]
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float x = st_s[a][e], y = st_q[a][e];
+                x += __shfl_xor(x, 16);
+                y += __shfl_xor(y, 16);
+                x += __shfl_xor(x, 32);
+                y += __shfl_xor(y, 32);
+                if (lane < 16) {
+                    const int col = a * 128 + lane * 8 + e;
+                    red[(w * 256 + col) * 2] = x;
+                    red[(w * 256 + col) * 2 + 1] = y;
+                }
+            }
+        __syncthreads();
+        if (threadIdx.x < 256) {
+            const int col = threadIdx.x, n = n0 + col;
+            float x = 0.f, y = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < 8; ++ww) {
+                x += red[(ww * 256 + col) * 2];
+                y += red[(ww * 256 + col) * 2 + 1];
+            }
+            if (n < p.N) {
+                p.colstats[(long)tm * 2 * p.N + n] = x;
+                p.colstats[(long)tm * 2 * p.N + p.N + n] = y;
+            }
         }
     }
 }
@@ -630,7 +678,7 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
 DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
                           float* workspace, long ws_elems, const int* conv, int row_remap, const void* res,
-                          int accumulate, const void* zero, hipStream_t st) {
+                          int accumulate, const void* zero, float* colstats, hipStream_t st) {
     if (M <= 0 || N <= 0) return 0;
     if (K % 8 || !zero) return -1;
     BigParams p{};
@@ -639,6 +687,8 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
     p.bias = bias; p.bias_bf16 = bias_bf16; p.act = act; p.aux = (bf16_t*)aux;
     p.res = (const bf16_t*)res; p.accumulate = accumulate; p.out_f32 = out_f32;
     p.row_remap = row_remap; p.zero = (const bf16_t*)zero;
+    p.colstats = colstats;
+    if (colstats && (out_f32 || accumulate || splits > 1 || bias || act || res)) return -6;
     if (conv) fill_conv(p.cd, conv);
     switch (mode) {
         case 0: return launch_big<KC, KC>(p, workspace, ws_elems, splits, st);

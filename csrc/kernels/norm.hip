@@ -383,6 +383,22 @@ DDL_API int ddl_bn_fwd_train(int dtype, const void* x, long M, int C, const void
     DDL_RETURN_LAUNCH();
 }
 
+// Training-mode BN statistics from partial sums a GEMM epilogue already produced
+// (``part`` = [nblk][sum(C) | sumsq(C)], see gemm.hip / gemm_big.hip colstats):
+// the statistics read pass over the conv output disappears.
+DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, long M, int C, const void* gamma,
+                                     const void* beta, float* running_mean, float* running_var, float momentum,
+                                     float eps, float* save_mean, float* save_invstd, float* scale, float* shift,
+                                     hipStream_t st) {
+    if (dtype == 1)
+        bn_stats_finalize_k<bf16_t><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
+            (const bf16_t*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+    else
+        bn_stats_finalize_k<float><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, (const float*)gamma,
+            (const float*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+    DDL_RETURN_LAUNCH();
+}
+
 DDL_API int ddl_bn_eval_coeffs(int dtype, int C, const void* gamma, const void* beta, const float* rm,
                                const float* rv, float eps, float* scale, float* shift, hipStream_t st) {
     if (dtype == 1)

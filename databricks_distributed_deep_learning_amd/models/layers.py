@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops.bridge import BNStats
 
 
 class Conv2d(nn.Module):
@@ -26,8 +27,8 @@ class Conv2d(nn.Module):
         std = math.sqrt(2.0 / (cout * k * k))
         nn.init.normal_(self.weight, 0.0, std)
 
-    def forward(self, x, grad_residual=None):
-        return ops.conv2d(x, self.weight, self.stride, self.padding, grad_residual=grad_residual)
+    def forward(self, x, grad_residual=None, bn_stats=None):
+        return ops.conv2d(x, self.weight, self.stride, self.padding, grad_residual=grad_residual, bn_stats=bn_stats)
 
     def extra_repr(self):
         return f"{self.cin}, {self.cout}, k={self.k}, stride={self.stride}, padding={self.padding}"
@@ -63,14 +64,14 @@ class BatchNorm2d(nn.Module):
         self._nbt_pending = 0
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None, residual_grad_to=None):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, residual_grad_to=None, stats=None):
         if self.training:
             # counted on the host (one tiny kernel per BN per step otherwise); folded into
             # the buffer whenever the state dict is read
             self._nbt_pending += 1
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var,
                               self.training, self.momentum, self.eps, self.relu, residual,
-                              residual_grad_to=residual_grad_to)
+                              residual_grad_to=residual_grad_to, stats=stats)
 
     def _apply(self, fn, recurse=True):
         # keep running stats in fp32 when the module is cast to bf16
@@ -105,6 +106,14 @@ class Linear(nn.Module):
 
     def extra_repr(self):
         return f"{self.fin}, {self.fout}, bias={self.bias is not None}, act={self.act}"
+
+
+def conv_bn(conv: "Conv2d", bn: "BatchNorm2d", x, residual=None, grad_residual=None, residual_grad_to=None):
+    """conv -> BatchNorm(+ReLU)(+residual) with the BN statistics produced by the conv's
+    GEMM epilogue in training mode (no separate statistics pass over the conv output)."""
+    st = BNStats() if bn.training else None
+    y = conv(x, grad_residual=grad_residual, bn_stats=st)
+    return bn(y, residual=residual, residual_grad_to=residual_grad_to, stats=st)
 
 
 class LayerNorm(nn.Module):

@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops.bridge import GradBridge
-from .layers import BatchNorm2d, Conv2d, Linear
+from .layers import BatchNorm2d, Conv2d, Linear, conv_bn
 
 
 _BRIDGE = os.environ.get("DDL_GRAD_BRIDGE", "1") != "0"
@@ -46,11 +46,11 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         if self.downsample is None:
             br = _bridge(x, self.training)
-            out = self.bn1(self.conv1(x, grad_residual=br))
-            return self.bn2(self.conv2(out), residual=x, residual_grad_to=br)
+            out = conv_bn(self.conv1, self.bn1, x, grad_residual=br)
+            return conv_bn(self.conv2, self.bn2, out, residual=x, residual_grad_to=br)
         identity = self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), residual=identity)
+        out = conv_bn(self.conv1, self.bn1, x)
+        return conv_bn(self.conv2, self.bn2, out, residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -68,16 +68,17 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        # every conv -> BN pair takes its BN statistics from the conv's GEMM epilogue
         if self.downsample is None:
             # identity block: the residual gradient is added inside conv1's dgrad epilogue
             br = _bridge(x, self.training)
-            out = self.bn1(self.conv1(x, grad_residual=br))
-            out = self.bn2(self.conv2(out))
-            return self.bn3(self.conv3(out), residual=x, residual_grad_to=br)
+            out = conv_bn(self.conv1, self.bn1, x, grad_residual=br)
+            out = conv_bn(self.conv2, self.bn2, out)
+            return conv_bn(self.conv3, self.bn3, out, residual=x, residual_grad_to=br)
         identity = self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=identity)
+        out = conv_bn(self.conv1, self.bn1, x)
+        out = conv_bn(self.conv2, self.bn2, out)
+        return conv_bn(self.conv3, self.bn3, out, residual=identity)
 
 
 class Downsample(nn.Module):
@@ -89,7 +90,7 @@ class Downsample(nn.Module):
         self.add_module("1", BatchNorm2d(cout, relu=False))
 
     def forward(self, x):
-        return self._modules["1"](self._modules["0"](x))
+        return conv_bn(self._modules["0"], self._modules["1"], x)
 
 
 class ResNet(nn.Module):
@@ -119,7 +120,7 @@ class ResNet(nn.Module):
     def features(self, x):
         if not self.channels_last_input:
             x = x.permute(0, 2, 3, 1).contiguous()
-        x = self.bn1(self.conv1(x))
+        x = conv_bn(self.conv1, self.bn1, x)
         x = ops.max_pool2d(x, 3, 2, 1)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return ops.global_avg_pool(x)

@@ -14,31 +14,45 @@ to 8 channels so every gathered chunk is one 16-byte load.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _lib
 from ._lib import grad_ready, grad_sink
-from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm
+from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm, stats_rows_max
 
 
 def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep=1, oa=0, ob=0):
     return [N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep, oa, ob]
 
 
-def _fwd(x, w, stride, pad, bias=None, act=None, residual=None):
+STATS_MIN_K = int(os.environ.get("DDL_BN_STATS_MIN_K", "2048"))
+
+
+def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
+    """Implicit-GEMM conv forward; ``stats`` (ops.bridge.BNStats) also collects the
+    BatchNorm statistics partials of the output in the GEMM epilogue."""
     N, H, W_, C = x.shape
     K, R, S, _ = w.shape
     P = (H + 2 * pad - R) // stride + 1
     Q = (W_ + 2 * pad - S) // stride + 1
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
     M = N * P * Q
+    part = None
+    # the statistics epilogue costs a cross-lane reduction per tile: it beats the
+    # separate read pass over y only when the tile's K loop is long (measured:
+    # scripts/debug/stats_overhead.py; +40 % on K=64 convs, break-even near K=1152)
+    if stats is not None and bias is None and act is None and residual is None and R * S * C >= STATS_MIN_K:
+        part = torch.empty(stats_rows_max(M) * 2 * K, dtype=torch.float32, device=x.device)
     if R == 1 and S == 1 and stride == 1 and pad == 0:
-        gemm(MODE_NT, x, C, w, C, y, K, M, K, C, bias=bias, act=act, residual=residual)
+        r = gemm(MODE_NT, x, C, w, C, y, K, M, K, C, bias=bias, act=act, residual=residual, colstats=part)
     else:
-        gemm(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C, bias=bias, act=act, residual=residual,
-             conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q))
+        r = gemm(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C, bias=bias, act=act, residual=residual,
+                 conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q), colstats=part)
+    if part is not None:
+        stats.set(y, part, r)
     return y
 
 
@@ -115,14 +129,14 @@ def _wgrad(dy, x, w_shape, stride, pad, out=None):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, bridge=None):
+    def forward(ctx, x, w, stride, pad, bridge=None, stats=None):
         ctx.w_param = w
         ctx.bridge = bridge
         x = x.contiguous()
         w = w.contiguous()
         ctx.stride, ctx.pad = stride, pad
         ctx.save_for_backward(x, w)
-        return _fwd(x, w, stride, pad)
+        return _fwd(x, w, stride, pad, stats=stats)
 
     @staticmethod
     def backward(ctx, dy):
@@ -141,10 +155,10 @@ class _Conv(torch.autograd.Function):
                 grad_ready(ctx.w_param)
             else:
                 dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv2d(x, w, stride, padding, bridge=None):
+def conv2d(x, w, stride, padding, bridge=None, stats=None):
     from .bridge import join
     from .conv import conv2d_reference
     C = x.shape[-1]
@@ -157,7 +171,7 @@ def conv2d(x, w, stride, padding, bridge=None):
         c8 = (C + 7) // 8 * 8
         x = F.pad(x, (0, c8 - C))
         w = F.pad(w, (0, c8 - C))
-    return _Conv.apply(x, w, stride, padding, bridge)
+    return _Conv.apply(x, w, stride, padding, bridge, stats)
 
 
 def conv2d_bias_act(x, w, b, stride, padding, relu=False, residual=None):

@@ -15,18 +15,25 @@ def _bn_supported(C: int) -> bool:
 
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual, bridge=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual, bridge=None,
+                pre=None):
         ctx.bridge = bridge
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
         dt = dcode(x)
-        nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
         f32 = dict(dtype=torch.float32, device=x.device)
-        part = torch.empty(nblk * 2 * C, **f32)
         stats = torch.empty(4, C, **f32)           # mean, invstd, scale, shift
-        call("ddl_bn_fwd_train", dt, p(x), M, C, p(weight), p(bias), p(running_mean), p(running_var),
-             float(momentum), float(eps), p(part), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
+        given = pre.take_for(x) if pre is not None else None
+        if given is not None:                      # partials from the producing GEMM's epilogue
+            part, nblk = given
+            call("ddl_bn_fwd_from_partials", dt, p(part), nblk, M, C, p(weight), p(bias), p(running_mean),
+                 p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
+        else:
+            nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
+            part = torch.empty(nblk * 2 * C, **f32)
+            call("ddl_bn_fwd_train", dt, p(x), M, C, p(weight), p(bias), p(running_mean), p(running_var),
+                 float(momentum), float(eps), p(part), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
         res = residual.contiguous() if residual is not None else None
         y = torch.empty_like(x)
         # ReLU: 1 bit per element for the backward instead of re-reading y
@@ -66,7 +73,7 @@ class _BatchNormTrain(torch.autograd.Function):
         if dres is not None and ctx.bridge is not None:
             ctx.bridge.put(dres)            # summed into the consumer's dgrad epilogue
             dres = None
-        return dx, dgamma, dbeta, None, None, None, None, None, dres, None
+        return dx, dgamma, dbeta, None, None, None, None, None, dres, None, None
 
 
 class _BatchNormEval(torch.autograd.Function):
@@ -85,7 +92,8 @@ class _BatchNormEval(torch.autograd.Function):
         return y
 
 
-def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual, bridge=None):
+def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual, bridge=None,
+               pre=None):
     from .norm import batch_norm_reference
     C = x.shape[-1]
     if not _bn_supported(C) or x.dtype not in (torch.bfloat16, torch.float32):
@@ -95,7 +103,7 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, e
         weight, bias = weight.to(x.dtype), bias.to(x.dtype)
     if training:
         return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
-                                     bridge)
+                                     bridge, pre)
     if torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)):
         # eval-mode BN with gradients (frozen-statistics fine-tuning): reference path
         return batch_norm_reference(x, weight, bias, running_mean, running_var, False, momentum, eps, relu,

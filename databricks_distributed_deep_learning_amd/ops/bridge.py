@@ -52,3 +52,28 @@ class _BridgeJoin(torch.autograd.Function):
 
 def join(x: torch.Tensor, bridge: Optional[GradBridge]) -> torch.Tensor:
     return x if bridge is None else _BridgeJoin.apply(x, bridge)
+
+
+class BNStats:
+    """Carries BatchNorm statistics partials from a conv GEMM epilogue to the BN that
+    consumes the conv output (forward-time side channel, see ``gemm(colstats=...)``).
+
+    The BN uses them only if they describe exactly the tensor it received (same
+    storage pointer and size); otherwise it computes its own statistics."""
+    __slots__ = ("ptr", "numel", "part", "nblk")
+
+    def __init__(self):
+        self.ptr = None
+        self.numel = 0
+        self.part = None
+        self.nblk = 0
+
+    def set(self, y: torch.Tensor, part: torch.Tensor, nblk: int) -> None:
+        self.ptr, self.numel, self.part, self.nblk = y.data_ptr(), y.numel(), part, nblk
+
+    def take_for(self, x: torch.Tensor):
+        if self.part is None or self.ptr != x.data_ptr() or self.numel != x.numel():
+            return None
+        part, nblk = self.part, self.nblk
+        self.part = None
+        return part, nblk

@@ -25,12 +25,14 @@ def conv2d_reference(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding:
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0,
-           grad_residual=None) -> torch.Tensor:
+           grad_residual=None, bn_stats=None) -> torch.Tensor:
     """``grad_residual``: a :class:`ops.bridge.GradBridge` whose pending gradient is
-    added to this conv's input gradient (fused into the dgrad GEMM epilogue)."""
+    added to this conv's input gradient (fused into the dgrad GEMM epilogue).
+    ``bn_stats``: a :class:`ops.bridge.BNStats` that receives BatchNorm statistics
+    partials of the output from the GEMM epilogue (for the BN that follows)."""
     if _lib.use_native(x):
         from . import _native_conv
-        return _native_conv.conv2d(x, w, stride, padding, grad_residual)
+        return _native_conv.conv2d(x, w, stride, padding, grad_residual, bn_stats)
     from .bridge import join
     return conv2d_reference(join(x, grad_residual), w, stride, padding)
 

@@ -36,13 +36,14 @@ def batch_norm_reference(x, weight, bias, running_mean, running_var, training: b
 
 def batch_norm(x, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
                eps: float = 1e-5, relu: bool = False, residual: Optional[torch.Tensor] = None,
-               residual_grad_to=None):
+               residual_grad_to=None, stats=None):
     """``residual_grad_to``: a :class:`ops.bridge.GradBridge` that receives the
-    residual's gradient instead of autograd (see ``ops/bridge.py``)."""
+    residual's gradient instead of autograd (see ``ops/bridge.py``).  ``stats``: the
+    :class:`ops.bridge.BNStats` the producing conv filled (skips the statistics pass)."""
     if _lib.use_native(x):
         from . import _native_norm
         return _native_norm.batch_norm(x, weight, bias, running_mean, running_var, training,
-                                       momentum, eps, relu, residual, residual_grad_to)
+                                       momentum, eps, relu, residual, residual_grad_to, stats)
     return batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps,
                                 relu, residual)
 
