@@ -1,5 +1,7 @@
-// Stand-alone A/B timing of GEMM kernel variants (no torch): hipEvent timing of
-// ddl_gemm_big2 (NT) against an alternative object linked in as ddl_gemm_big.
+// Stand-alone A/B timing of GEMM kernel variants (no torch): hipEvent timing of two
+// builds of csrc/kernels/gemm_big.hip linked side by side (the second compiled with
+// -Dddl_gemm_big2=ddl_gemm_big3 and different -D switches), plus an older object as
+// ddl_gemm_big.  Build: see profiles/README.md (gemm_ab_*.log).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -9,11 +11,11 @@
 extern "C" int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M,
                              int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
                              int splits, void* ws, long ws_elems, const int* conv, int row_remap, const void* res,
-                             int accumulate, const void* zero, hipStream_t st);
+                             int accumulate, const void* zero, float* colstats, hipStream_t st);
 extern "C" int ddl_gemm_big3(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M,
                              int N, int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32,
                              int splits, void* ws, long ws_elems, const int* conv, int row_remap, const void* res,
-                             int accumulate, const void* zero, hipStream_t st);
+                             int accumulate, const void* zero, float* colstats, hipStream_t st);
 extern "C" int ddl_gemm_big(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                             const void* bias, int bias_bf16, int act, void* aux, int accumulate, hipStream_t st);
 
@@ -62,7 +64,7 @@ int main() {
             auto run = [&] {
                 auto f = v == 1 ? ddl_gemm_big2 : ddl_gemm_big3;
                 f(c.mode, A, lda, B, ldb, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, c.splits, ws, 8L * 4096 * 4096,
-                  nullptr, 0, nullptr, 0, Z, 0);
+                  nullptr, 0, nullptr, 0, Z, nullptr, 0);
             };
             for (int i = 0; i < 5; ++i) run();
             hipEventRecord(e0, 0);
