@@ -68,6 +68,32 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ x,
     }
     store8(part + (long)blockIdx.x * C + c0, s);
 }
+// dz = dy * gelu'(z) written once, with its column partial sums (the Linear's bias
+// gradient) accumulated in the same pass
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_bwd_colsum_k(const T* __restrict__ dy, const T* __restrict__ z,
+                                                         T* __restrict__ dz, long rows, int C, int rows_per_blk,
+                                                         float* __restrict__ part) {
+    const int c0 = (blockIdx.y * 256 + threadIdx.x) * 8;
+    if (c0 >= C) return;
+    const long r0 = (long)blockIdx.x * rows_per_blk;
+    const long r1 = std::min<long>(rows, r0 + rows_per_blk);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 2
+    for (long r = r0; r < r1; ++r) {
+        float g[8], v[8];
+        load8(dy + r * C + c0, g);
+        load8(z + r * C + c0, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            g[j] *= gelu_erf_grad(v[j]);
+            s[j] += to_f(from_f<T>(g[j]));
+        }
+        store8(dz + r * C + c0, g);
+    }
+    store8(part + (long)blockIdx.x * C + c0, s);
+}
+
 template <typename TO>
 __global__ __launch_bounds__(1024) void colsum_final_k(const float* __restrict__ part, int nblk, int C,
                                                        TO* __restrict__ out, int accumulate) {
@@ -313,6 +339,23 @@ DDL_API int ddl_colsum(int dtype, const void* x, long rows, int C, float* part, 
     dim3 g(nblk, (C / 8 + 255) / 256);
     DISPATCH_T(dtype, (colsum_partial_k<bf16_t><<<g, 256, 0, st>>>((const bf16_t*)x, rows, C, rpb, part)),
                (colsum_partial_k<float><<<g, 256, 0, st>>>((const float*)x, rows, C, rpb, part)));
+    if (out_dtype == 1) colsum_final_k<bf16_t><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, (bf16_t*)out, accumulate);
+    else colsum_final_k<float><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, (float*)out, accumulate);
+    DDL_RETURN_LAUNCH();
+}
+
+// dz = dy * gelu'(z) and out[c] (+)= sum_r dz[r, c] in one pass over dy / z
+DDL_API int ddl_gelu_bwd_colsum(int dtype, const void* dy, const void* z, void* dz, long rows, int C, float* part,
+                                void* out, int out_dtype, int accumulate, hipStream_t st) {
+    if (C % 8) return -1;
+    const int nblk = ddl_colsum_nblk(rows);
+    const int rpb = (int)((rows + nblk - 1) / nblk);
+    dim3 g(nblk, (C / 8 + 255) / 256);
+    DISPATCH_T(dtype,
+               (gelu_bwd_colsum_k<bf16_t><<<g, 256, 0, st>>>((const bf16_t*)dy, (const bf16_t*)z, (bf16_t*)dz, rows,
+                                                              C, rpb, part)),
+               (gelu_bwd_colsum_k<float><<<g, 256, 0, st>>>((const float*)dy, (const float*)z, (float*)dz, rows, C,
+                                                             rpb, part)));
     if (out_dtype == 1) colsum_final_k<bf16_t><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, (bf16_t*)out, accumulate);
     else colsum_final_k<float><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, (float*)out, accumulate);
     DDL_RETURN_LAUNCH();

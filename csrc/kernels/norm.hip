@@ -274,15 +274,17 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
                                                 const T* __restrict__ res, long res_rows, const T* __restrict__ gamma,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 T* __restrict__ dx, float* __restrict__ part, long rows, int H,
-                                                int rows_per_blk) {
-    __shared__ float s_acc[2][4][VPL * 256];
+                                                int rows_per_blk, int dxsum) {
+    // part row per block: [dgamma(H) | dbeta(H) | (dxsum) sum of dx (H)] -- the last is the
+    // bias gradient of the Linear that produced this LayerNorm's input
+    __shared__ float s_acc[3][4][VPL * 256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float dg[VPL][4], db[VPL][4], g[VPL][4];
+    float dg[VPL][4], db[VPL][4], ds[VPL][4], g[VPL][4];
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
         load4(gamma + 256 * k + 4 * lane, g[k]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; }
+        for (int j = 0; j < 4; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; ds[k][j] = 0.f; }
     }
     const long r0 = (long)blockIdx.x * rows_per_blk;
     const long r1 = min(rows, r0 + rows_per_blk);
@@ -317,7 +319,10 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
         for (int k = 0; k < VPL; ++k) {
             float o[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
+            for (int j = 0; j < 4; ++j) {
+                o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
+                ds[k][j] += to_f(from_f<T>(o[j]));       // sum of the stored (rounded) dx
+            }
             store4(dx + row * H + 256 * k + 4 * lane, o);
         }
     }
@@ -327,24 +332,31 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
         for (int j = 0; j < 4; ++j) {
             s_acc[0][w][256 * k + 4 * lane + j] = dg[k][j];
             s_acc[1][w][256 * k + 4 * lane + j] = db[k][j];
+            s_acc[2][w][256 * k + 4 * lane + j] = ds[k][j];
         }
     __syncthreads();
+    const int nv = dxsum ? 3 : 2;
     for (int c = threadIdx.x; c < H; c += 256) {
-        part[(long)blockIdx.x * 2 * H + c] = s_acc[0][0][c] + s_acc[0][1][c] + s_acc[0][2][c] + s_acc[0][3][c];
-        part[(long)blockIdx.x * 2 * H + H + c] = s_acc[1][0][c] + s_acc[1][1][c] + s_acc[1][2][c] + s_acc[1][3][c];
+        for (int v = 0; v < nv; ++v)
+            part[(long)blockIdx.x * nv * H + v * H + c] = s_acc[v][0][c] + s_acc[v][1][c] + s_acc[v][2][c] + s_acc[v][3][c];
     }
 }
 
 template <typename TP>
 __global__ __launch_bounds__(1024) void colsum_partials_k(const float* __restrict__ part, int nblk, int H,
-                                                          TP* __restrict__ dg, TP* __restrict__ db, int acc) {
+                                                          TP* __restrict__ dg, TP* __restrict__ db, int acc,
+                                                          float* __restrict__ dxsum) {
     __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const float a = colsum64(part, nblk, 2L * H, c, c < H, red);
-    const float b = colsum64(part, nblk, 2L * H, H + c, c < H, red);
+    const long stride = (dxsum ? 3L : 2L) * H;
+    const float a = colsum64(part, nblk, stride, c, c < H, red);
+    const float b = colsum64(part, nblk, stride, H + c, c < H, red);
+    float d = 0.f;
+    if (dxsum) d = colsum64(part, nblk, stride, 2 * H + c, c < H, red);
     if (threadIdx.x >= 64 || c >= H) return;
     dg[c] = from_f<TP>(a + (acc ? to_f(dg[c]) : 0.f));
     db[c] = from_f<TP>(b + (acc ? to_f(db[c]) : 0.f));
+    if (dxsum) dxsum[c] = d;
 }
 
 inline int grid_for(long n, int nt = 256, int cap = 4096) {
@@ -510,33 +522,35 @@ DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
                            const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, int acc,
-                           hipStream_t st) {
+                           float* dxsum, hipStream_t st) {
     const int nblk = ddl_ln_bwd_nblk(rows);
     const int rpb = (int)((rows + nblk - 1) / nblk);
     switch (H / 256) {
-        case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
-        case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
-        case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
-        case 4: ln_bwd_k<T, 4><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
-        case 5: ln_bwd_k<T, 5><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
-        case 6: ln_bwd_k<T, 6><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
-        case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb); break;
+        case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 4: ln_bwd_k<T, 4><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 5: ln_bwd_k<T, 5><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 6: ln_bwd_k<T, 6><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
         default: return -1;
     }
-    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(part, nblk, H, dg, db, acc);
+    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(part, nblk, H, dg, db, acc, dxsum);
     return 0;
 }
 
+// part: nblk * (dxsum ? 3 : 2) * H floats; dxsum (nullable, fp32 [H]) receives the
+// column sums of dx -- the bias gradient of the Linear feeding this LayerNorm
 DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res, long res_rows, const void* g,
                        const float* mean, const float* rstd, void* dx, float* part, void* dg, void* db, long rows, int H,
-                       int acc_params, hipStream_t st) {
+                       int acc_params, float* dxsum, hipStream_t st) {
     if (!ddl_ln_supported(H)) return -1;
     if (res_rows <= 0) res_rows = rows;
     int rc = dtype == 1
                  ? ln_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
-                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, st)
+                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, dxsum, st)
                  : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
-                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, st);
+                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum, st);
     if (rc) return rc;
     DDL_RETURN_LAUNCH();
 }

@@ -14,6 +14,7 @@ from typing import Optional
 
 import torch
 
+from . import _lib
 from ._lib import call, dcode, grad_ready, grad_sink, p
 from ._native_gemm import MODE_NN, MODE_NT, MODE_TN, gemm
 from . import _native_elementwise as E
@@ -56,9 +57,25 @@ class _Linear(torch.autograd.Function):
         dy2 = dy.reshape(M, N)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
+        bias_done = False
         if ctx.act == "gelu":
             dz = torch.empty_like(dy2)
-            call("ddl_gelu_bwd", dcode(dy2), p(dy2), p(saved), p(dz), dz.numel())
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                # dGELU and the bias gradient (column sums of dz) in one pass
+                sink = grad_sink(ctx.b_param)
+                db_out = sink if sink is not None else torch.empty(N, dtype=w.dtype, device=w.device)
+                nblk = _lib.fn("ddl_colsum_nblk")(M)
+                part = torch.empty(nblk * N, dtype=torch.float32, device=dy2.device)
+                call("ddl_gelu_bwd_colsum", dcode(dy2), p(dy2), p(saved), p(dz), M, N, p(part), p(db_out),
+                     dcode(db_out), int(sink is not None))
+                if sink is not None:
+                    grad_ready(ctx.b_param)
+                    db_ret = None
+                else:
+                    db_ret = db_out
+                bias_done = True
+            else:
+                call("ddl_gelu_bwd", dcode(dy2), p(dy2), p(saved), p(dz), dz.numel())
         elif ctx.act == "tanh":
             dz = (dy2.float() * (1 - saved.float() ** 2)).to(dy2.dtype)
         elif ctx.act == "relu":
@@ -78,9 +95,20 @@ class _Linear(torch.autograd.Function):
             else:
                 dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
                 gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if bias_done:
+            db = db_ret
+        elif ctx.has_bias and ctx.needs_input_grad[2]:
             sink = grad_sink(ctx.b_param)
-            if sink is not None:
+            # a LayerNorm backward that produced dy already summed its columns
+            pre = getattr(dy, "_ddl_colsum", None) if ctx.act is None else None
+            pre = pre[0] if (pre is not None and pre[1] == dy._version) else None
+            if pre is not None and pre.numel() == N:
+                if sink is not None:
+                    sink.add_(pre)
+                    grad_ready(ctx.b_param)
+                else:
+                    db = pre.to(w.dtype)
+            elif sink is not None:
                 E.colsum(dz, sink, accumulate=True)
                 grad_ready(ctx.b_param)
             else:

@@ -136,13 +136,18 @@ class _LayerNorm(torch.autograd.Function):
         H = x.shape[-1]
         rows = x.numel() // H
         nblk = _lib.fn("ddl_ln_bwd_nblk")(rows)
-        part = torch.empty(nblk * 2 * H, dtype=torch.float32, device=x.device)
+        part = torch.empty(nblk * 3 * H, dtype=torch.float32, device=x.device)
+        dxsum = torch.empty(H, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
         direct = sg is not None and sb is not None
         dg, db = (sg, sb) if direct else (torch.empty_like(weight), torch.empty_like(weight))
         call("ddl_ln_bwd", dcode(x), p(dy), p(x), p(res), ctx.res_rows, p(weight), p(stats[0]), p(stats[1]), p(dx),
-             p(part), p(dg), p(db), rows, H, int(direct))
+             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum))
+        # the column sums of dx ride along on the gradient tensor: the Linear whose output
+        # fed this LayerNorm takes them as its bias gradient instead of re-reading dx
+        # (the version guards against autograd accumulating another gradient into dx in place)
+        dx._ddl_colsum = (dxsum, dx._version)
         if direct:
             grad_ready(ctx.params[0])
             grad_ready(ctx.params[1])
