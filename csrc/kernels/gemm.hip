@@ -264,10 +264,9 @@ __device__ __forceinline__ long out_row(const Params& p, int m) {
 }
 
 template <int LA, int LB, int BNT>
-__global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
+__device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
     constexpr int WN = BNT / 2;        // wave tile N extent (64 or 32)
     constexpr int NJ = WN / 16;        // MFMA column tiles per wave
-    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
     // ---- XCD-aware bijective tile remap
     const int nwg = p.tiles_m * p.tiles_n;
     const int bid = blockIdx.x;
@@ -494,6 +493,28 @@ __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
     }
 }
 
+template <int LA, int LB, int BNT>
+__global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+    gemm_body<LA, LB, BNT>(p, smem);
+}
+
+// Several independent GEMMs of one shape class in one launch (blockIdx.z picks the
+// problem): the stride-s conv dgrad's s*s output-parity classes run concurrently
+// instead of as s*s short serial launches.
+constexpr int MAX_MC = 4;
+struct ParamsMC {
+    Params c[MAX_MC];
+};
+
+template <int LA, int LB, int BNT>
+__global__ __launch_bounds__(NT, 2) void gemm_mc_k(ParamsMC pm) {
+    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+    const Params& p = pm.c[blockIdx.z];
+    if ((int)blockIdx.x >= p.tiles_m * p.tiles_n) return;   // this class has fewer tiles
+    gemm_body<LA, LB, BNT>(p, smem);
+}
+
 // Sum split-K fp32 partials, apply the epilogue, write bf16/fp32.
 __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ part, int splits, long split_stride,
                                                      long ldw, int M, int N, long ldc, void* out, int out_f32,
@@ -641,4 +662,42 @@ DDL_API int ddl_gemm_n64(int mode, const void* A, long lda, const void* B, long 
                          int accumulate, float* colstats, hipStream_t st) {
     return gemm_entry(1, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, bias_bf16, act, aux, out_f32, splits, workspace,
                       ws_elems, conv, row_remap, res, accumulate, colstats, st);
+}
+
+// Multi-problem launch: n (<= 4) CONV-mode GEMMs sharing A, N and the output tensor,
+// each with its own B, K and conv descriptor (18 ints per problem, as ddl_gemm) and
+// output-row remap -- the parity classes of a strided convolution's dgrad.
+// No split-K, no epilogue ops.
+DDL_API int ddl_gemm_conv_multi(int narrow, int n, const void* A, const void* const* Bs, const int* Ms, const int* Ks,
+                                void* C, long ldc, int N, const int* convs, hipStream_t st) {
+    if (n < 1 || n > MAX_MC) return -1;
+    ParamsMC pm{};
+    int max_tiles = 0;
+    const int bnt = narrow ? 64 : 128;
+    for (int i = 0; i < n; ++i) {
+        Params& p = pm.c[i];
+        p.A = (const bf16_t*)A;
+        p.B = (const bf16_t*)Bs[i];
+        p.lda = 0;
+        p.ldb = Ks[i];
+        p.C = C;
+        p.ldc = ldc;
+        p.M = Ms[i];
+        p.N = N;
+        p.K = Ks[i];
+        p.row_remap = 1;
+        p.splits = 1;
+        p.kt_per_split = (Ks[i] + BK - 1) / BK;
+        p.ldw = ldc;
+        fill_conv(p.cd, convs + 18 * i);
+        p.tiles_m = (p.M + BM - 1) / BM;
+        p.tiles_n = (p.N + bnt - 1) / bnt;
+        if (p.M <= 0) p.tiles_m = 0;
+        max_tiles = std::max(max_tiles, p.tiles_m * p.tiles_n);
+    }
+    if (max_tiles == 0) return 0;
+    dim3 grid(max_tiles, 1, n);
+    if (narrow) hipLaunchKernelGGL((gemm_mc_k<CONV, KC, 64>), grid, dim3(NT), 0, st, pm);
+    else hipLaunchKernelGGL((gemm_mc_k<CONV, KC, 128>), grid, dim3(NT), 0, st, pm);
+    return (int)hipGetLastError();
 }

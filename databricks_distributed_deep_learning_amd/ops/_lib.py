@@ -113,6 +113,7 @@ _SIGS = {
     "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P],
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
+    "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],
     "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_ln_supported": [I],
     "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, P],

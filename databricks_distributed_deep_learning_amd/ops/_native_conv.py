@@ -29,6 +29,7 @@ def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, 
 
 
 STATS_MIN_K = int(os.environ.get("DDL_BN_STATS_MIN_K", "2048"))
+_DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
 
 def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
@@ -76,7 +77,10 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
     _, P, Q, _ = dy.shape
     if R == 1 and S == 1 and stride == 1 and pad == 0:
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
-        gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K, residual=residual)
+        if _DGRAD_NT:   # NT against W^T (k-contiguous operands; the weight copy is tiny)
+            gemm(MODE_NT, dy, K, _w_dgrad(w, [0], [0]).view(C, K), K, dx, C, N * H * W_, C, K, residual=residual)
+        else:
+            gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K, residual=residual)
         return dx
     if stride == 1:
         wt = _w_dgrad(w, list(range(R - 1, -1, -1)), list(range(S - 1, -1, -1)))   # flipped [C, R, S, K]
@@ -101,15 +105,68 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
                 continue
             classes.append((a, b, rs, ss, Ho, Wo))
     dx = (torch.zeros if empty else torch.empty)(N, H, W_, C, dtype=dy.dtype, device=dy.device)
+    probs = []
     for a, b, rs, ss, Ho, Wo in classes:
         wc = _w_dgrad(w, rs, ss)                                     # [C, R', S', K]
         h_off = (a + pad - rs[0]) // stride
         w_off = (b + pad - ss[0]) // stride
         Rp, Sp = len(rs), len(ss)
-        gemm(MODE_CONV, dy, 0, wc, Rp * Sp * K, dx, C, N * Ho * Wo, C, Rp * Sp * K,
-             conv=_desc(N, P, Q, K, Ho, Wo, 1, h_off, w_off, -1, -1, Rp, Sp, H, W_, stride, a, b),
-             row_remap=True)
+        probs.append((wc, N * Ho * Wo, Rp * Sp * K,
+                      _desc(N, P, Q, K, Ho, Wo, 1, h_off, w_off, -1, -1, Rp, Sp, H, W_, stride, a, b)))
+
+    def serial(out):
+        for wc, Mc, Kc, desc in probs:
+            gemm(MODE_CONV, dy, 0, wc, Kc, out, C, Mc, C, Kc, conv=desc, row_remap=True)
+
+    def multi(out, narrow):
+        bs = (ctypes.c_void_p * len(probs))(*[pr[0].data_ptr() for pr in probs])
+        ms = (ctypes.c_int * len(probs))(*[pr[1] for pr in probs])
+        ks = (ctypes.c_int * len(probs))(*[pr[2] for pr in probs])
+        cv = (ctypes.c_int * (18 * len(probs)))(*[v for pr in probs for v in pr[3]])
+        rc = _lib.fn("ddl_gemm_conv_multi")(int(narrow), len(probs), dy.data_ptr(), bs, ms, ks, out.data_ptr(), C, C,
+                                            cv, _lib.stream())
+        if rc != 0:
+            raise RuntimeError(f"ddl_gemm_conv_multi failed: {rc}")
+
+    if 1 < len(probs) <= 4:
+        key = (tuple(dy.shape), tuple(w.shape), stride, pad)
+        choice = _MULTI_CHOICE.get(key)
+        if choice is None:
+            choice = _pick_dgrad_path(key, serial, multi, dx)
+        if choice == "serial":
+            serial(dx)
+        else:
+            multi(dx, choice == "multi_narrow")
+    else:
+        serial(dx)
     return dx
+
+
+_MULTI_CHOICE: dict = {}
+
+
+def _pick_dgrad_path(key, serial, multi, dx):
+    """Time the per-class launches against the single multi-class launch (once per shape)."""
+    if not dx.is_cuda or torch.cuda.is_current_stream_capturing():
+        return "serial"
+    scratch = torch.empty_like(dx)
+    serial(scratch)                      # also tunes the per-class GEMMs
+    cands = {"serial": lambda: serial(scratch), "multi": lambda: multi(scratch, False),
+             "multi_narrow": lambda: multi(scratch, True)}
+    best, best_t = "serial", float("inf")
+    for name, fn in cands.items():
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            fn()
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1)
+        if t < best_t:
+            best, best_t = name, t
+    _MULTI_CHOICE[key] = best
+    return best
 
 
 def _wgrad(dy, x, w_shape, stride, pad, out=None):

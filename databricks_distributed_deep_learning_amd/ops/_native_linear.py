@@ -10,6 +10,7 @@ backward: dz = dy * act'(z)       (GELU: ddl_gelu_bwd; tanh/relu from the output
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -25,6 +26,9 @@ def _ok(x, w) -> bool:
     N = w.shape[0]
     return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0
             and x.numel() > 0)
+
+
+_DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
 
 class _Linear(torch.autograd.Function):
@@ -85,7 +89,13 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
-            gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
+            if _DGRAD_NT and M >= 4 * K:
+                # dx = dz W as an NT GEMM against W^T (both operands k-contiguous: ds_read_b128
+                # fragments instead of transposed reads); the weight copy is tiny next to dz
+                wt = w.t().contiguous()
+                gemm(MODE_NT, dz, N, wt, N, dx, K, M, K, N)
+            else:
+                gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
             dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
