@@ -1,0 +1,112 @@
+// Stand-alone GEMM timing against the built kernel library (no torch, no Python):
+// every case is timed with hipEvents around back-to-back launches, so the numbers
+// are pure device time.  Also the target for `rocprofv3 --pmc` passes.
+//
+//   build: hipcc -O2 --offload-arch=gfx950 csrc/bench/gemm_sweep.cpp -o build/gemm_sweep \
+//            -Ldatabricks_distributed_deep_learning_amd/_native -lddl_kernels \
+//            -Wl,-rpath,$PWD/databricks_distributed_deep_learning_amd/_native
+//   run:   build/gemm_sweep [kernel mode M N K splits]...   (no args: the built-in sweep)
+//          kernel: big | small | narrow; mode 0 NT, 1 NN, 2 TN
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define GEMM_ARGS                                                                                                    \
+    int mode, const void *A, long lda, const void *B, long ldb, void *C, long ldc, int M, int N, int K,            \
+        const void *bias, int bias_bf16, int act, void *aux, int out_f32, int splits, float *ws, long ws_elems,     \
+        const int *conv, int row_remap, const void *res, int accumulate
+extern "C" int ddl_gemm_big2(GEMM_ARGS, const void* zero, float* colstats, hipStream_t st);
+extern "C" int ddl_gemm(GEMM_ARGS, float* colstats, hipStream_t st);
+extern "C" int ddl_gemm_n64(GEMM_ARGS, float* colstats, hipStream_t st);
+
+struct Case {
+    std::string kernel;
+    int mode, M, N, K, splits;
+};
+
+int main(int argc, char** argv) {
+    std::vector<Case> cases;
+    if (argc > 1) {
+        for (int i = 1; i + 5 < argc; i += 6)
+            cases.push_back({argv[i], atoi(argv[i + 1]), atoi(argv[i + 2]), atoi(argv[i + 3]), atoi(argv[i + 4]),
+                             atoi(argv[i + 5])});
+    } else {
+        for (int K : {256, 512, 768, 1536, 3072, 6144}) cases.push_back({"big", 0, 16384, 3072, K, 1});
+        const int bert[][3] = {{16384, 2304, 768}, {16384, 768, 768}, {16384, 3072, 768}, {16384, 768, 3072}};
+        for (auto& s : bert)
+            for (const char* k : {"big", "small"}) cases.push_back({k, 0, s[0], s[1], s[2], 1});
+        for (auto& s : bert)
+            for (const char* k : {"big", "small"}) cases.push_back({k, 1, s[0], s[2], s[1], 1});
+        for (int sp : {2, 4, 8, 9}) cases.push_back({"big", 2, 2304, 768, 16384, sp});
+        for (int sp : {2, 4, 8}) cases.push_back({"big", 2, 3072, 768, 16384, sp});
+        for (int sp : {1, 2, 4}) cases.push_back({"small", 2, 2304, 768, 16384, sp});
+        cases.push_back({"big", 0, 8192, 8192, 8192, 1});
+    }
+    // buffers sized from the cases (an operand smaller than M*K would be read out of bounds)
+    long maxe = 0, maxc = 0, ws_elems = 0;
+    for (const Case& c : cases) {
+        maxe = std::max({maxe, (long)c.M * c.K, (long)c.N * c.K});
+        maxc = std::max(maxc, (long)c.M * c.N);
+        if (c.splits > 1) ws_elems = std::max(ws_elems, (long)c.M * c.N * c.splits);
+    }
+    void *A, *B, *C, *Z;
+    float* ws = nullptr;
+    if (hipMalloc(&A, maxe * 2) || hipMalloc(&B, maxe * 2) || hipMalloc(&C, maxc * 4) || hipMalloc(&Z, 256) ||
+        (ws_elems && hipMalloc(&ws, ws_elems * 4))) {
+        printf("allocation failed\n");
+        return 1;
+    }
+    {   // uniform random bf16 in [-1, 1): zero / constant operands clock the chip up
+        std::vector<uint16_t> h(maxe);
+        uint32_t s = 12345;
+        for (auto& v : h) {
+            s = s * 1664525u + 1013904223u;
+            const float f = ((s >> 8) * (1.0f / 16777216.0f)) * 2.f - 1.f;
+            uint32_t u;
+            memcpy(&u, &f, 4);
+            v = (uint16_t)(u >> 16);
+        }
+        hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+        hipMemcpy(B, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    }
+    hipMemset(Z, 0, 256);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (const Case& c : cases) {
+        const long lda = c.mode == 2 ? c.M : c.K;
+        const long ldb = c.mode == 0 ? c.K : c.N;
+        auto run = [&]() -> int {
+            if (c.kernel == "big")
+                return ddl_gemm_big2(c.mode, A, lda, B, ldb, C, c.N, c.M, c.N, c.K, nullptr, 0, 0, nullptr, 0, c.splits,
+                                     ws, ws_elems, nullptr, 0, nullptr, 0, Z, nullptr, 0);
+            auto f = c.kernel == "narrow" ? ddl_gemm_n64 : ddl_gemm;
+            return f(c.mode, A, lda, B, ldb, C, c.N, c.M, c.N, c.K, nullptr, 0, 0, nullptr, 0, c.splits, ws, ws_elems,
+                     nullptr, 0, nullptr, 0, nullptr, 0);
+        };
+        int rc = run();
+        if (rc != 0) {
+            printf("%-6s mode=%d M=%d N=%d K=%d splits=%d  error %d\n", c.kernel.c_str(), c.mode, c.M, c.N, c.K,
+                   c.splits, rc);
+            continue;
+        }
+        for (int i = 0; i < 5; ++i) run();
+        const int it = 30;
+        hipEventRecord(e0, 0);
+        for (int i = 0; i < it; ++i) run();
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        ms /= it;
+        printf("%-6s mode=%d M=%5d N=%5d K=%5d splits=%d  %.4f ms  %7.1f TF\n", c.kernel.c_str(), c.mode, c.M, c.N, c.K,
+               c.splits, ms, 2.0 * c.M * c.N * c.K / ms / 1e9);
+        fflush(stdout);
+    }
+    return 0;
+}

@@ -33,6 +33,8 @@
 //     epilogue) by a second kernel; XCD-aware bijective block remap.
 #include "ddl_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 #ifndef DDL_STAGGER
@@ -360,22 +362,82 @@ __device__ __forceinline__ void epilogue4(const BigParams& p, long orow, int n, 
     }
 }
 
-template <int LA, int LB, bool KTAIL>
-__global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
+// Direct epilogue site: the MFMA output layout gives a lane 4 consecutive
+// columns of one row, so a site is finished in registers and written with one
+// 8-byte (bf16) or 16-byte (fp32) store -- no LDS round trip, which is what lets
+// a persistent block restage the next tile's operands while this tile drains.
+// Covers bias / ReLU / accumulate / fp32 / split-K partial outputs; GELU, tanh,
+// dGELU, residual, row remap and BN statistics take the LDS-staged epilogue.
+__device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const f32x4& a, int split) {
+    if (m >= p.M || n >= p.N) return;
+    const bool full = n + 3 < p.N;
+    const int nv = p.N - n;
+    float v[4] = {a[0], a[1], a[2], a[3]};
+    if (p.splits > 1) {
+        store4g((float*)p.C + split * p.split_stride + (long)m * p.ldc + n, full, nv, v);
+        return;
+    }
+    if (p.bias) {
+        float bv[4];
+        if (p.bias_bf16) load4g((const bf16_t*)p.bias + n, full, nv, bv);
+        else load4g((const float*)p.bias + n, full, nv, bv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bv[r];
+    }
+    if (p.act == ACT_RELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+    if (p.out_f32) {
+        float* cp = (float*)p.C + (long)m * p.ldc + n;
+        if (p.accumulate) {
+            float o[4];
+            load4g(cp, full, nv, o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += o[r];
+        }
+        store4g(cp, full, nv, v);
+    } else {
+        bf16_t* cp = (bf16_t*)p.C + (long)m * p.ldc + n;
+        if (p.accumulate) {
+            float o[4];
+            load4g(cp, full, nv, o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += o[r];
+        }
+        store4g(cp, full, nv, v);
+    }
+}
+
+// DIRECT: epilogue from registers (direct4) and, with it, a persistent grid: a
+// block walks tiles blockIdx.x, +gridDim.x, ...; after a tile's last MFMA it
+// stages the next tile's first K-tile, stores this tile from registers, then
+// stages the rest of the prologue, so the result stores drain under the next
+// tile's loads instead of in a chip-wide burst between waves of blocks.
+template <int LA, int LB, bool KTAIL, bool DIRECT>
+__global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
     const int nwg = p.tiles_m * p.tiles_n;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, qn_ = nwg >> 3, rn = nwg & 7;
-    const int wg = (xcd < rn ? xcd * (qn_ + 1) : rn * (qn_ + 1) + (xcd - rn) * qn_) + (bid >> 3);
-    // grouped order: consecutive tiles (the ones an XCD runs together) cover a
-    // GROUP_M x k block of tiles instead of one long row, so the A and B panels
-    // they stream stay L2-resident at large M, N
-    const int per_group = DDL_GROUP_M * p.tiles_n;
-    const int grp = wg / per_group, first_m = grp * DDL_GROUP_M;
-    const int gsz = min(p.tiles_m - first_m, DDL_GROUP_M);
-    const int wl = wg - grp * per_group;
-    const int tm = first_m + wl % gsz, tn = wl / gsz;
-    const int m0 = tm * TB, n0 = tn * TB;
+    int tm, tn, m0, n0;
+    // XCD-aware bijective remap: an XCD (blockIdx & 7) owns a contiguous range of
+    // tile ids; a persistent block's later tiles keep its XCD (gridDim.x % 8 == 0)
+    auto coords = [&](int bid) {
+        const int xcd = bid & 7, qn_ = nwg >> 3, rn = nwg & 7;
+        const int wg = (xcd < rn ? xcd * (qn_ + 1) : rn * (qn_ + 1) + (xcd - rn) * qn_) + (bid >> 3);
+        // grouped order: consecutive tiles (the ones an XCD runs together) cover a
+        // GROUP_M x k block of tiles instead of one long row, so the A and B panels
+        // they stream stay L2-resident at large M, N
+        const int per_group = DDL_GROUP_M * p.tiles_n;
+        const int grp = wg / per_group, first_m = grp * DDL_GROUP_M;
+        const int gsz = min(p.tiles_m - first_m, DDL_GROUP_M);
+        const int wl = wg - grp * per_group;
+        tm = first_m + wl % gsz;
+        tn = wl / gsz;
+        m0 = tm * TB;
+        n0 = tn * TB;
+    };
+    int vt = blockIdx.x;
+    coords(vt);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = w >> 2, wn = w & 3;
     const int split = blockIdx.y;
@@ -390,14 +452,17 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
     sb.init(p, n0);
 
     f32x4 acc[2][2][4][2];
+    auto zero_acc = [&]() {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+                    for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    };
+    zero_acc();
 
     bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
     auto readA = [&](int buf, int qm) {
@@ -456,12 +521,15 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
         BARRIER();
     };
 
-    if (nK > 0) {
-        // prologue: E <- tile kt0 (all halves), O <- tile kt0+1 (A0, B0, B1)
+    // prologue, first part: E <- tile kt0 (all halves)
+    auto prologueE = [&]() {
         sa.stage(p, smem, 0, 0, kt0);
         sb.stage(p, smem, 0, 0, kt0);
         sb.stage(p, smem, 0, 1, kt0);
         sa.stage(p, smem, 0, 1, kt0);
+    };
+    // second part: O <- tile kt0+1 (A0, B0, B1); E landed; wave groups staggered
+    auto prologueO = [&]() {
         if (nK > 1) {
             sa.stage(p, smem, 1, 0, kt0 + 1);
             sb.stage(p, smem, 1, 0, kt0 + 1);
@@ -476,45 +544,84 @@ __global__ __launch_bounds__(NTH, 2) void gemm_big_k(BigParams p) {
         // overlaps the other's LDS reads / DMA issue on the same SIMD
         if (wm == 1) BARRIER();
 #endif
-        const int pairs = nK / 2;
-        for (int it = 0; it < pairs; ++it) {
-            const int kE = kt0 + 2 * it, kO = kE + 1;
-            const bool more = kE + 2 < kt_end;
-            const bool moreO = kO + 2 < kt_end;
-            phasesE(kE, true, more);
-            // phase 5: O (0,0)
-            readA(1, 0);
-            readB(1, 0, fb0);
-            if (more) sa.stage(p, smem, 0, 1, kE + 2);
-            READS_DONE_BARRIER();
-            mma(0, 0, fb0);
-            BARRIER();
-            // phase 6: O (0,1)
-            readB(1, 1, fb1);
-            if (moreO) sa.stage(p, smem, 1, 0, kO + 2);
-            READS_DONE_BARRIER();
-            mma(0, 1, fb1);
-            BARRIER();
-            // phase 7: O (1,1)
-            readA(1, 1);
-            if (moreO) sb.stage(p, smem, 1, 0, kO + 2);
-            READS_DONE_BARRIER();
-            mma(1, 1, fb1);
-            BARRIER();
-            // phase 8: O (1,0); retire E(kE+2)
-            if (moreO) { sb.stage(p, smem, 1, 1, kO + 2); VM6(); } else { VM0(); }
-            BARRIER();
-            mma(1, 0, fb0);
-            BARRIER();
-        }
-        // odd tile count: the last E tile (fully landed: phase 8 waited vmcnt(0))
-        if (nK & 1) phasesE(kt_end - 1, false, false);
+    };
+
+    if (nK > 0) {
+        prologueE();
+        prologueO();
+    }
+    for (;;) {
+        if (nK > 0) {
+            const int pairs = nK / 2;
+            for (int it = 0; it < pairs; ++it) {
+                const int kE = kt0 + 2 * it, kO = kE + 1;
+                const bool more = kE + 2 < kt_end;
+                const bool moreO = kO + 2 < kt_end;
+                phasesE(kE, true, more);
+                // phase 5: O (0,0)
+                readA(1, 0);
+                readB(1, 0, fb0);
+                if (more) sa.stage(p, smem, 0, 1, kE + 2);
+                READS_DONE_BARRIER();
+                mma(0, 0, fb0);
+                BARRIER();
+                // phase 6: O (0,1)
+                readB(1, 1, fb1);
+                if (moreO) sa.stage(p, smem, 1, 0, kO + 2);
+                READS_DONE_BARRIER();
+                mma(0, 1, fb1);
+                BARRIER();
+                // phase 7: O (1,1)
+                readA(1, 1);
+                if (moreO) sb.stage(p, smem, 1, 0, kO + 2);
+                READS_DONE_BARRIER();
+                mma(1, 1, fb1);
+                BARRIER();
+                // phase 8: O (1,0); retire E(kE+2)
+                if (moreO) { sb.stage(p, smem, 1, 1, kO + 2); VM6(); } else { VM0(); }
+                BARRIER();
+                mma(1, 0, fb0);
+                BARRIER();
+            }
+            // odd tile count: the last E tile (fully landed: phase 8 waited vmcnt(0))
+            if (nK & 1) phasesE(kt_end - 1, false, false);
 #if DDL_STAGGER
-        if (wm == 0) BARRIER();
+            // realign the groups: after this barrier every wave has finished its
+            // last MFMA and every fragment read, so the LDS buffers are free
+            if (wm == 0) BARRIER();
 #endif
+        }
+        if (DIRECT) {
+            const int vn = vt + gridDim.x;
+            const bool next = vn < nwg;
+            const int m0c = m0, n0c = n0;
+            if (next) {
+                coords(vn);
+                sa.init(p, m0);
+                sb.init(p, n0);
+                if (nK > 0) prologueE();
+            }
+            const int g4 = (lane >> 4) * 4, r16 = lane & 15;
+#pragma unroll
+            for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+                for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            direct4(p, m0c + qm * 128 + wm * 64 + i * 16 + r16, n0c + qn * 128 + wn * 32 + j * 16 + g4,
+                                    acc[qm][qn][i][j], split);
+            if (!next) return;
+            zero_acc();
+            vt = vn;
+            if (nK > 0) prologueO();
+            continue;
+        }
+        break;
     }
 
-    // ---------------- epilogue
+    // ---------------- LDS-staged epilogue (general: every epilogue option)
     // The accumulators go through LDS one 128x128 quarter at a time (fp32, rows
     // padded to 132 floats: the 16 rows a ds_write_b128 group touches land on
     // distinct bank quads).  Each thread then owns 8 consecutive columns of a
@@ -639,6 +746,26 @@ void fill_conv(ConvDesc& cd, const int* d) {
     cd.fd_S = make_fastdiv((uint32_t)std::max(1, cd.S));
 }
 
+int num_cus() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                     hipSuccess || v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
+
+// DDL_GEMM_DIRECT=0 forces the LDS-staged epilogue everywhere (A/B timing, tests)
+bool direct_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int LA, int LB>
 int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st) {
     p.tiles_m = (p.M + TB - 1) / TB;
@@ -658,10 +785,24 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // KTAIL: per-chunk K checks; also selects the per-chunk tap decomposition for
     // convolutions whose channel count is not a multiple of 64
     const bool ktail = (p.K % BK) != 0 || ((LA == CONV || LB == CONVW) && (p.cd.C % BK) != 0);
-    if (ktail)
-        hipLaunchKernelGGL((gemm_big_k<LA, LB, true>), dim3(p.tiles_m * p.tiles_n, splits), dim3(NTH), 0, st, kp);
-    else
-        hipLaunchKernelGGL((gemm_big_k<LA, LB, false>), dim3(p.tiles_m * p.tiles_n, splits), dim3(NTH), 0, st, kp);
+    // register epilogue + persistent grid when the epilogue is one direct4 covers
+    // (split-K partials always: the reduce kernel applies the real epilogue)
+    const bool direct = direct_enabled() &&
+        (splits > 1 || (!p.colstats && !p.row_remap && !p.res && (p.act == ACT_NONE || p.act == ACT_RELU)));
+    const int nwg = p.tiles_m * p.tiles_n;
+    int gx = nwg;
+    if (direct) {
+        const int cap = std::max(8, (num_cus() / splits) & ~7);   // multiple of 8: blocks keep their XCD
+        gx = std::min(nwg, cap);
+    }
+    const dim3 grid(gx, splits);
+    if (direct) {
+        if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true>), grid, dim3(NTH), 0, st, kp);
+        else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true>), grid, dim3(NTH), 0, st, kp);
+    } else {
+        if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, false>), grid, dim3(NTH), 0, st, kp);
+        else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, false>), grid, dim3(NTH), 0, st, kp);
+    }
     if (splits > 1) {
         const long total = (long)p.M * ((p.N + 3) / 4);
         const int g = (int)std::min<long>(16384, (total + 255) / 256);

@@ -201,3 +201,41 @@ def test_strided_dgrad_class_paths(path, N, H, W, C, K, R, pad):
     xr = x.float().requires_grad_(True)
     conv2d_reference(xr, w.float(), 2, pad).backward(dy.float())
     assert _rel_err(dx, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(8292, 2304, 136), (4100, 4200, 768), (520, 264, 1024)])
+@pytest.mark.parametrize("variant", ["plain", "bias_bf16_relu", "bias_f32", "acc_f32", "acc_bf16"])
+def test_big_direct_persistent_epilogue(M, N, K, variant):
+    """Register epilogue + persistent grid of the 256x256 kernel (> 256 tiles: blocks
+    walk several tiles, the next tile's prologue overlaps this tile's stores)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    torch.manual_seed(7)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    ref = a.float() @ w.float().t()
+    kw = {}
+    out_dtype = torch.bfloat16
+    if variant == "bias_bf16_relu":
+        b = torch.randn(N, device=dev).to(torch.bfloat16)
+        kw = dict(bias=b, act="relu")
+        ref = torch.relu(ref + b.float())
+    elif variant == "bias_f32":
+        b = torch.randn(N, device=dev)
+        kw = dict(bias=b)
+        ref = ref + b
+    elif variant.startswith("acc"):
+        out_dtype = torch.float32 if variant == "acc_f32" else torch.bfloat16
+        kw = dict(accumulate=True)
+    c = torch.randn(M, N, device=dev).to(out_dtype)
+    if variant.startswith("acc"):
+        ref = ref + c.float()
+    NG.gemm(0, a, K, w, K, c, N, M, N, K, kernel="big", **kw)
+    assert _rel_err(c, ref) < (2e-3 if out_dtype == torch.float32 else 1e-2)
+    # every output element written exactly once: a second run into a NaN-filled
+    # buffer must leave no NaN (non-accumulating variants)
+    if not variant.startswith("acc"):
+        c2 = torch.full((M, N), float("nan"), device=dev, dtype=out_dtype)
+        NG.gemm(0, a, K, w, K, c2, N, M, N, K, kernel="big", **kw)
+        assert not torch.isnan(c2).any()
+        assert torch.equal(c2, c)
