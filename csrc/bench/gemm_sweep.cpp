@@ -6,7 +6,8 @@
 //            -Ldatabricks_distributed_deep_learning_amd/_native -lddl_kernels \
 //            -Wl,-rpath,$PWD/databricks_distributed_deep_learning_amd/_native
 //   run:   build/gemm_sweep [kernel mode M N K splits]...   (no args: the built-in sweep)
-//          kernel: big | small | narrow; mode 0 NT, 1 NN, 2 TN
+//          kernel: big | bigs (big + BatchNorm-statistics epilogue) | small | narrow;
+//          mode 0 NT, 1 NN, 2 TN
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
@@ -54,10 +55,12 @@ int main(int argc, char** argv) {
         maxc = std::max(maxc, (long)c.M * c.N);
         if (c.splits > 1) ws_elems = std::max(ws_elems, (long)c.M * c.N * c.splits);
     }
+    long stats_elems = 0;
+    for (const Case& c : cases) stats_elems = std::max(stats_elems, 2L * ((c.M + 255) / 256) * 2 * c.N);
     void *A, *B, *C, *Z;
-    float* ws = nullptr;
+    float *ws = nullptr, *stats = nullptr;
     if (hipMalloc(&A, maxe * 2) || hipMalloc(&B, maxe * 2) || hipMalloc(&C, maxc * 4) || hipMalloc(&Z, 256) ||
-        (ws_elems && hipMalloc(&ws, ws_elems * 4))) {
+        hipMalloc(&stats, stats_elems * 4) || (ws_elems && hipMalloc(&ws, ws_elems * 4))) {
         printf("allocation failed\n");
         return 1;
     }
@@ -82,9 +85,9 @@ int main(int argc, char** argv) {
         const long lda = c.mode == 2 ? c.M : c.K;
         const long ldb = c.mode == 0 ? c.K : c.N;
         auto run = [&]() -> int {
-            if (c.kernel == "big")
+            if (c.kernel == "big" || c.kernel == "bigs")
                 return ddl_gemm_big2(c.mode, A, lda, B, ldb, C, c.N, c.M, c.N, c.K, nullptr, 0, 0, nullptr, 0, c.splits,
-                                     ws, ws_elems, nullptr, 0, nullptr, 0, Z, nullptr, 0);
+                                     ws, ws_elems, nullptr, 0, nullptr, 0, Z, c.kernel == "bigs" ? stats : nullptr, 0);
             auto f = c.kernel == "narrow" ? ddl_gemm_n64 : ddl_gemm;
             return f(c.mode, A, lda, B, ldb, C, c.N, c.M, c.N, c.K, nullptr, 0, 0, nullptr, 0, c.splits, ws, ws_elems,
                      nullptr, 0, nullptr, 0, nullptr, 0);

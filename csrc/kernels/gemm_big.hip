@@ -83,7 +83,9 @@ struct BigParams {
     float* colstats;          // BN statistics partials of the bf16 output: [tile_m][2][N]
     ConvDesc cd;
     int tiles_m, tiles_n;
+    int ek;                   // register-epilogue variant (EK_*), set by the launcher
 };
+enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2 };
 
 __device__ __forceinline__ int half_off(int buf, int x, int h) { return ((buf * 2 + x) * 2 + h) * HALF; }
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -362,6 +364,20 @@ __device__ __forceinline__ void epilogue4(const BigParams& p, long orow, int n, 
     }
 }
 
+// Sum over the 16 lanes of a DPP row (every lane of the row gets the total):
+// xor 1, xor 2 (quad_perm), then half-row and row mirrors -- four DPP adds, no LDS.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                                     false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);   // row_half_mirror
+    return dpp_add<0x140>(v);   // row_mirror
+}
+
 // Direct epilogue site: the MFMA output layout gives a lane 4 consecutive
 // columns of one row, so a site is finished in registers and written with one
 // 8-byte (bf16) or 16-byte (fp32) store -- no LDS round trip, which is what lets
@@ -407,6 +423,86 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
         }
         store4g(cp, full, nv, v);
     }
+}
+
+// Register epilogue of one 256x256 tile.  Lane layout: acc[qm][qn][i][j] holds
+// row m0 + qm*128 + wm*64 + i*16 + (lane & 15), columns n0 + qn*128 + wn*32 +
+// j*16 + 4*(lane >> 4) .. +3.
+//   EK_BF16: interior tile, bf16 out, optional bf16 bias -- one 8-byte store a site
+//   EK_F32 : interior tile, fp32 split-K partial or fp32 out (+accumulate) -- one 16-byte store
+//   EK_GEN : anything direct4 covers, with bounds checks (edge tiles)
+// With colstats (EK_BF16 / EK_GEN) the BatchNorm statistics of the bf16 output --
+// what BN will read -- are summed per lane over its 8 rows, then over the 16
+// lanes holding the same columns; one partial row per (tile, wave row).
+template <int EK>
+__device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
+                                           int wm, int wn, int lane, int split) {
+    const int g4 = (lane >> 4) * 4, r16 = lane & 15;
+    const bool stats = EK != EK_F32 && p.colstats;
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + qn * 128 + wn * 32 + j * 16 + g4;
+            float bv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (EK == EK_BF16 && p.bias) load4((const bf16_t*)p.bias + n, bv);
+            float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = m0 + qm * 128 + wm * 64 + i * 16 + r16;
+                    const f32x4& a = acc[qm][qn][i][j];
+                    if (EK == EK_BF16) {
+                        const uint32_t lo = pack2bf(a[0] + bv[0], a[1] + bv[1]);
+                        const uint32_t hi = pack2bf(a[2] + bv[2], a[3] + bv[3]);
+                        *reinterpret_cast<uint2*>((bf16_t*)p.C + (long)m * p.ldc + n) = make_uint2(lo, hi);
+                        if (stats) {
+                            const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                                __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                cs[e] += t[e];
+                                cq[e] += t[e] * t[e];
+                            }
+                        }
+                    } else if (EK == EK_F32) {
+                        if (p.splits > 1) {
+                            *reinterpret_cast<f32x4*>((float*)p.C + split * p.split_stride + (long)m * p.ldc + n) = a;
+                        } else {
+                            f32x4* cp = reinterpret_cast<f32x4*>((float*)p.C + (long)m * p.ldc + n);
+                            *cp = p.accumulate ? a + *cp : a;
+                        }
+                    } else {
+                        direct4(p, m, n, a, split);
+                        if (stats && m < p.M) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float t = bf2f(f2bf(a[e]));
+                                cs[e] += t;
+                                cq[e] += t * t;
+                            }
+                        }
+                    }
+                }
+            if (stats) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    cs[e] = row16_sum(cs[e]);
+                    cq[e] = row16_sum(cq[e]);
+                }
+                if (r16 == 0 && n < p.N) {
+                    float* row = p.colstats + (long)(tm * 2 + wm) * 2 * p.N;
+                    if (EK == EK_BF16) {
+                        *reinterpret_cast<f32x4*>(row + n) = (f32x4){cs[0], cs[1], cs[2], cs[3]};
+                        *reinterpret_cast<f32x4*>(row + p.N + n) = (f32x4){cq[0], cq[1], cq[2], cq[3]};
+                    } else {
+                        store4g(row + n, n + 3 < p.N, p.N - n, cs);
+                        store4g(row + p.N + n, n + 3 < p.N, p.N - n, cq);
+                    }
+                }
+            }
+        }
 }
 
 // DIRECT: epilogue from registers (direct4) and, with it, a persistent grid: a
@@ -594,24 +690,21 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         if (DIRECT) {
             const int vn = vt + gridDim.x;
             const bool next = vn < nwg;
-            const int m0c = m0, n0c = n0;
+            const int m0c = m0, n0c = n0, tm_c = tm;
             if (next) {
                 coords(vn);
                 sa.init(p, m0);
                 sb.init(p, n0);
                 if (nK > 0) prologueE();
             }
-            const int g4 = (lane >> 4) * 4, r16 = lane & 15;
-#pragma unroll
-            for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-                for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j)
-                            direct4(p, m0c + qm * 128 + wm * 64 + i * 16 + r16, n0c + qn * 128 + wn * 32 + j * 16 + g4,
-                                    acc[qm][qn][i][j], split);
+            // interior tiles take a lean variant (no bounds checks, one store per site);
+            // edge tiles and the rarer epilogue options the general one
+            if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_BF16)
+                epi_direct<EK_BF16>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+            else if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_F32)
+                epi_direct<EK_F32>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+            else
+                epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             if (!next) return;
             zero_acc();
             vt = vn;
@@ -709,8 +802,13 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 y += red[(ww * 256 + col) * 2 + 1];
             }
             if (n < p.N) {
-                p.colstats[(long)tm * 2 * p.N + n] = x;
-                p.colstats[(long)tm * 2 * p.N + p.N + n] = y;
+                // partial rows are per 128 output rows (the direct epilogue writes one
+                // per wave row): this tile's sums in row 2*tm, zeros in row 2*tm+1
+                float* row = p.colstats + (long)tm * 4 * p.N;
+                row[n] = x;
+                row[p.N + n] = y;
+                row[2 * p.N + n] = 0.f;
+                row[3 * p.N + n] = 0.f;
             }
         }
     }
@@ -788,7 +886,14 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // register epilogue + persistent grid when the epilogue is one direct4 covers
     // (split-K partials always: the reduce kernel applies the real epilogue)
     const bool direct = direct_enabled() &&
-        (splits > 1 || (!p.colstats && !p.row_remap && !p.res && (p.act == ACT_NONE || p.act == ACT_RELU)));
+        (splits > 1 || (!p.row_remap && !p.res && (p.act == ACT_NONE || p.act == ACT_RELU)));
+    if (splits > 1 || (p.out_f32 && !p.bias && p.act == ACT_NONE))
+        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_F32 : EK_GEN;
+    else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16))
+        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_BF16 : EK_GEN;
+    else
+        p.ek = EK_GEN;
+    kp.ek = p.ek;
     const int nwg = p.tiles_m * p.tiles_n;
     int gx = nwg;
     if (direct) {

@@ -398,10 +398,44 @@ DDL_API int ddl_bn_fwd_train(int dtype, const void* x, long M, int C, const void
 // Training-mode BN statistics from partial sums a GEMM epilogue already produced
 // (``part`` = [nblk][sum(C) | sumsq(C)], see gemm.hip / gemm_big.hip colstats):
 // the statistics read pass over the conv output disappears.
+// First level for many partial rows (a GEMM epilogue writes one per 128 output
+// rows: 6272 for a 56x56 layer at batch 256): blockIdx.y sums PC_ROWS rows of
+// every column (consecutive threads on consecutive columns, all PC_ROWS loads
+// in flight as 4 independent chains), so the finalize kernel reads nblk/PC_ROWS
+// rows instead of thousands.
+constexpr int PC_ROWS = 32;
+__global__ __launch_bounds__(256) void bn_partials_collapse_k(const float* __restrict__ part, int nblk, int width,
+                                                              float* __restrict__ out) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= width) return;
+    const int r0 = blockIdx.y * PC_ROWS;
+    const float* src = part + (long)r0 * width + col;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r0 + PC_ROWS <= nblk) {
+#pragma unroll
+        for (int r = 0; r < PC_ROWS; ++r) acc[r & 3] += src[(long)r * width];
+    } else {
+        for (int r = 0; r < nblk - r0; ++r) acc[r & 3] += src[(long)r * width];
+    }
+    out[(long)blockIdx.y * width + col] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
+DDL_API long ddl_bn_partials_ws(int nblk, int C) {
+    return nblk > 256 ? (long)((nblk + PC_ROWS - 1) / PC_ROWS) * 2 * C : 0;
+}
+
 DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, long M, int C, const void* gamma,
                                      const void* beta, float* running_mean, float* running_var, float momentum,
                                      float eps, float* save_mean, float* save_invstd, float* scale, float* shift,
-                                     hipStream_t st) {
+                                     float* ws, long ws_elems, hipStream_t st) {
+    const long need = ddl_bn_partials_ws(nblk, C);
+    if (need > 0) {
+        if (!ws || ws_elems < need) return -2;
+        const int chunks = (nblk + PC_ROWS - 1) / PC_ROWS;
+        bn_partials_collapse_k<<<dim3((2 * C + 255) / 256, chunks), 256, 0, st>>>(part, nblk, 2 * C, ws);
+        part = ws;
+        nblk = chunks;
+    }
     if (dtype == 1)
         bn_stats_finalize_k<bf16_t><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, (const bf16_t*)gamma,
             (const bf16_t*)beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);

@@ -110,7 +110,7 @@ _SIGS = {
     "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],
     "ddl_bn_eval_coeffs": [I, I, P, P, P, P, F, P, P, P],
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P, P],
-    "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P],
+    "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P, L],
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
     "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],

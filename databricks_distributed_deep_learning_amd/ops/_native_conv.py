@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import grad_ready, grad_sink
-from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm, stats_rows_max
+from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm, plan, stats_rows_max
 
 
 def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep=1, oa=0, ob=0):
@@ -29,6 +29,7 @@ def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, 
 
 
 STATS_MIN_K = int(os.environ.get("DDL_BN_STATS_MIN_K", "2048"))
+STATS_EPILOGUE = os.environ.get("DDL_BN_STATS_EPI", "1") != "0"   # 0: always a separate statistics pass
 _DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
 
@@ -42,16 +43,30 @@ def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
     M = N * P * Q
     part = None
-    # the statistics epilogue costs a cross-lane reduction per tile: it beats the
-    # separate read pass over y only when the tile's K loop is long (measured:
-    # scripts/debug/stats_overhead.py; +40 % on K=64 convs, break-even near K=1152)
-    if stats is not None and bias is None and act is None and residual is None and R * S * C >= STATS_MIN_K:
-        part = torch.empty(stats_rows_max(M) * 2 * K, dtype=torch.float32, device=x.device)
-    if R == 1 and S == 1 and stride == 1 and pad == 0:
-        r = gemm(MODE_NT, x, C, w, C, y, K, M, K, C, bias=bias, act=act, residual=residual, colstats=part)
+    kernel = None
+    plain11 = R == 1 and S == 1 and stride == 1 and pad == 0
+    desc = None if plain11 else _desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q)
+    if STATS_EPILOGUE and stats is not None and bias is None and act is None and residual is None and x.is_cuda:
+        # BatchNorm statistics from the GEMM epilogue instead of a separate read pass
+        # over y: nearly free in the 256x256 kernel's register epilogue (a 16-lane
+        # shuffle reduction per tile), so taken whenever that is this shape's tuned
+        # kernel; the 128-row kernels' LDS-staged statistics only pay off on long K
+        # loops (scripts/debug/stats_overhead.py: break-even near K=1152)
+        if R * S * C >= STATS_MIN_K:
+            use = True
+        elif plain11:
+            use = plan(MODE_NT, x, C, w, C, y, K, M, K, C) == "big"
+        else:
+            use = plan(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C, conv=desc) == "big"
+        if use:
+            part = torch.empty(stats_rows_max(M) * 2 * K, dtype=torch.float32, device=x.device)
+            kernel = None if R * S * C >= STATS_MIN_K else "big"
+    if plain11:
+        r = gemm(MODE_NT, x, C, w, C, y, K, M, K, C, bias=bias, act=act, residual=residual, colstats=part,
+                 kernel=kernel)
     else:
         r = gemm(MODE_CONV, x, 0, w, R * S * C, y, K, M, K, R * S * C, bias=bias, act=act, residual=residual,
-                 conv=_desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q), colstats=part)
+                 conv=desc, colstats=part, kernel=kernel)
     if part is not None:
         stats.set(y, part, r)
     return y

@@ -229,22 +229,9 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     return (timed[0][1], timed[0][2])
 
 
-def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
-         M: int, N: int, K: int, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
-         aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
-         conv: Optional[Sequence[int]] = None, row_remap: bool = False,
-         residual: Optional[torch.Tensor] = None, accumulate: bool = False,
-         kernel: Optional[str] = None, colstats: Optional[torch.Tensor] = None):
-    """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
-    "narrow" (128x64) or "tnarrow" (weight gradient computed transposed on 128x64 tiles).
-
-    ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm
-    statistics partials of the bf16 output; the function then returns the number of
-    partial rows written (one per M-tile).  Otherwise it returns ``C``.
-    """
-    conv_arr = None
-    if conv is not None:
-        conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
+def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap, residual,
+            kernel, colstats):
+    """(kernel kind, splits) for one GEMM call: forced, explicit, tuned (cached) or heuristic."""
     kernel = kernel or _forced
     if kernel is not None:
         if kernel == "big" and not _big_allowed(mode, K, lda, ldb):
@@ -278,13 +265,44 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
         choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
     if colstats is not None and (choice[1] != 1 or choice[0].startswith("t")):
         choice = ("big" if choice[0] == "big" else "small", 1)
+    return choice
+
+
+def plan(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
+         M: int, N: int, K: int, conv: Optional[Sequence[int]] = None) -> str:
+    """The kernel kind a plain call of this signature runs (tuning it now if needed)."""
+    conv_arr = None if conv is None else (ctypes.c_int * len(conv))(*[int(v) for v in conv])
+    return _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, None, None, None, None, conv, conv_arr, False, None,
+                   None, None)[0]
+
+
+def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
+         M: int, N: int, K: int, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
+         aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
+         conv: Optional[Sequence[int]] = None, row_remap: bool = False,
+         residual: Optional[torch.Tensor] = None, accumulate: bool = False,
+         kernel: Optional[str] = None, colstats: Optional[torch.Tensor] = None):
+    """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
+    "narrow" (128x64) or "tnarrow" (weight gradient computed transposed on 128x64 tiles).
+
+    ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm
+    statistics partials of the bf16 output; the function then returns the number of
+    partial rows written (one per M-tile).  Otherwise it returns ``C``.
+    """
+    conv_arr = None
+    if conv is not None:
+        conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
+    choice = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap,
+                     residual, kernel, colstats)
     _launch(choice[0], choice[1], mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
             residual, accumulate, colstats)
     if colstats is not None:
-        return -(-M // (256 if choice[0] == "big" else 128))
+        # one partial row per 128 output rows (256x256 tiles: one per wave row)
+        return 2 * -(-M // 256) if choice[0] == "big" else -(-M // 128)
     return C
 
 
 def stats_rows_max(M: int) -> int:
-    """Partial-row capacity a ``colstats`` buffer needs (the 128-row tiles' count)."""
-    return -(-M // 128)
+    """Partial-row capacity a ``colstats`` buffer needs: one row per 128 output rows
+    (128-row tiles), or two per 256-row tile of the large kernel."""
+    return max(-(-M // 128), 2 * -(-M // 256))

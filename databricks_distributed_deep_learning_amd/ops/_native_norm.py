@@ -27,8 +27,11 @@ class _BatchNormTrain(torch.autograd.Function):
         given = pre.take_for(x) if pre is not None else None
         if given is not None:                      # partials from the producing GEMM's epilogue
             part, nblk = given
+            # thousands of partial rows (one per 128 GEMM rows) are first collapsed 32:1
+            ws = torch.empty(-(-nblk // 32) * 2 * C, **f32) if nblk > 256 else None
             call("ddl_bn_fwd_from_partials", dt, p(part), nblk, M, C, p(weight), p(bias), p(running_mean),
-                 p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
+                 p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]),
+                 p(ws), 0 if ws is None else ws.numel())
         else:
             nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
             part = torch.empty(nblk * 2 * C, **f32)

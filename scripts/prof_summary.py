@@ -51,8 +51,20 @@ def main():
     ap.add_argument("--split", default=None)
     ap.add_argument("--names", nargs="*", default=["phase 1", "phase 2"])
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--after", default=None,
+                    help="NAME:COUNT -- drop every dispatch up to and including the COUNT-th one whose name "
+                         "contains NAME (e.g. sgd_k:3 skips 3 warm-up steps incl. the GEMM tuner's timing runs)")
     a = ap.parse_args()
     rows = load(a.db)
+    if a.after:
+        name, cnt = a.after.rsplit(":", 1)
+        seen = 0
+        for i, r in enumerate(rows):
+            if name in r[0]:
+                seen += 1
+                if seen == int(cnt):
+                    rows = rows[i + 1:]
+                    break
     phases = [rows]
     if a.split:
         idx = next((i for i, r in enumerate(rows) if a.split in r[0]), len(rows))

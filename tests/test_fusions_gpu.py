@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("kernel", ["big", "small", "narrow"])
 @pytest.mark.parametrize("N,H,C,K,R,stride", [(4, 20, 64, 64, 3, 1), (2, 17, 32, 256, 1, 1), (3, 15, 64, 256, 3, 2),
-                                              (8, 28, 128, 512, 1, 1)])
+                                              (8, 28, 128, 512, 1, 1), (32, 56, 64, 256, 1, 1),
+                                              (16, 30, 64, 128, 3, 1)])
 def test_bn_stats_from_gemm_epilogue(kernel, N, H, C, K, R, stride):
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd import ops
