@@ -547,6 +547,97 @@ __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ p
     }
 }
 
+// Vectorised split-K reduce: a thread owns 4 consecutive output elements along the
+// output's contiguous dimension (n, or m for the transposed store), 16-byte slab
+// loads when the slab dimension is contiguous, no 64-bit division per element.
+__global__ __launch_bounds__(256) void gemm_reduce4_k(const float* __restrict__ part, int splits, long split_stride,
+                                                      long ldw, int M, int N, long ldc, void* out, int out_f32,
+                                                      const void* bias, int bias_bf16, int act, void* aux,
+                                                      const bf16_t* __restrict__ res, int accumulate, int trans,
+                                                      FastDiv fd_w, int w4, int total4) {
+    // plain: i = m * (N/4) + n/4;   transposed: i = (m/4) * N + n
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+        const int row = (int)fdiv((uint32_t)i, fd_w);
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (!trans) {
+            // row = m, columns c4..c4+3 (consecutive threads: consecutive column groups)
+            const int c4 = (i - row * w4) * 4;
+            const float* src = part + (long)row * ldw + c4;
+            for (int s = 0; s < splits; ++s) {
+                const float4 t = *reinterpret_cast<const float4*>(src + s * split_stride);
+                v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+            }
+            const long o = (long)row * ldc + c4;
+            if (bias) {
+                float bv[4];
+                if (bias_bf16) load4((const bf16_t*)bias + c4, bv);
+                else load4((const float*)bias + c4, bv);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += bv[r];
+            }
+            if (res) {
+                float rv[4];
+                load4(res + o, rv);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += rv[r];
+            }
+            if (act == ACT_DGELU) {
+                float z[4];
+                load4((const bf16_t*)aux + o, z);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] *= gelu_erf_grad(z[r]);
+            } else if (act != ACT_NONE) {
+                if (aux) store4((bf16_t*)aux + o, v);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], act);
+            }
+            if (out_f32) {
+                if (accumulate) {
+                    float t[4];
+                    load4((const float*)out + o, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += t[r];
+                }
+                store4((float*)out + o, v);
+            } else {
+                if (accumulate) {
+                    float t[4];
+                    load4((const bf16_t*)out + o, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += t[r];
+                }
+                store4((bf16_t*)out + o, v);
+            }
+        } else {
+            // rows m = 4*row .. +3 of slab column n (consecutive threads: consecutive n, so
+            // the slab reads coalesce); stored as 4 consecutive elements of C^T row n
+            const int n = i - row * w4, m4 = row * 4;
+            const float* src = part + (long)m4 * ldw + n;
+            for (int s = 0; s < splits; ++s)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += src[s * split_stride + r * ldw];
+            const long o = (long)n * ldc + m4;
+            if (out_f32) {
+                if (accumulate) {
+                    float t[4];
+                    load4((const float*)out + o, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += t[r];
+                }
+                store4((float*)out + o, v);
+            } else {
+                if (accumulate) {
+                    float t[4];
+                    load4((const bf16_t*)out + o, t);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += t[r];
+                }
+                store4((bf16_t*)out + o, v);
+            }
+        }
+    }
+}
+
 template <int LA, int LB, int BNT = 128>
 int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t st) {
     p.tiles_m = (p.M + BM - 1) / BM;
@@ -574,10 +665,22 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
     hipLaunchKernelGGL((gemm_k<LA, LB, BNT>), grid, dim3(NT), 0, st, p);
     if (splits > 1) {
         const long total = (long)p.M * p.N;
-        const int g = (int)std::min<long>(8192, (total + 255) / 256);
-        gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out,
-                                          final_f32, p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final,
-                                          p.trans_out);
+        // 4 outputs per thread along the output's contiguous dimension (n; m for C^T)
+        const bool vec = (p.trans_out ? p.M % 4 == 0 : (p.N % 4 == 0 && p.ldw % 4 == 0 && p.split_stride % 4 == 0)) &&
+                         p.ldc % 4 == 0 && total < (1L << 31);
+        if (vec) {
+            const int w4 = p.trans_out ? p.N : p.N / 4;     // index divisor: i = row * w4 + col
+            const int total4 = (int)(total / 4);
+            const int g = std::min(8192, (total4 + 255) / 256);
+            gemm_reduce4_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out,
+                                               final_f32, p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final,
+                                               p.trans_out, make_fastdiv((uint32_t)w4), w4, total4);
+        } else {
+            const int g = (int)std::min<long>(8192, (total + 255) / 256);
+            gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out,
+                                              final_f32, p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final,
+                                              p.trans_out);
+        }
     }
     return (int)hipGetLastError();
 }

@@ -382,8 +382,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 // columns of one row, so a site is finished in registers and written with one
 // 8-byte (bf16) or 16-byte (fp32) store -- no LDS round trip, which is what lets
 // a persistent block restage the next tile's operands while this tile drains.
-// Covers bias / ReLU / accumulate / fp32 / split-K partial outputs; GELU, tanh,
-// dGELU, residual, row remap and BN statistics take the LDS-staged epilogue.
+// Covers bias / residual / ReLU / accumulate / fp32 / split-K partial outputs;
+// GELU, tanh, dGELU and row remap take the LDS-staged epilogue.
 __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const f32x4& a, int split) {
     if (m >= p.M || n >= p.N) return;
     const bool full = n + 3 < p.N;
@@ -399,6 +399,12 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
         else load4g((const float*)p.bias + n, full, nv, bv);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += bv[r];
+    }
+    if (p.res) {
+        float rv[4];
+        load4g(p.res + (long)m * p.ldc + n, full, nv, rv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += rv[r];
     }
     if (p.act == ACT_RELU) {
 #pragma unroll
@@ -428,7 +434,7 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
 // Register epilogue of one 256x256 tile.  Lane layout: acc[qm][qn][i][j] holds
 // row m0 + qm*128 + wm*64 + i*16 + (lane & 15), columns n0 + qn*128 + wn*32 +
 // j*16 + 4*(lane >> 4) .. +3.
-//   EK_BF16: interior tile, bf16 out, optional bf16 bias -- one 8-byte store a site
+//   EK_BF16: interior tile, bf16 out, optional bf16 bias / residual -- one 8-byte store a site
 //   EK_F32 : interior tile, fp32 split-K partial or fp32 out (+accumulate) -- one 16-byte store
 //   EK_GEN : anything direct4 covers, with bounds checks (edge tiles)
 // With colstats (EK_BF16 / EK_GEN) the BatchNorm statistics of the bf16 output --
@@ -454,8 +460,10 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                     const int m = m0 + qm * 128 + wm * 64 + i * 16 + r16;
                     const f32x4& a = acc[qm][qn][i][j];
                     if (EK == EK_BF16) {
-                        const uint32_t lo = pack2bf(a[0] + bv[0], a[1] + bv[1]);
-                        const uint32_t hi = pack2bf(a[2] + bv[2], a[3] + bv[3]);
+                        float rv[4] = {0.f, 0.f, 0.f, 0.f};
+                        if (p.res) load4(p.res + (long)m * p.ldc + n, rv);
+                        const uint32_t lo = pack2bf(a[0] + bv[0] + rv[0], a[1] + bv[1] + rv[1]);
+                        const uint32_t hi = pack2bf(a[2] + bv[2] + rv[2], a[3] + bv[3] + rv[3]);
                         *reinterpret_cast<uint2*>((bf16_t*)p.C + (long)m * p.ldc + n) = make_uint2(lo, hi);
                         if (stats) {
                             const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
@@ -886,10 +894,10 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // register epilogue + persistent grid when the epilogue is one direct4 covers
     // (split-K partials always: the reduce kernel applies the real epilogue)
     const bool direct = direct_enabled() &&
-        (splits > 1 || (!p.row_remap && !p.res && (p.act == ACT_NONE || p.act == ACT_RELU)));
+        (splits > 1 || (!p.row_remap && (p.act == ACT_NONE || p.act == ACT_RELU)));
     if (splits > 1 || (p.out_f32 && !p.bias && p.act == ACT_NONE))
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_F32 : EK_GEN;
-    else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16))
+    else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16) && !p.row_remap)
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_BF16 : EK_GEN;
     else
         p.ek = EK_GEN;

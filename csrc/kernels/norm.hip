@@ -32,8 +32,17 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_partial_k(const T* __restrict_
     float s[8], q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
-#pragma unroll 4
-    for (long r = r0 + rr; r < r1; r += rpi) {
+    long r = r0 + rr;
+    for (; r + 3 * rpi < r1; r += 4 * rpi) {   // 4 rows of 16-byte loads in flight
+        float v[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load8(x + (r + u * rpi) * C + cg * 8, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s[j] += v[u][j]; q[j] += v[u][j] * v[u][j]; }
+    }
+    for (; r < r1; r += rpi) {
         float v[8];
         load8(x + r * C + cg * 8, v);
 #pragma unroll
@@ -129,6 +138,63 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, const
     }
 }
 
+// Row-major variant of bn_apply for C / 8 dividing 256: a thread owns one
+// 8-channel group for the whole launch (coefficients loaded once, no per-element
+// channel modulo) and keeps 4 rows of 16-byte loads in flight.
+template <typename T, bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_rows_k(const T* __restrict__ x, const T* __restrict__ res,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       T* __restrict__ y, uint8_t* __restrict__ mask, long M, int C) {
+    const int tpr = C / 8, rpb = 256 / tpr;
+    const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
+    float sc[8], sh[8];
+    load8(scale + cg * 8, sc);
+    load8(shift + cg * 8, sh);
+    const long rs = (long)gridDim.x * rpb;
+    auto one = [&](const float* v, const float* r, long row) {
+        float o[8];
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float t = v[j] * sc[j] + sh[j];
+            if (RES) t += r[j];
+            if (RELU) {
+                // the bit must agree with the stored (rounded) output
+                t = fmaxf(t, 0.f);
+                bits |= (to_f(from_f<T>(t)) > 0.f ? 1u : 0u) << j;
+            }
+            o[j] = t;
+        }
+        store8(y + row * C + cg * 8, o);
+        if (RELU && mask) mask[row * tpr + cg] = (uint8_t)bits;
+    };
+    long r = (long)blockIdx.x * rpb + rr;
+    for (; r + 3 * rs < M; r += 4 * rs) {
+        float v[4][8], rv[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            load8(x + (r + u * rs) * C + cg * 8, v[u]);
+            if (RES) load8(res + (r + u * rs) * C + cg * 8, rv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) one(v[u], rv[u], r + u * rs);
+    }
+    for (; r < M; r += rs) {
+        float v[8], rv[8];
+        load8(x + r * C + cg * 8, v);
+        if (RES) load8(res + r * C + cg * 8, rv);
+        one(v, rv, r);
+    }
+}
+
+// blocks for the row-major passes: ~8 blocks of 256 threads per CU, each thread
+// looping over rows
+static int rows_grid(long M, int C) {
+    const long rpb = 256 / (C / 8);
+    return (int)std::max<long>(1, std::min<long>(2048, (M + rpb - 1) / rpb));
+}
+static bool rows_ok(int C) { return C % 8 == 0 && 256 % (C / 8) == 0; }
+
 // ------------------------------------------------------------------ BN backward
 template <typename T, bool RELU>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
@@ -218,6 +284,64 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ dy, 
         }
         store8(dx + i * 8, o);
         if (DRES) store8(dres + i * 8, dz);
+    }
+}
+
+// Row-major backward apply (C / 8 dividing 256): per-thread channel group, the
+// five per-channel coefficients folded once into dx = A*dz + B*x + D.
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(256) void bn_bwd_apply_rows_k(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                           const T* __restrict__ x, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef, T* __restrict__ dx,
+                                                           T* __restrict__ dres, long M, int C) {
+    const int tpr = C / 8, rpb = 256 / tpr;
+    const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
+    float A[8], B[8], D[8];
+    {
+        float mu[8], is[8], k1[8], mb[8], mg[8];
+        load8(mean + cg * 8, mu);
+        load8(invstd + cg * 8, is);
+        load8(coef + cg * 8, k1);
+        load8(coef + C + cg * 8, mb);
+        load8(coef + 2 * C + cg * 8, mg);
+        // dx = k1 * (dz - mb - (x - mu) * is * mg)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            A[j] = k1[j];
+            B[j] = -k1[j] * is[j] * mg[j];
+            D[j] = k1[j] * (mu[j] * is[j] * mg[j] - mb[j]);
+        }
+    }
+    const long rs = (long)gridDim.x * rpb;
+    auto one = [&](const float* g, const float* xv, uint32_t bits, long row) {
+        float o[8], dz[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dz[j] = ((bits >> j) & 1u) ? g[j] : 0.f;
+            o[j] = A[j] * dz[j] + B[j] * xv[j] + D[j];
+        }
+        store8(dx + row * C + cg * 8, o);
+        if (DRES) store8(dres + row * C + cg * 8, dz);
+    };
+    long r = (long)blockIdx.x * rpb + rr;
+    for (; r + 3 * rs < M; r += 4 * rs) {
+        float g[4][8], xv[4][8];
+        uint32_t bits[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            load8(dy + (r + u * rs) * C + cg * 8, g[u]);
+            load8(x + (r + u * rs) * C + cg * 8, xv[u]);
+            bits[u] = RELU ? mask[(r + u * rs) * tpr + cg] : 0xffu;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) one(g[u], xv[u], bits[u], r + u * rs);
+    }
+    for (; r < M; r += rs) {
+        float g[8], xv[8];
+        load8(dy + r * C + cg * 8, g);
+        load8(x + r * C + cg * 8, xv);
+        one(g, xv, RELU ? mask[r * tpr + cg] : 0xffu, r);
     }
 }
 
@@ -369,6 +493,13 @@ inline int grid_for(long n, int nt = 256, int cap = 4096) {
 // =================================================================== C ABI
 // dtype codes: 0 = fp32, 1 = bf16
 
+// backward partial pass: two input streams per row, 4 blocks per CU in flight
+DDL_API int ddl_bn_bwd_nblk(long M, int C) {
+    const int rpi = BN_NT / (C / 8);
+    long nblk = std::min<long>(1024, (M + rpi * 8 - 1) / (rpi * 8));
+    return (int)std::max<long>(1, nblk);
+}
+
 DDL_API int ddl_bn_stats_nblk(long M, int C) {
     const int rpi = BN_NT / (C / 8);
     long nblk = std::min<long>(512, (M + rpi * 8 - 1) / (rpi * 8));
@@ -459,6 +590,18 @@ DDL_API int ddl_bn_eval_coeffs(int dtype, int C, const void* gamma, const void* 
 template <typename T>
 static void bn_apply_dispatch(const T* x, const T* res, const float* sc, const float* sh, T* y, uint8_t* mask, long n,
                               int C, int relu, hipStream_t st) {
+    if (rows_ok(C) && n % C == 0) {
+        const long M = n / C;
+        const int gr = rows_grid(M, C);
+        if (res) {
+            if (relu) bn_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
+            else bn_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
+        } else {
+            if (relu) bn_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
+            else bn_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
+        }
+        return;
+    }
     const long n8 = n / 8;
     const int g = grid_for(n8, 256, 8192);
     if (res) {
@@ -483,13 +626,24 @@ template <typename T>
 static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const float* mean, const float* invstd,
                             const T* gamma, long M, int C, int relu, float* part, T* dgamma, T* dbeta, float* coef,
                             T* dx, T* dres, int acc, hipStream_t st) {
-    const int nblk = ddl_bn_stats_nblk(M, C);
+    const int nblk = ddl_bn_bwd_nblk(M, C);
     const int rpi = BN_NT / (C / 8);
     long rpb = (M + nblk - 1) / nblk;
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
+    if (rows_ok(C)) {
+        const int gr = rows_grid(M, C);
+        if (relu) {
+            if (dres) bn_bwd_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
+            else bn_bwd_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
+        } else {
+            if (dres) bn_bwd_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
+            else bn_bwd_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
+        }
+        return;
+    }
     const long n8 = M * C / 8;
     const int g = grid_for(n8, 256, 8192);
     if (relu) {

@@ -107,6 +107,7 @@ P, I, L, F, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, 
 _SIGS = {
     # norm.hip
     "ddl_bn_stats_nblk": [L, I],
+    "ddl_bn_bwd_nblk": [L, I],
     "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],
     "ddl_bn_eval_coeffs": [I, I, P, P, P, P, F, P, P, P],
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P, P],

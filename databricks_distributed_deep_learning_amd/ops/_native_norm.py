@@ -54,7 +54,7 @@ class _BatchNormTrain(torch.autograd.Function):
         dy = dy.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
-        nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
+        nblk = _lib.fn("ddl_bn_bwd_nblk")(M, C)
         f32 = dict(dtype=torch.float32, device=x.device)
         part = torch.empty(nblk * 2 * C, **f32)
         coef = torch.empty(3 * C, **f32)

@@ -204,7 +204,7 @@ def test_strided_dgrad_class_paths(path, N, H, W, C, K, R, pad):
 
 
 @pytest.mark.parametrize("M,N,K", [(8292, 2304, 136), (4100, 4200, 768), (520, 264, 1024)])
-@pytest.mark.parametrize("variant", ["plain", "bias_bf16_relu", "bias_f32", "acc_f32", "acc_bf16"])
+@pytest.mark.parametrize("variant", ["plain", "bias_bf16_relu", "bias_f32", "acc_f32", "acc_bf16", "residual"])
 def test_big_direct_persistent_epilogue(M, N, K, variant):
     """Register epilogue + persistent grid of the 256x256 kernel (> 256 tiles: blocks
     walk several tiles, the next tile's prologue overlaps this tile's stores)."""
@@ -227,6 +227,10 @@ def test_big_direct_persistent_epilogue(M, N, K, variant):
     elif variant.startswith("acc"):
         out_dtype = torch.float32 if variant == "acc_f32" else torch.bfloat16
         kw = dict(accumulate=True)
+    elif variant == "residual":
+        r = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        kw = dict(residual=r)
+        ref = ref + r.float()
     c = torch.randn(M, N, device=dev).to(out_dtype)
     if variant.startswith("acc"):
         ref = ref + c.float()
