@@ -118,14 +118,22 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
     return cdf + x * pdf;
 }
 
-// Counter-based hash RNG (splitmix/murmur finaliser): uniform in [0,1) from
-// (seed, index) so dropout masks are regenerated in backward, never stored.
+// Counter-based hash RNG: uniform 32-bit value from (seed, index) so dropout
+// masks are regenerated in backward, never stored.  Two rounds of the
+// "lowbias32" integer finaliser (xor-shift / 32-bit multiply): ~12 VALU ops per
+// element, cheap enough to recompute inside bandwidth-bound kernels (LayerNorm
+// backward) where a 64-bit-multiply hash was VALU-bound.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-    uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xBF58476D1CE4E5B9ull + 0x94D049BB133111EBull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (uint32_t)(z >> 32);
+    const uint32_t a = lowbias32((uint32_t)idx ^ (uint32_t)seed);
+    return lowbias32(a + (uint32_t)(idx >> 32) * 0x9E3779B9u + (uint32_t)(seed >> 32));
 }
 __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
     return hash_u32(seed, idx) >= thresh;   // P(keep) = 1 - thresh / 2^32

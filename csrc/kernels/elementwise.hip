@@ -299,6 +299,14 @@ __global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ x, T
 }  // namespace
 
 // =================================================================== C ABI
+// dst (bf16 / fp32) += src (fp32): folds an fp32 side-channel result (e.g. the bias
+// gradient a LayerNorm backward summed) into a parameter-gradient slot in one launch
+template <typename T>
+__global__ __launch_bounds__(256) void acc_f32_k(T* __restrict__ dst, const float* __restrict__ src, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        dst[i] = from_f<T>(to_f(dst[i]) + src[i]);
+}
+
 #define DISPATCH_T(dtype, KERNEL_CALL_BF16, KERNEL_CALL_F32) \
     do { if ((dtype) == 1) { KERNEL_CALL_BF16; } else { KERNEL_CALL_F32; } } while (0)
 
@@ -463,5 +471,12 @@ DDL_API int ddl_conv_w_dgrad(const void* w, void* out, int K, int R, int S, int 
     for (int i = 0; i < Sp; ++i) tm.s[i] = smap[i];
     const long total = (long)C * Rp * Sp * K;
     conv_w_dgrad_k<<<grid_for(total), 256, 0, st>>>((const bf16_t*)w, (bf16_t*)out, K, R, S, C, Rp, Sp, tm);
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_acc_f32(int dtype, void* dst, const float* src, long n, hipStream_t st) {
+    const int g = (int)std::min<long>(1024, (n + 255) / 256);
+    DISPATCH_T(dtype, (acc_f32_k<bf16_t><<<g, 256, 0, st>>>((bf16_t*)dst, src, n)),
+               (acc_f32_k<float><<<g, 256, 0, st>>>((float*)dst, src, n)));
     DDL_RETURN_LAUNCH();
 }

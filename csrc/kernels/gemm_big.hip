@@ -85,7 +85,7 @@ struct BigParams {
     int tiles_m, tiles_n;
     int ek;                   // register-epilogue variant (EK_*), set by the launcher
 };
-enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2 };
+enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3 };
 
 __device__ __forceinline__ int half_off(int buf, int x, int h) { return ((buf * 2 + x) * 2 + h) * HALF; }
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -382,8 +382,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 // columns of one row, so a site is finished in registers and written with one
 // 8-byte (bf16) or 16-byte (fp32) store -- no LDS round trip, which is what lets
 // a persistent block restage the next tile's operands while this tile drains.
-// Covers bias / residual / ReLU / accumulate / fp32 / split-K partial outputs;
-// GELU, tanh, dGELU and row remap take the LDS-staged epilogue.
+// Covers bias / residual / ReLU / GELU (+pre-activation) / accumulate / fp32 /
+// split-K partial outputs; tanh, dGELU and row remap take the LDS-staged epilogue.
 __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const f32x4& a, int split) {
     if (m >= p.M || n >= p.N) return;
     const bool full = n + 3 < p.N;
@@ -409,6 +409,10 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
     if (p.act == ACT_RELU) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    } else if (p.act == ACT_GELU) {
+        if (p.aux) store4g(p.aux + (long)m * p.ldc + n, full, nv, v);   // pre-activation for the backward
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
     }
     if (p.out_f32) {
         float* cp = (float*)p.C + (long)m * p.ldc + n;
@@ -435,6 +439,7 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
 // row m0 + qm*128 + wm*64 + i*16 + (lane & 15), columns n0 + qn*128 + wn*32 +
 // j*16 + 4*(lane >> 4) .. +3.
 //   EK_BF16: interior tile, bf16 out, optional bf16 bias / residual -- one 8-byte store a site
+//   EK_GELU: interior tile, bf16 out = GELU(acc + bf16 bias), pre-activation to aux
 //   EK_F32 : interior tile, fp32 split-K partial or fp32 out (+accumulate) -- one 16-byte store
 //   EK_GEN : anything direct4 covers, with bounds checks (edge tiles)
 // With colstats (EK_BF16 / EK_GEN) the BatchNorm statistics of the bf16 output --
@@ -444,14 +449,14 @@ template <int EK>
 __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
                                            int wm, int wn, int lane, int split) {
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
-    const bool stats = EK != EK_F32 && p.colstats;
+    const bool stats = (EK == EK_BF16 || EK == EK_GEN) && p.colstats;
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int n = n0 + qn * 128 + wn * 32 + j * 16 + g4;
             float bv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (EK == EK_BF16 && p.bias) load4((const bf16_t*)p.bias + n, bv);
+            if ((EK == EK_BF16 || EK == EK_GELU) && p.bias) load4((const bf16_t*)p.bias + n, bv);
             float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int qm = 0; qm < 2; ++qm)
@@ -474,6 +479,14 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                                 cq[e] += t[e] * t[e];
                             }
                         }
+                    } else if (EK == EK_GELU) {
+                        // z = acc + bias kept for the backward (aux), y = GELU(z)
+                        float z[4] = {a[0] + bv[0], a[1] + bv[1], a[2] + bv[2], a[3] + bv[3]};
+                        const long o = (long)m * p.ldc + n;
+                        if (p.aux)
+                            *reinterpret_cast<uint2*>(p.aux + o) = make_uint2(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]));
+                        *reinterpret_cast<uint2*>((bf16_t*)p.C + o) =
+                            make_uint2(pack2bf(gelu_erf(z[0]), gelu_erf(z[1])), pack2bf(gelu_erf(z[2]), gelu_erf(z[3])));
                     } else if (EK == EK_F32) {
                         if (p.splits > 1) {
                             *reinterpret_cast<f32x4*>((float*)p.C + split * p.split_stride + (long)m * p.ldc + n) = a;
@@ -711,6 +724,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 epi_direct<EK_BF16>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_F32)
                 epi_direct<EK_F32>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+            else if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_GELU)
+                epi_direct<EK_GELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else
                 epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             if (!next) return;
@@ -894,11 +909,13 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // register epilogue + persistent grid when the epilogue is one direct4 covers
     // (split-K partials always: the reduce kernel applies the real epilogue)
     const bool direct = direct_enabled() &&
-        (splits > 1 || (!p.row_remap && (p.act == ACT_NONE || p.act == ACT_RELU)));
+        (splits > 1 || (!p.row_remap && (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU)));
     if (splits > 1 || (p.out_f32 && !p.bias && p.act == ACT_NONE))
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_F32 : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16) && !p.row_remap)
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_BF16 : EK_GEN;
+    else if (!p.out_f32 && !p.accumulate && p.act == ACT_GELU && (!p.bias || p.bias_bf16) && !p.row_remap && !p.res)
+        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_GELU : EK_GEN;
     else
         p.ek = EK_GEN;
     kp.ek = p.ek;

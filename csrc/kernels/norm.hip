@@ -349,11 +349,26 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_k(const T* __restrict__
 // One wave per row; each lane owns VPL = H/256 chunks of 4 contiguous elements
 // (lane chunk k covers columns 256*k + 4*lane .. +3): every load is 8 B/lane,
 // fully coalesced per wave.
+// Dropout fused on the LayerNorm's main input: y = LN(dropout(x) + res).  The keep
+// mask is the counter hash of (seed, flat element index), regenerated in the
+// backward, which writes the residual gradient g and the x gradient g*mask/(1-p)
+// (and the column sums of the latter: the producing Linear's bias gradient).
+struct Drop {
+    uint64_t seed;
+    uint32_t thresh;   // 0: no dropout
+    float scale;       // 1 / (1 - p)
+    void* dres;        // backward: residual gradient (unmasked), only with dropout
+};
+__device__ __forceinline__ void drop4(const Drop& d, long idx, float* v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = keep_elem(d.seed, (uint64_t)(idx + j), d.thresh) ? v[j] * d.scale : 0.f;
+}
+
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T* __restrict__ res, long res_rows,
                                                 const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
                                                 float* __restrict__ save_mean, float* __restrict__ save_rstd, long rows,
-                                                int H, float eps) {
+                                                int H, float eps, Drop drop) {
     const int lane = threadIdx.x & 63;
     const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -363,6 +378,7 @@ __global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T
     for (int k = 0; k < VPL; ++k) {
         const int col = 256 * k + 4 * lane;
         load4(x + row * H + col, v[k]);
+        if (drop.thresh) drop4(drop, row * H + col, v[k]);
         if (res) {
             float r[4];
             load4(res + (row % res_rows) * H + col, r);
@@ -398,7 +414,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
                                                 const T* __restrict__ res, long res_rows, const T* __restrict__ gamma,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 T* __restrict__ dx, float* __restrict__ part, long rows, int H,
-                                                int rows_per_blk, int dxsum) {
+                                                int rows_per_blk, int dxsum, Drop drop) {
     // part row per block: [dgamma(H) | dbeta(H) | (dxsum) sum of dx (H)] -- the last is the
     // bias gradient of the Linear that produced this LayerNorm's input
     __shared__ float s_acc[3][4][VPL * 256];
@@ -412,43 +428,68 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
     }
     const long r0 = (long)blockIdx.x * rows_per_blk;
     const long r1 = min(rows, r0 + rows_per_blk);
-    for (long row = r0 + w; row < r1; row += 4) {
+    // raw loads of one row: input (x, plus residual) and dy
+    auto load_row = [&](long row, float (&xv)[VPL][4], float (&d)[VPL][4]) {
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+            const int col = 256 * k + 4 * lane;
+            load4(x + row * H + col, xv[k]);
+            load4(dy + row * H + col, d[k]);
+        }
+        if (res) {
+#pragma unroll
+            for (int k = 0; k < VPL; ++k) {
+                float r[4];
+                load4(res + (row % res_rows) * H + 256 * k + 4 * lane, r);
+                if (drop.thresh) drop4(drop, row * H + 256 * k + 4 * lane, xv[k]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) xv[k][j] += r[j];
+            }
+        } else if (drop.thresh) {
+#pragma unroll
+            for (int k = 0; k < VPL; ++k) drop4(drop, row * H + 256 * k + 4 * lane, xv[k]);
+        }
+    };
+    auto finish_row = [&](long row, const float (&xv)[VPL][4], const float (&d)[VPL][4]) {
         const float mu = mean[row], rs = rstd[row];
         float xh[VPL][4], gy[VPL][4];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < VPL; ++k) {
-            const int col = 256 * k + 4 * lane;
-            float xv[4], d[4];
-            load4(x + row * H + col, xv);
-            if (res) {
-                float r[4];
-                load4(res + (row % res_rows) * H + col, r);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) xv[j] += r[j];
-            }
-            load4(dy + row * H + col, d);
+        for (int k = 0; k < VPL; ++k)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                xh[k][j] = (xv[j] - mu) * rs;
-                gy[k][j] = d[j] * g[k][j];
+                xh[k][j] = (xv[k][j] - mu) * rs;
+                gy[k][j] = d[k][j] * g[k][j];
                 s1 += gy[k][j];
                 s2 += gy[k][j] * xh[k][j];
-                dg[k][j] += d[j] * xh[k][j];
-                db[k][j] += d[j];
+                dg[k][j] += d[k][j] * xh[k][j];
+                db[k][j] += d[k][j];
             }
-        }
         const float m1 = wave_sum(s1) / H, m2 = wave_sum(s2) / H;
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
             float o[4];
+            const long idx = row * H + 256 * k + 4 * lane;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
-                ds[k][j] += to_f(from_f<T>(o[j]));       // sum of the stored (rounded) dx
+            for (int j = 0; j < 4; ++j) o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
+            if (drop.thresh) {
+                store4((T*)drop.dres + idx, o);      // residual gradient: unmasked
+                drop4(drop, idx, o);                 // x gradient: through the dropout mask
             }
-            store4(dx + row * H + 256 * k + 4 * lane, o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ds[k][j] += to_f(from_f<T>(o[j]));   // sum of the stored (rounded) dx
+            store4(dx + idx, o);
         }
+    };
+    // two rows per wave per iteration: the second row's loads are in flight while
+    // the first row's reductions run
+    for (long row = r0 + w; row < r1; row += 8) {
+        const bool two = row + 4 < r1;   // wave-uniform
+        float xa[VPL][4], da[VPL][4], xb[VPL][4], dbv[VPL][4];
+        load_row(row, xa, da);
+        if (two) load_row(row + 4, xb, dbv);
+        finish_row(row, xa, da);
+        if (two) finish_row(row + 4, xb, dbv);
     }
 #pragma unroll
     for (int k = 0; k < VPL; ++k)
@@ -551,6 +592,19 @@ __global__ __launch_bounds__(256) void bn_partials_collapse_k(const float* __res
     out[(long)blockIdx.y * width + col] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
+// Partial rows beyond this are first collapsed 32:1 (a single finalize block per
+// 64 columns is too little parallelism for ~1000 rows).  The caller allocates
+// `part` with room for the collapsed rows behind the nblk partial rows.
+constexpr int COLLAPSE_OVER = 64;
+static const float* collapse_partials(const float* part, int& nblk, int width, hipStream_t st) {
+    if (nblk <= COLLAPSE_OVER) return part;
+    float* ws = const_cast<float*>(part) + (long)nblk * width;
+    const int chunks = (nblk + PC_ROWS - 1) / PC_ROWS;
+    bn_partials_collapse_k<<<dim3((width + 255) / 256, chunks), 256, 0, st>>>(part, nblk, width, ws);
+    nblk = chunks;
+    return ws;
+}
+
 DDL_API long ddl_bn_partials_ws(int nblk, int C) {
     return nblk > 256 ? (long)((nblk + PC_ROWS - 1) / PC_ROWS) * 2 * C : 0;
 }
@@ -632,7 +686,9 @@ static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const 
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
-    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(part, nblk, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
+    int nrows = nblk;
+    const float* fin = collapse_partials(part, nrows, 2 * C, st);
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(fin, nrows, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
     if (rows_ok(C)) {
         const int gr = rows_grid(M, C);
         if (relu) {
@@ -655,7 +711,8 @@ static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const 
     }
 }
 
-// relu: `mask` is the bit mask written by ddl_bn_apply (required when relu != 0)
+// relu: `mask` is the bit mask written by ddl_bn_apply (required when relu != 0);
+// part: (nblk + ceil(nblk/32)) * 2C floats, nblk = ddl_bn_bwd_nblk(M, C)
 DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* mask, const void* x, const float* mean,
                        const float* invstd, const void* gamma, long M, int C, int relu, float* part, void* dgamma,
                        void* dbeta, float* coef, void* dx, void* dres, int acc_params, hipStream_t st) {
@@ -673,16 +730,16 @@ DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* mask, const void* 
 // ---------------------------------------------------------------- LayerNorm
 template <typename T>
 static int ln_fwd_dispatch(const T* x, const T* res, long res_rows, const T* g, const T* b, T* y, float* mean,
-                           float* rstd, long rows, int H, float eps, hipStream_t st) {
+                           float* rstd, long rows, int H, float eps, Drop drop, hipStream_t st) {
     const int grid = (int)((rows + 3) / 4);
     switch (H / 256) {
-        case 1: ln_fwd_k<T, 1><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
-        case 2: ln_fwd_k<T, 2><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
-        case 3: ln_fwd_k<T, 3><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
-        case 4: ln_fwd_k<T, 4><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
-        case 5: ln_fwd_k<T, 5><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
-        case 6: ln_fwd_k<T, 6><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
-        case 8: ln_fwd_k<T, 8><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps); break;
+        case 1: ln_fwd_k<T, 1><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
+        case 2: ln_fwd_k<T, 2><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
+        case 3: ln_fwd_k<T, 3><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
+        case 4: ln_fwd_k<T, 4><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
+        case 5: ln_fwd_k<T, 5><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
+        case 6: ln_fwd_k<T, 6><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
+        case 8: ln_fwd_k<T, 8><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
         default: return -1;
     }
     return 0;
@@ -693,14 +750,28 @@ DDL_API int ddl_ln_supported(int H) {
     return (H % 256 == 0) && (v >= 1 && v <= 8 && v != 7);
 }
 
+static Drop make_drop(unsigned long long seed, float p, void* dres) {
+    Drop d{};
+    if (p > 0.f) {
+        d.seed = seed;
+        d.thresh = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+        d.scale = 1.f / (1.f - p);
+        d.dres = dres;
+    }
+    return d;
+}
+
+// drop_p > 0: y = LN(dropout(x) + res) with the hash mask of drop_seed
 DDL_API int ddl_ln_fwd(int dtype, const void* x, const void* res, long res_rows, const void* g, const void* b, void* y,
-                       float* mean, float* rstd, long rows, int H, float eps, hipStream_t st) {
+                       float* mean, float* rstd, long rows, int H, float eps, unsigned long long drop_seed,
+                       float drop_p, hipStream_t st) {
     if (!ddl_ln_supported(H)) return -1;
     if (res_rows <= 0) res_rows = rows;
+    const Drop drop = make_drop(drop_seed, drop_p, nullptr);
     int rc = dtype == 1 ? ln_fwd_dispatch((const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
-                                          (const bf16_t*)b, (bf16_t*)y, mean, rstd, rows, H, eps, st)
+                                          (const bf16_t*)b, (bf16_t*)y, mean, rstd, rows, H, eps, drop, st)
                         : ln_fwd_dispatch((const float*)x, (const float*)res, res_rows, (const float*)g,
-                                          (const float*)b, (float*)y, mean, rstd, rows, H, eps, st);
+                                          (const float*)b, (float*)y, mean, rstd, rows, H, eps, drop, st);
     if (rc) return rc;
     DDL_RETURN_LAUNCH();
 }
@@ -710,35 +781,44 @@ DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
                            const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, int acc,
-                           float* dxsum, hipStream_t st) {
+                           float* dxsum, Drop drop, hipStream_t st) {
     const int nblk = ddl_ln_bwd_nblk(rows);
     const int rpb = (int)((rows + nblk - 1) / nblk);
     switch (H / 256) {
-        case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
-        case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
-        case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
-        case 4: ln_bwd_k<T, 4><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
-        case 5: ln_bwd_k<T, 5><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
-        case 6: ln_bwd_k<T, 6><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
-        case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr); break;
+        case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 4: ln_bwd_k<T, 4><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 5: ln_bwd_k<T, 5><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 6: ln_bwd_k<T, 6><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         default: return -1;
     }
-    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(part, nblk, H, dg, db, acc, dxsum);
+    int nrows = nblk;
+    const float* fin = collapse_partials(part, nrows, (dxsum ? 3 : 2) * H, st);
+    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(fin, nrows, H, dg, db, acc, dxsum);
     return 0;
 }
 
-// part: nblk * (dxsum ? 3 : 2) * H floats; dxsum (nullable, fp32 [H]) receives the
+// part: (nblk + ceil(nblk/32)) * (dxsum ? 3 : 2) * H floats (partial rows + their
+// collapse); dxsum (nullable, fp32 [H]) receives the
 // column sums of dx -- the bias gradient of the Linear feeding this LayerNorm
+// drop_p > 0: dx = gradient of x through the dropout mask, dres (required) = the
+// unmasked gradient of (dropout(x) + res); dxsum then sums the masked dx
 DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res, long res_rows, const void* g,
                        const float* mean, const float* rstd, void* dx, float* part, void* dg, void* db, long rows, int H,
-                       int acc_params, float* dxsum, hipStream_t st) {
+                       int acc_params, float* dxsum, unsigned long long drop_seed, float drop_p, void* dres,
+                       hipStream_t st) {
     if (!ddl_ln_supported(H)) return -1;
     if (res_rows <= 0) res_rows = rows;
+    if (drop_p > 0.f && (!dres || res_rows != rows)) return -2;
+    const Drop drop = make_drop(drop_seed, drop_p, dres);
     int rc = dtype == 1
                  ? ln_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
-                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, dxsum, st)
+                                   mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, dxsum,
+                                   drop, st)
                  : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
-                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum, st);
+                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum, drop, st);
     if (rc) return rc;
     DDL_RETURN_LAUNCH();
 }

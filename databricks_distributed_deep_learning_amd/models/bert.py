@@ -18,7 +18,12 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops.bridge import GradBridge
 from .layers import Dropout, Embedding, LayerNorm, Linear
+
+
+def _bridge(h: torch.Tensor):
+    return GradBridge() if (torch.is_grad_enabled() and h.requires_grad) else None
 
 
 @dataclass
@@ -86,12 +91,16 @@ class BertLayer(nn.Module):
             nn.init.zeros_(lin.bias)
 
     def forward(self, h, mask: Optional[torch.Tensor] = None):
-        qkv = self.qkv(h)
+        # hidden dropout fused into the post-LN kernels: LN(dropout(sublayer) + h); each
+        # residual gradient is bridged into the dgrad epilogue of the Linear that also
+        # reads h (qkv / ffn_in) instead of an autograd add
+        br1, br2 = _bridge(h), None
+        qkv = self.qkv(h, grad_residual=br1)
         ctx = ops.attention(qkv, self.num_heads, mask, self.attn_dropout, self.training)
-        a = self.dropout(self.attn_out(ctx))
-        h = self.attn_ln(a, residual=h)
-        f = self.dropout(self.ffn_out(self.ffn_in(h)))
-        return self.ffn_ln(f, residual=h)
+        h = self.attn_ln(self.attn_out(ctx), residual=h, dropout=self.dropout.p, residual_grad_to=br1)
+        br2 = _bridge(h)
+        f = self.ffn_out(self.ffn_in(h, grad_residual=br2))
+        return self.ffn_ln(f, residual=h, dropout=self.dropout.p, residual_grad_to=br2)
 
 
 class BertModel(nn.Module):

@@ -114,12 +114,13 @@ _SIGS = {
     "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P, L],
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
+    "ddl_acc_f32": [I, P, P, L, P],
     "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],
     "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_ln_supported": [I],
-    "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, P],
+    "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, U64, F, P],
     "ddl_ln_bwd_nblk": [L],
-    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P, P],
+    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P, U64, F, P, P],
     # elementwise.hip
     "ddl_gelu_fwd": [I, P, P, L, P],
     "ddl_gelu_bwd": [I, P, P, P, L, P],

@@ -31,10 +31,25 @@ def _ok(x, w) -> bool:
 _DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
 
+def _transposed(param, w: torch.Tensor) -> torch.Tensor:
+    """W^T for the NT dgrad, cached on the parameter until the weights change (the
+    optimizer's in-place update bumps the shared version counter): one transpose per
+    optimizer step instead of one per backward."""
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    c = getattr(param, "_ddl_wt", None) if param is not None else None
+    if c is not None and c[0] == key:
+        return c[1]
+    wt = w.t().contiguous()
+    if param is not None:
+        param._ddl_wt = (key, wt)
+    return wt
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act):
+    def forward(ctx, x, w, b, act, bridge=None):
         ctx.w_param, ctx.b_param = w, b
+        ctx.bridge = bridge
         K = x.shape[-1]
         N = w.shape[0]
         x2 = x.reshape(-1, K)
@@ -89,14 +104,22 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
+            # a residual branch's gradient handed over by the LayerNorm backward: summed
+            # in the dgrad epilogue (one extra read instead of an autograd add kernel)
+            res = ctx.bridge.take() if ctx.bridge is not None else None
+            if res is not None:
+                res = res.reshape(M, K)
+                if not res.is_contiguous() or res.dtype != dx.dtype:
+                    res = res.contiguous().to(dx.dtype)
             if _DGRAD_NT and M >= 4 * K:
                 # dx = dz W as an NT GEMM against W^T (both operands k-contiguous: ds_read_b128
                 # fragments instead of transposed reads); the weight copy is tiny next to dz
-                wt = w.t().contiguous()
-                gemm(MODE_NT, dz, N, wt, N, dx, K, M, K, N)
+                gemm(MODE_NT, dz, N, _transposed(ctx.w_param, w), N, dx, K, M, K, N, residual=res)
             else:
-                gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N)
+                gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N, residual=res)
             dx = dx.view(ctx.xshape)
+        elif ctx.bridge is not None:
+            ctx.bridge.take()
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
             if sink is not None:       # accumulate straight into the reducer's gradient arena
@@ -114,7 +137,7 @@ class _Linear(torch.autograd.Function):
             pre = pre[0] if (pre is not None and pre[1] == dy._version) else None
             if pre is not None and pre.numel() == N:
                 if sink is not None:
-                    sink.add_(pre)
+                    call("ddl_acc_f32", dcode(sink), p(sink), p(pre), N)
                     grad_ready(ctx.b_param)
                 else:
                     db = pre.to(w.dtype)
@@ -124,11 +147,13 @@ class _Linear(torch.autograd.Function):
             else:
                 db = torch.empty(N, dtype=w.dtype, device=w.device)
                 E.colsum(dz, db)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str]) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str],
+           bridge=None) -> torch.Tensor:
     if not _ok(x, w) or (b is not None and b.dtype != w.dtype):
+        from .bridge import join
         from .linear import linear_reference
-        return linear_reference(x, w, b, act)
-    return _Linear.apply(x, w, b, act)
+        return linear_reference(join(x, bridge), w, b, act)
+    return _Linear.apply(x, w, b, act, bridge)

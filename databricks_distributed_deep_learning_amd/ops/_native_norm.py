@@ -6,6 +6,7 @@ from typing import Optional
 import torch
 
 from . import _lib
+from ._native_elementwise import new_seed
 from ._lib import call, dcode, grad_ready, grad_sink, p
 
 
@@ -56,7 +57,8 @@ class _BatchNormTrain(torch.autograd.Function):
         M = x.numel() // C
         nblk = _lib.fn("ddl_bn_bwd_nblk")(M, C)
         f32 = dict(dtype=torch.float32, device=x.device)
-        part = torch.empty(nblk * 2 * C, **f32)
+        # partial rows + room for their 32:1 collapse (see norm.hip collapse_partials)
+        part = torch.empty((nblk + -(-nblk // 32)) * 2 * C, **f32)
         coef = torch.empty(3 * C, **f32)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
@@ -116,7 +118,7 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, e
 
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual):
+    def forward(ctx, x, weight, bias, eps, residual, drop_p, bridge=None):
         x = x.contiguous()
         H = x.shape[-1]
         rows = x.numel() // H
@@ -124,8 +126,11 @@ class _LayerNorm(torch.autograd.Function):
         res_rows = res.numel() // H if res is not None else rows
         stats = torch.empty(2, rows, dtype=torch.float32, device=x.device)
         y = torch.empty_like(x)
+        seed = new_seed() if drop_p > 0.0 else 0
         call("ddl_ln_fwd", dcode(x), p(x), p(res), res_rows, p(weight), p(bias), p(y), p(stats[0]), p(stats[1]),
-             rows, H, float(eps))
+             rows, H, float(eps), seed, float(drop_p))
+        ctx.seed, ctx.drop_p = seed, float(drop_p)
+        ctx.bridge = bridge
         ctx.res_shape = residual.shape if residual is not None else None
         ctx.params = (weight, bias)
         ctx.res_rows = res_rows
@@ -139,14 +144,16 @@ class _LayerNorm(torch.autograd.Function):
         H = x.shape[-1]
         rows = x.numel() // H
         nblk = _lib.fn("ddl_ln_bwd_nblk")(rows)
-        part = torch.empty(nblk * 3 * H, dtype=torch.float32, device=x.device)
+        part = torch.empty((nblk + -(-nblk // 32)) * 3 * H, dtype=torch.float32, device=x.device)
         dxsum = torch.empty(H, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
         direct = sg is not None and sb is not None
         dg, db = (sg, sb) if direct else (torch.empty_like(weight), torch.empty_like(weight))
+        # with fused dropout the residual gets the unmasked gradient, x the masked one
+        dres_buf = torch.empty_like(x) if ctx.drop_p > 0.0 else None
         call("ddl_ln_bwd", dcode(x), p(dy), p(x), p(res), ctx.res_rows, p(weight), p(stats[0]), p(stats[1]), p(dx),
-             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum))
+             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum), ctx.seed, ctx.drop_p, p(dres_buf))
         # the column sums of dx ride along on the gradient tensor: the Linear whose output
         # fed this LayerNorm takes them as its bias gradient instead of re-reading dx
         # (the version guards against autograd accumulating another gradient into dx in place)
@@ -157,14 +164,19 @@ class _LayerNorm(torch.autograd.Function):
             dg = db = None
         dres = None
         if ctx.res_shape is not None:
+            g = dres_buf if dres_buf is not None else dx
             if ctx.res_rows == rows:
-                dres = dx.view(ctx.res_shape)
+                dres = g.view(ctx.res_shape)
+                if ctx.bridge is not None:
+                    ctx.bridge.put(dres)       # summed into the consuming Linear's dgrad epilogue
+                    dres = None
             else:
-                dres = dx.view(-1, ctx.res_rows, H).float().sum(0).to(dx.dtype).view(ctx.res_shape)
-        return dx, dg, db, None, dres
+                dres = g.view(-1, ctx.res_rows, H).float().sum(0).to(dx.dtype).view(ctx.res_shape)
+        return dx, dg, db, None, dres, None, None
 
 
-def layer_norm(x, weight, bias, eps, residual: Optional[torch.Tensor] = None):
+def layer_norm(x, weight, bias, eps, residual: Optional[torch.Tensor] = None, dropout: float = 0.0,
+               residual_grad_to=None):
     from .norm import layer_norm_reference
     H = x.shape[-1]
     ok = bool(_lib.fn("ddl_ln_supported")(H)) and x.dtype in (torch.bfloat16, torch.float32)
@@ -175,8 +187,13 @@ def layer_norm(x, weight, bias, eps, residual: Optional[torch.Tensor] = None):
             # only leading-dimension broadcast ([1, S, H] against [B, S, H]) is supported
             ok = residual.dim() == x.dim() and all(r in (1, s) for r, s in zip(residual.shape, x.shape)) and \
                 residual.shape[0] == 1 and tuple(residual.shape[1:]) == tuple(x.shape[1:])
+    if dropout > 0.0 and (residual is None or residual.numel() != x.numel()):
+        ok = False                      # fused dropout: full-size residual only
     if not ok:
+        if dropout > 0.0:
+            from .activation import dropout as _dropout
+            x = _dropout(x, dropout, True)
         return layer_norm_reference(x, weight, bias, eps, residual)
     if weight.dtype != x.dtype:
         weight, bias = weight.to(x.dtype), bias.to(x.dtype)
-    return _LayerNorm.apply(x, weight, bias, eps, residual)
+    return _LayerNorm.apply(x, weight, bias, eps, residual, float(dropout), residual_grad_to)

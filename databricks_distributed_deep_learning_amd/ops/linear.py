@@ -39,10 +39,14 @@ def linear_reference(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
-           act: Optional[str] = None) -> torch.Tensor:
+           act: Optional[str] = None, grad_residual=None) -> torch.Tensor:
+    """``grad_residual``: a :class:`ops.bridge.GradBridge` whose pending gradient (a
+    post-LN residual branch's) is added to this layer's input gradient inside the
+    dgrad GEMM epilogue instead of by an autograd add kernel."""
     if act not in ACTS:
         raise ValueError(f"act must be one of {ACTS}")
     if _lib.use_native(x):
         from . import _native_linear
-        return _native_linear.linear(x, w, b, act)
-    return linear_reference(x, w, b, act)
+        return _native_linear.linear(x, w, b, act, grad_residual)
+    from .bridge import join
+    return linear_reference(join(x, grad_residual), w, b, act)

@@ -56,9 +56,19 @@ def layer_norm_reference(x, weight, bias, eps: float = 1e-12, residual: Optional
     return y.to(x.dtype)
 
 
-def layer_norm(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Tensor] = None):
-    """``LayerNorm(x + residual)`` over the last axis; fp32 statistics."""
+def layer_norm(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Tensor] = None,
+               dropout: float = 0.0, residual_grad_to=None):
+    """``LayerNorm(dropout(x) + residual)`` over the last axis; fp32 statistics.
+
+    ``dropout`` (training-time probability on ``x``; post-LN transformers apply it to
+    the sublayer output right before the residual add) is fused into the kernels on
+    the HIP path: the mask is a counter hash regenerated in the backward, which also
+    emits the masked gradient's column sums for the producing Linear's bias.
+    ``residual_grad_to``: a :class:`ops.bridge.GradBridge` that receives the residual's
+    gradient (for the Linear that also consumes ``residual``) instead of autograd."""
     if _lib.use_native(x):
         from . import _native_norm
-        return _native_norm.layer_norm(x, weight, bias, eps, residual)
+        return _native_norm.layer_norm(x, weight, bias, eps, residual, dropout, residual_grad_to)
+    if dropout > 0.0:
+        x = F.dropout(x, dropout, True)
     return layer_norm_reference(x, weight, bias, eps, residual)

@@ -8,28 +8,22 @@ from conftest import gpu_device
 
 pytestmark = pytest.mark.gpu
 
-M64 = (1 << 64) - 1
+M32 = 0xFFFFFFFF
 
 
-def _s64(v):
-    v &= M64
-    return v - (1 << 64) if v >= (1 << 63) else v
-
-
-C1, C2, C3 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
-
-
-def _lsr(z, k):
-    return (z >> k) & ((1 << (64 - k)) - 1)
+def _lowbias32(x):
+    """ddl_common.h lowbias32 on int64 tensors holding uint32 values."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7feb352d) & M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846ca68b) & M32
+    return x ^ (x >> 16)
 
 
 def hash_u32(seed, idx):
-    """torch re-implementation of ddl_common.h hash_u32 (int64 wraps like uint64)."""
-    z = idx * C2 + _s64(seed * C1 + C3)
-    z = (z ^ _lsr(z, 30)) * C2
-    z = (z ^ _lsr(z, 27)) * C3
-    z = z ^ _lsr(z, 31)
-    return _lsr(z, 32)
+    """torch re-implementation of ddl_common.h hash_u32 (two lowbias32 rounds)."""
+    a = _lowbias32((idx & M32) ^ (seed & M32))
+    return _lowbias32((a + ((idx >> 32) * 0x9E3779B9 & M32) + (seed >> 32)) & M32)
 
 
 def ref_attention(qkv, H, mask=None, keep=None, p=0.0):

@@ -204,7 +204,8 @@ def test_strided_dgrad_class_paths(path, N, H, W, C, K, R, pad):
 
 
 @pytest.mark.parametrize("M,N,K", [(8292, 2304, 136), (4100, 4200, 768), (520, 264, 1024)])
-@pytest.mark.parametrize("variant", ["plain", "bias_bf16_relu", "bias_f32", "acc_f32", "acc_bf16", "residual"])
+@pytest.mark.parametrize("variant", ["plain", "bias_bf16_relu", "bias_f32", "acc_f32", "acc_bf16", "residual",
+                                     "bias_gelu_aux"])
 def test_big_direct_persistent_epilogue(M, N, K, variant):
     """Register epilogue + persistent grid of the 256x256 kernel (> 256 tiles: blocks
     walk several tiles, the next tile's prologue overlaps this tile's stores)."""
@@ -231,11 +232,19 @@ def test_big_direct_persistent_epilogue(M, N, K, variant):
         r = torch.randn(M, N, device=dev).to(torch.bfloat16)
         kw = dict(residual=r)
         ref = ref + r.float()
+    elif variant == "bias_gelu_aux":
+        b = torch.randn(N, device=dev).to(torch.bfloat16)
+        z = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        kw = dict(bias=b, act="gelu", aux=z)
+        pre = ref + b.float()
+        ref = torch.nn.functional.gelu(pre)
     c = torch.randn(M, N, device=dev).to(out_dtype)
     if variant.startswith("acc"):
         ref = ref + c.float()
     NG.gemm(0, a, K, w, K, c, N, M, N, K, kernel="big", **kw)
     assert _rel_err(c, ref) < (2e-3 if out_dtype == torch.float32 else 1e-2)
+    if variant == "bias_gelu_aux":
+        assert _rel_err(z, pre) < 1e-2
     # every output element written exactly once: a second run into a NaN-filled
     # buffer must leave no NaN (non-accumulating variants)
     if not variant.startswith("acc"):

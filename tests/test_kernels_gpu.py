@@ -65,6 +65,68 @@ def test_batchnorm_train(dtype, relu, res, C, big):
         _close(rs[0].grad, rs[1].grad, tol, tol, "bn dres")
 
 
+def _hash_keep(seed: int, n: int, p: float):
+    """Python replica of the kernels' counter hash (ddl_common.h hash_u32): keep mask."""
+    import numpy as np
+
+    def lowbias32(x):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7feb352d)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846ca68b)
+        return x ^ (x >> np.uint32(16))
+    with np.errstate(over="ignore"):
+        idx = np.arange(n, dtype=np.uint64)
+        lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (idx >> np.uint64(32)).astype(np.uint32)
+        a = lowbias32(lo ^ np.uint32(seed & 0xFFFFFFFF))
+        h = lowbias32(a + hi * np.uint32(0x9E3779B9) + np.uint32(seed >> 32)).astype(np.float64)
+    thresh = min(4294967295.0, float(int(p * 4294967296.0)))
+    return torch.from_numpy(h >= thresh)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [768, 1024])
+def test_layernorm_fused_dropout(dtype, H):
+    """LN(dropout(Linear(x)) + res) with the dropout fused into the LN kernels, against
+    an fp32 reference that rebuilds the mask from the same counter hash: forward, x /
+    residual / gamma / beta gradients and the producing Linear's bias gradient (taken
+    from the LN backward's column sums of the masked gradient)."""
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.ops import norm
+    torch.manual_seed(2)
+    B, S, pdrop = 4, 64, 0.1
+    x = torch.randn(B, S, H, device=dev).to(dtype)
+    w = (torch.randn(H, H, device=dev) / H ** 0.5).to(dtype)
+    lb = (torch.randn(H, device=dev) * 0.1).to(dtype)
+    g = (torch.rand(H, device=dev) + 0.5).to(dtype)
+    b = (torch.randn(H, device=dev) * 0.1).to(dtype)
+    r = torch.randn(B, S, H, device=dev).to(dtype)
+    leaves = lambda ts: [t.clone().requires_grad_(True) for t in ts]  # noqa: E731
+    a = leaves([x, w, lb, g, b, r])
+    f = leaves([t.float() for t in (x, w, lb, g, b, r)])
+    torch.manual_seed(123)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())     # what the op will draw (new_seed)
+    torch.manual_seed(123)
+    y = norm.layer_norm(ops.linear(a[0], a[1], a[2], None), a[3], a[4], 1e-12, a[5], dropout=pdrop)
+    keep = _hash_keep(seed, B * S * H, pdrop).to(dev).view(B, S, H)
+    assert 0.85 < keep.float().mean().item() < 0.95
+    hidden = (f[0] @ f[1].t() + f[2]) * keep / (1 - pdrop)
+    yr = norm.layer_norm_reference(hidden, f[3], f[4], 1e-12, f[5])
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, yr, tol, tol, "ln+dropout fwd")
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dtype))
+    yr.backward(dy)
+    _close(a[0].grad, f[0].grad, tol, tol, "dx")
+    _close(a[2].grad, f[2].grad, tol * 20, tol, "linear bias grad (LN column sums)")
+    _close(a[3].grad, f[3].grad, tol * 20, tol, "dgamma")
+    _close(a[4].grad, f[4].grad, tol * 20, tol, "dbeta")
+    _close(a[5].grad, f[5].grad, tol * 10, tol, "dres")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H", [768, 1024])
 @pytest.mark.parametrize("res", [None, "full", "bcast"])
