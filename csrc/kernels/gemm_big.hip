@@ -921,8 +921,11 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     kp.ek = p.ek;
     const int nwg = p.tiles_m * p.tiles_n;
     int gx = nwg;
-    if (direct) {
-        const int cap = std::max(8, (num_cus() / splits) & ~7);   // multiple of 8: blocks keep their XCD
+    if (direct && splits == 1) {
+        // persistent: one block per CU walks tiles blockIdx.x, +gridDim.x, ...
+        // (a multiple of 8, so a block's tiles stay on its XCD); split-K grids keep
+        // one block per (tile, split) -- a capped grid would leave tiles for a second round
+        const int cap = std::max(8, num_cus() & ~7);
         gx = std::min(nwg, cap);
     }
     const dim3 grid(gx, splits);

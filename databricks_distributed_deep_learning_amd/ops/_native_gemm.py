@@ -67,11 +67,13 @@ def use_big(mode: int, M: int, N: int, K: int) -> bool:
 
 
 def big_splits(M: int, N: int, K: int) -> int:
+    """Split-K count for the 256x256 kernel: as many splits as keep every (tile, split)
+    block in ONE round on the CUs (floor, not ceil: a 257th block doubles the time)."""
     tiles = (-(-M // 256)) * (-(-N // 256))
     nk = -(-K // BK)
     if tiles >= 200:
         return 1
-    return max(1, min(-(-NUM_CU // tiles), nk // 4))
+    return max(1, min(NUM_CU // tiles, nk // 4))
 
 
 def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
