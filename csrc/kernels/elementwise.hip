@@ -136,6 +136,67 @@ __global__ __launch_bounds__(256) void softmax_ce_k(const T* __restrict__ logits
         }
     }
 }
+// Inference post-processing (K11): softmax over a row and its k largest
+// probabilities, one 256-thread block per row (the reference's batch-1 top-5 over
+// 1000 ImageNet classes).  Probabilities are staged in LDS (C <= 4096); the top-k
+// is k rounds of a block-wide (value, index) argmax that masks the winner --
+// ties resolve to the lower index, like torch.topk on distinct values.
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_topk_k(const T* __restrict__ logits, int C, int k,
+                                                      float* __restrict__ probs, float* __restrict__ top_v,
+                                                      int64_t* __restrict__ top_i) {
+    __shared__ float pr[4096];
+    __shared__ float red[4];
+    __shared__ float bv[4];
+    __shared__ int bi[4];
+    const long row = blockIdx.x;
+    const T* x = logits + row * C;
+    float m = -INFINITY;
+    for (int c = threadIdx.x; c < C; c += 256) m = fmaxf(m, to_f(x[c]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float s = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float e = __expf(to_f(x[c]) - m);
+        pr[c] = e;
+        s += e;
+    }
+    s = block_sum<256>(s, red);
+    const float inv_s = 1.f / s;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        pr[c] *= inv_s;
+        if (probs) probs[row * C + c] = pr[c];
+    }
+    __syncthreads();
+    for (int r = 0; r < k; ++r) {
+        float v = -1.f;
+        int vi = C;
+        for (int c = threadIdx.x; c < C; c += 256)
+            if (pr[c] > v) { v = pr[c]; vi = c; }
+        // wave argmax (higher value, then lower index)
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(v, o);
+            const int oi = __shfl_xor(vi, o);
+            if (ov > v || (ov == v && oi < vi)) { v = ov; vi = oi; }
+        }
+        if ((threadIdx.x & 63) == 0) { bv[threadIdx.x >> 6] = v; bi[threadIdx.x >> 6] = vi; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float best = bv[0];
+            int besti = bi[0];
+            for (int w = 1; w < 4; ++w)
+                if (bv[w] > best || (bv[w] == best && bi[w] < besti)) { best = bv[w]; besti = bi[w]; }
+            top_v[row * k + r] = best;
+            top_i[row * k + r] = besti;
+            pr[besti] = -2.f;     // remove the winner for the next round
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void mean_k(const float* __restrict__ v, long n, float* __restrict__ out) {
     __shared__ float red[4];
     float s = 0.f;
@@ -478,5 +539,15 @@ DDL_API int ddl_acc_f32(int dtype, void* dst, const float* src, long n, hipStrea
     const int g = (int)std::min<long>(1024, (n + 255) / 256);
     DISPATCH_T(dtype, (acc_f32_k<bf16_t><<<g, 256, 0, st>>>((bf16_t*)dst, src, n)),
                (acc_f32_k<float><<<g, 256, 0, st>>>((float*)dst, src, n)));
+    DDL_RETURN_LAUNCH();
+}
+
+// probs (nullable) [B, C], top_v [B, k], top_i (int64) [B, k]; C <= 4096, k <= C
+DDL_API int ddl_softmax_topk(int dtype, const void* logits, long B, int C, int k, float* probs, float* top_v,
+                             int64_t* top_i, hipStream_t st) {
+    if (C > 4096 || k < 1 || k > C) return -1;
+    DISPATCH_T(dtype,
+               (softmax_topk_k<bf16_t><<<B, 256, 0, st>>>((const bf16_t*)logits, C, k, probs, top_v, top_i)),
+               (softmax_topk_k<float><<<B, 256, 0, st>>>((const float*)logits, C, k, probs, top_v, top_i)));
     DDL_RETURN_LAUNCH();
 }

@@ -596,9 +596,10 @@ __global__ __launch_bounds__(256) void bn_partials_collapse_k(const float* __res
 // 64 columns is too little parallelism for ~1000 rows).  The caller allocates
 // `part` with room for the collapsed rows behind the nblk partial rows.
 constexpr int COLLAPSE_OVER = 64;
-static const float* collapse_partials(const float* part, int& nblk, int width, hipStream_t st) {
+static const float* collapse_partials(const float* part, int& nblk, int width, hipStream_t st,
+                                      float* ws = nullptr) {
     if (nblk <= COLLAPSE_OVER) return part;
-    float* ws = const_cast<float*>(part) + (long)nblk * width;
+    if (!ws) ws = const_cast<float*>(part) + (long)nblk * width;
     const int chunks = (nblk + PC_ROWS - 1) / PC_ROWS;
     bn_partials_collapse_k<<<dim3((width + 255) / 256, chunks), 256, 0, st>>>(part, nblk, width, ws);
     nblk = chunks;
@@ -820,5 +821,91 @@ DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res
                  : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
                                    rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum, drop, st);
     if (rc) return rc;
+    DDL_RETURN_LAUNCH();
+}
+
+// ---------------------------------------------------------------- SyncBatchNorm pieces
+// Cross-rank BatchNorm needs the per-channel sums as ONE row before the finalize (the
+// all-reduce runs between): partial passes, rows -> one row, finalize / apply with
+// the global row count.
+namespace {
+__global__ __launch_bounds__(1024) void rows_sum_k(const float* __restrict__ part, int nrows, int width,
+                                                   float* __restrict__ out) {
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const float s = colsum64(part, nrows, width, c, c < width, red);
+    if (threadIdx.x < 64 && c < width) out[c] = s;
+}
+}  // namespace
+
+// out[c] = sum_r part[r][c]; ws (ceil(nblk/32) * width floats) may be null when part
+// itself holds (nblk + ceil(nblk/32)) * width floats
+DDL_API int ddl_bn_rows_sum(const float* part, int nblk, int width, float* out, float* ws, hipStream_t st) {
+    int nrows = nblk;
+    const float* src = collapse_partials(part, nrows, width, st, ws);
+    rows_sum_k<<<(width + 63) / 64, 1024, 0, st>>>(src, nrows, width, out);
+    DDL_RETURN_LAUNCH();
+}
+
+// forward statistics partials only: nblk = ddl_bn_stats_nblk(M, C) rows of [sum | sumsq]
+DDL_API int ddl_bn_stats_partials(int dtype, const void* x, long M, int C, float* part, hipStream_t st) {
+    if (C % 8 || (BN_NT % (C / 8) != 0)) return -1;
+    const int nblk = ddl_bn_stats_nblk(M, C);
+    const int rpi = BN_NT / (C / 8);
+    long rpb = (M + nblk - 1) / nblk;
+    rpb = (rpb + rpi - 1) / rpi * rpi;
+    if (dtype == 1) bn_stats_partial_k<bf16_t><<<nblk, BN_NT, 0, st>>>((const bf16_t*)x, M, C, (int)rpb, part);
+    else bn_stats_partial_k<float><<<nblk, BN_NT, 0, st>>>((const float*)x, M, C, (int)rpb, part);
+    DDL_RETURN_LAUNCH();
+}
+
+// backward partials only: nblk = ddl_bn_bwd_nblk(M, C) rows of [sum dz | sum dz*xhat]
+DDL_API int ddl_bn_bwd_partials(int dtype, const void* dy, const void* mask, const void* x, const float* mean,
+                                const float* invstd, long M, int C, int relu, float* part, hipStream_t st) {
+    if (C % 8 || (BN_NT % (C / 8) != 0) || (relu && !mask)) return -1;
+    const int nblk = ddl_bn_bwd_nblk(M, C);
+    const int rpi = BN_NT / (C / 8);
+    long rpb = (M + nblk - 1) / nblk;
+    rpb = (rpb + rpi - 1) / rpi * rpi;
+    const uint8_t* mk = (const uint8_t*)mask;
+#define BWP(T) do { if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>((const T*)dy, mk, (const T*)x, mean, invstd, M, C, (int)rpb, part); \
+                    else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>((const T*)dy, mk, (const T*)x, mean, invstd, M, C, (int)rpb, part); } while (0)
+    if (dtype == 1) BWP(bf16_t);
+    else BWP(float);
+#undef BWP
+    DDL_RETURN_LAUNCH();
+}
+
+// backward finish from ONE (all-reduced) row [sum dz | sum dz*xhat]: dgamma / dbeta and the
+// coefficients use the global row count M_total, the apply walks the local M rows
+template <typename T>
+static void bn_bwd_finish_t(const T* dy, const uint8_t* mk, const T* x, const float* mean, const float* invstd,
+                            const T* gamma, long M, long M_total, int C, int relu, const float* row, T* dgamma,
+                            T* dbeta, float* coef, T* dx, T* dres, int acc, hipStream_t st) {
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(row, 1, C, M_total, gamma, invstd, dgamma, dbeta, coef, acc);
+    if (rows_ok(C)) {
+        const int gr = rows_grid(M, C);
+        if (relu) {
+            if (dres) bn_bwd_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+            else bn_bwd_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+        } else {
+            if (dres) bn_bwd_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+            else bn_bwd_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+        }
+    }
+}
+
+DDL_API int ddl_bn_bwd_finish(int dtype, const void* dy, const void* mask, const void* x, const float* mean,
+                              const float* invstd, const void* gamma, long M, long M_total, int C, int relu,
+                              const float* row, void* dgamma, void* dbeta, float* coef, void* dx, void* dres,
+                              int acc_params, hipStream_t st) {
+    if (!rows_ok(C) || (relu && !mask)) return -1;
+    const uint8_t* mk = (const uint8_t*)mask;
+    if (dtype == 1)
+        bn_bwd_finish_t((const bf16_t*)dy, mk, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M, M_total, C,
+                        relu, row, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
+    else
+        bn_bwd_finish_t((const float*)dy, mk, (const float*)x, mean, invstd, (const float*)gamma, M, M_total, C,
+                        relu, row, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st);
     DDL_RETURN_LAUNCH();
 }

@@ -49,6 +49,7 @@ class TrainConfig:
     comm: str = "auto"               # gradient all-reduce engine: auto|native (C++ RCCL engine)|torch
     grad_reduce_dtype: str = "auto"  # auto|fp32|bf16  all-reduce payload dtype
     broadcast_buffers: bool = False
+    sync_bn: bool = False            # SyncBatchNorm: BN statistics summed over all ranks (CV models)
     # ---- runtime ----------------------------------------------------------
     native: str = "auto"             # auto|on|off  HIP kernels (off = stock torch ops)
     cuda_graph: bool = False         # capture the whole train step in a hipGraph

@@ -6,7 +6,7 @@ import torch.nn as nn
 from .resnet import ResNet, resnet18, resnet34, resnet50, resnet101, resnet152  # noqa: F401
 from .bert import BertConfig, BertForSequenceClassification, bert_base, bert_large  # noqa: F401
 from .vit import ViTConfig, ViTForImageClassification, vit_b16  # noqa: F401
-from .layers import cast_params  # noqa: F401
+from .layers import cast_params, convert_sync_batchnorm  # noqa: F401
 
 _REGISTRY = {
     "resnet18": resnet18, "resnet34": resnet34, "resnet50": resnet50,

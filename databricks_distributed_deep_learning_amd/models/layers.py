@@ -50,6 +50,7 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
         self._nbt_pending = 0
+        self.sync_group = None      # process group: SyncBatchNorm in training (convert_sync_batchnorm)
 
     def _flush_nbt(self):
         if self._nbt_pending:
@@ -71,7 +72,7 @@ class BatchNorm2d(nn.Module):
             self._nbt_pending += 1
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var,
                               self.training, self.momentum, self.eps, self.relu, residual,
-                              residual_grad_to=residual_grad_to, stats=stats)
+                              residual_grad_to=residual_grad_to, stats=stats, group=self.sync_group)
 
     def _apply(self, fn, recurse=True):
         # keep running stats in fp32 when the module is cast to bf16
@@ -146,6 +147,18 @@ class Dropout(nn.Module):
 
     def forward(self, x):
         return ops.dropout(x, self.p, self.training)
+
+
+def convert_sync_batchnorm(module: nn.Module, group=None) -> nn.Module:
+    """Make every :class:`BatchNorm2d` a SyncBatchNorm over ``group`` (default: the world
+    group): training statistics summed across ranks -- one [2C] all-reduce per layer in
+    forward and one in backward.  The analogue of ``nn.SyncBatchNorm.convert_sync_batchnorm``."""
+    import torch.distributed as dist
+    g = group if group is not None else dist.group.WORLD
+    for m in module.modules():
+        if isinstance(m, BatchNorm2d):
+            m.sync_group = g
+    return module
 
 
 def cast_params(module: nn.Module, dtype: torch.dtype) -> nn.Module:

@@ -108,6 +108,10 @@ _SIGS = {
     # norm.hip
     "ddl_bn_stats_nblk": [L, I],
     "ddl_bn_bwd_nblk": [L, I],
+    "ddl_bn_rows_sum": [P, I, I, P, P, P],
+    "ddl_bn_stats_partials": [I, P, L, I, P, P],
+    "ddl_bn_bwd_partials": [I, P, P, P, P, P, L, I, I, P, P],
+    "ddl_bn_bwd_finish": [I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],
     "ddl_bn_eval_coeffs": [I, I, P, P, P, P, F, P, P, P],
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P, P],
@@ -115,6 +119,7 @@ _SIGS = {
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
     "ddl_acc_f32": [I, P, P, L, P],
+    "ddl_softmax_topk": [I, P, L, I, I, P, P, P, P],
     "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],
     "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_ln_supported": [I],

@@ -14,11 +14,18 @@ def _bn_supported(C: int) -> bool:
     return C % 8 == 0 and 256 % (C // 8) == 0
 
 
+def _group_sum(row: torch.Tensor, group) -> None:
+    """In-place SUM all-reduce of a small fp32 row over the SyncBatchNorm group."""
+    import torch.distributed as dist
+    dist.all_reduce(row, op=dist.ReduceOp.SUM, group=group)
+
+
 class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual, bridge=None,
-                pre=None):
+                pre=None, group=None):
         ctx.bridge = bridge
+        ctx.group = group
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
@@ -26,7 +33,27 @@ class _BatchNormTrain(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=x.device)
         stats = torch.empty(4, C, **f32)           # mean, invstd, scale, shift
         given = pre.take_for(x) if pre is not None else None
-        if given is not None:                      # partials from the producing GEMM's epilogue
+        if group is not None:
+            # SyncBatchNorm: [sum | sumsq] as one row, summed over the group, finalised with
+            # the global row count (equal per-rank batches, as data-parallel training runs)
+            import torch.distributed as dist
+            world = dist.get_world_size(group)
+            if given is not None:
+                part, nblk = given
+                ws = torch.empty(-(-nblk // 32) * 2 * C, **f32)
+            else:
+                nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
+                part = torch.empty((nblk + -(-nblk // 32)) * 2 * C, **f32)
+                call("ddl_bn_stats_partials", dt, p(x), M, C, p(part))
+                ws = None
+            row = torch.empty(2 * C, **f32)
+            call("ddl_bn_rows_sum", p(part), nblk, 2 * C, p(row), p(ws))
+            _group_sum(row, group)
+            call("ddl_bn_fwd_from_partials", dt, p(row), 1, M * world, C, p(weight), p(bias), p(running_mean),
+                 p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]),
+                 None, 0)
+            ctx.m_total = M * world
+        elif given is not None:                    # partials from the producing GEMM's epilogue
             part, nblk = given
             # thousands of partial rows (one per 128 GEMM rows) are first collapsed 32:1
             ws = torch.empty(-(-nblk // 32) * 2 * C, **f32) if nblk > 256 else None
@@ -69,8 +96,18 @@ class _BatchNormTrain(torch.autograd.Function):
         else:
             dgamma = torch.empty_like(weight) if weight is not None else None
             dbeta = torch.empty_like(weight) if weight is not None else None
-        call("ddl_bn_bwd", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M, C, int(ctx.relu),
-             p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+        if ctx.group is not None:
+            # SyncBatchNorm: [sum dz | sum dz*xhat] summed over the group before the finalize
+            call("ddl_bn_bwd_partials", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), M, C,
+                 int(ctx.relu), p(part))
+            row = torch.empty(2 * C, **f32)
+            call("ddl_bn_rows_sum", p(part), nblk, 2 * C, p(row), None)
+            _group_sum(row, ctx.group)
+            call("ddl_bn_bwd_finish", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M,
+                 ctx.m_total, C, int(ctx.relu), p(row), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+        else:
+            call("ddl_bn_bwd", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M, C,
+                 int(ctx.relu), p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
         if direct:
             grad_ready(ctx.params[0])
             grad_ready(ctx.params[1])
@@ -78,7 +115,7 @@ class _BatchNormTrain(torch.autograd.Function):
         if dres is not None and ctx.bridge is not None:
             ctx.bridge.put(dres)            # summed into the consumer's dgrad epilogue
             dres = None
-        return dx, dgamma, dbeta, None, None, None, None, None, dres, None, None
+        return dx, dgamma, dbeta, None, None, None, None, None, dres, None, None, None
 
 
 class _BatchNormEval(torch.autograd.Function):
@@ -98,17 +135,20 @@ class _BatchNormEval(torch.autograd.Function):
 
 
 def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual, bridge=None,
-               pre=None):
-    from .norm import batch_norm_reference
+               pre=None, group=None):
+    from .norm import batch_norm_reference, sync_batch_norm_reference
     C = x.shape[-1]
     if not _bn_supported(C) or x.dtype not in (torch.bfloat16, torch.float32):
+        if training and group is not None:
+            return sync_batch_norm_reference(x, weight, bias, running_mean, running_var, momentum, eps, relu,
+                                             residual, group)
         return batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu,
                                     residual)
     if weight is not None and weight.dtype != x.dtype:
         weight, bias = weight.to(x.dtype), bias.to(x.dtype)
     if training:
         return _BatchNormTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
-                                     bridge, pre)
+                                     bridge, pre, group)
     if torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)):
         # eval-mode BN with gradients (frozen-statistics fine-tuning): reference path
         return batch_norm_reference(x, weight, bias, running_mean, running_var, False, momentum, eps, relu,

@@ -34,16 +34,52 @@ def batch_norm_reference(x, weight, bias, running_mean, running_var, training: b
     return y.to(x.dtype)
 
 
+def sync_batch_norm_reference(x, weight, bias, running_mean, running_var, momentum: float = 0.1,
+                              eps: float = 1e-5, relu: bool = False, residual: Optional[torch.Tensor] = None,
+                              group=None):
+    """Training-mode BatchNorm whose statistics are summed over ``group`` (SyncBatchNorm).
+
+    Per-channel [sum, sumsq] of every rank are all-reduced (differentiably: the
+    backward sums the statistics' gradients over the group too); ranks hold equal
+    batch sizes, as in data-parallel training."""
+    import torch.distributed as dist
+    from torch.distributed.nn.functional import all_reduce
+    C = x.shape[-1]
+    xf = x.reshape(-1, C).float()
+    world = dist.get_world_size(group)
+    n = xf.shape[0] * world
+    st = all_reduce(torch.cat([xf.sum(0), (xf * xf).sum(0)]), op=dist.ReduceOp.SUM, group=group)
+    mean = st[:C] / n
+    var = (st[C:] / n - mean * mean).clamp_min(0)
+    y = (xf - mean) * torch.rsqrt(var + eps)
+    if weight is not None:
+        y = y * weight.float() + bias.float()
+    with torch.no_grad():
+        running_mean.mul_(1 - momentum).add_(mean.detach(), alpha=momentum)
+        running_var.mul_(1 - momentum).add_(var.detach() * (n / max(1, n - 1)), alpha=momentum)
+    y = y.view_as(x)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
 def batch_norm(x, weight, bias, running_mean, running_var, training: bool, momentum: float = 0.1,
                eps: float = 1e-5, relu: bool = False, residual: Optional[torch.Tensor] = None,
-               residual_grad_to=None, stats=None):
+               residual_grad_to=None, stats=None, group=None):
     """``residual_grad_to``: a :class:`ops.bridge.GradBridge` that receives the
     residual's gradient instead of autograd (see ``ops/bridge.py``).  ``stats``: the
-    :class:`ops.bridge.BNStats` the producing conv filled (skips the statistics pass)."""
+    :class:`ops.bridge.BNStats` the producing conv filled (skips the statistics pass).
+    ``group``: a process group -> SyncBatchNorm (statistics summed over its ranks in
+    training; one [2C] all-reduce in forward and one in backward per layer)."""
     if _lib.use_native(x):
         from . import _native_norm
         return _native_norm.batch_norm(x, weight, bias, running_mean, running_var, training,
-                                       momentum, eps, relu, residual, residual_grad_to, stats)
+                                       momentum, eps, relu, residual, residual_grad_to, stats, group)
+    if training and group is not None:
+        return sync_batch_norm_reference(x, weight, bias, running_mean, running_var, momentum, eps, relu,
+                                         residual, group)
     return batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps,
                                 relu, residual)
 

@@ -24,7 +24,7 @@ import torch
 from .. import ops
 from ..config import TrainConfig, apply_overrides
 from ..data import SyntheticImageNet, SyntheticTokens
-from ..models import build_model, cast_params, count_params
+from ..models import build_model, cast_params, convert_sync_batchnorm, count_params
 from ..optim import LRSchedule, ParamArena, build_optimizer
 from ..parallel import dist as ddist
 from ..parallel.ddp import DataParallel
@@ -52,6 +52,8 @@ class Trainer:
                             image_size=cfg.image_size)
         model = model.to(self.device)
         cast_params(model, self.dtype)
+        if cfg.sync_bn and self.world > 1:
+            convert_sync_batchnorm(model)
         self.model = model
         self.n_params = count_params(model)
         self.arena = ParamArena(list(model.named_parameters()))

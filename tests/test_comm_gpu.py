@@ -75,3 +75,34 @@ def test_reducer_native_engine(pg):
     ref = torch.cat([grads2[e.name].reshape(-1) for e in ddp.arena.entries])
     got = torch.cat([g[e.offset:e.offset + e.numel] for e in ddp.arena.entries])
     assert ((got.float() - ref.float()).abs().max() / ref.abs().max()).item() < 1e-3
+
+
+@pytest.mark.parametrize("fused_stats", [False, True])
+def test_sync_batchnorm_native_world1(pg, fused_stats):
+    """SyncBatchNorm's split native path (partials -> one row -> all-reduce -> finalize /
+    apply with the global count) at world size 1 must equal the fused single-GPU path,
+    with statistics from the BN's own pass or from the conv GEMM epilogue."""
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.ops.bridge import BNStats
+    torch.manual_seed(9)
+    x = torch.randn(16, 30, 30, 64, device=pg).to(torch.bfloat16)
+    w = (torch.randn(128, 3, 3, 64, device=pg) * 0.05).to(torch.bfloat16)
+    g = (torch.rand(128, device=pg) + 0.5).to(torch.bfloat16)
+    b = (torch.randn(128, device=pg) * 0.1).to(torch.bfloat16)
+    dy = torch.randn(16, 30, 30, 128, device=pg).to(torch.bfloat16)
+    outs = []
+    for group in (None, dist.group.WORLD):
+        xs, gs, bs = (t.clone().requires_grad_(True) for t in (x, g, b))
+        rm, rv = torch.zeros(128, device=pg), torch.ones(128, device=pg)
+        st = BNStats() if fused_stats else None
+        from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+        saved, NC.STATS_MIN_K = NC.STATS_MIN_K, 0
+        try:
+            y = ops.conv2d(xs, w, 1, 1, bn_stats=st)
+        finally:
+            NC.STATS_MIN_K = saved
+        z = ops.batch_norm(y, gs, bs, rm, rv, True, 0.1, 1e-5, True, None, stats=st, group=group)
+        z.backward(dy)
+        outs.append((z.float(), xs.grad.float(), gs.grad.float(), bs.grad.float(), rm, rv))
+    for a, c in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, c, rtol=2e-2, atol=2e-2)

@@ -132,6 +132,42 @@ def _broadcast_init_check():
 
 
 # ---------------------------------------------------------------- tests
+def _sync_bn_equivalence():
+    """SyncBatchNorm on each rank's half batch == BatchNorm over the full batch."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.models.layers import BatchNorm2d, convert_sync_batchnorm
+    rank, world = dist.get_rank(), dist.get_world_size()
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(8, 5, 5, 16, generator=g) * 2 + 0.5
+    r = torch.randn(8, 5, 5, 16, generator=g)
+    dy = torch.randn(8, 5, 5, 16, generator=g)
+    ref = BatchNorm2d(16, relu=True)
+    with torch.no_grad():
+        ref.weight.copy_(torch.rand(16, generator=g) + 0.5)
+    sync = BatchNorm2d(16, relu=True)
+    sync.load_state_dict(ref.state_dict())
+    convert_sync_batchnorm(sync)
+    xr = x.clone().requires_grad_(True)
+    (ref(xr, residual=r) * dy).sum().backward()
+    lo, hi = rank * 8 // world, (rank + 1) * 8 // world
+    xs = x[lo:hi].clone().requires_grad_(True)
+    (sync(xs, residual=r[lo:hi]) * dy[lo:hi]).sum().backward()
+    out_err = (sync(x[lo:hi].clone(), residual=r[lo:hi]) - ref(x.clone(), residual=r)[lo:hi]).abs().max().item()
+    # parameter gradients are per-rank partials: their sum over ranks is the full-batch gradient
+    gw = sync.weight.grad.clone()
+    dist.all_reduce(gw)
+    return {"dx": (xs.grad - xr.grad[lo:hi]).abs().max().item(),
+            "dw": (gw - ref.weight.grad).abs().max().item(),
+            "rm": (sync.running_mean - ref.running_mean).abs().max().item(),
+            "rv": (sync.running_var - ref.running_var).abs().max().item(),
+            "out": out_err}
+
+
+def test_sync_batchnorm_matches_full_batch():
+    out = Distributor(num_processes=2, use_gpu=False).run(_sync_bn_equivalence)
+    assert max(out.values()) < 1e-4, out
+
+
 def test_distributor_returns_rank0_value():
     out = Distributor(num_processes=2, use_gpu=False).run(_rank_info, "hello")
     assert out == {"tag": "hello", "rank": 0, "world": 2, "sum": 3.0}

@@ -274,3 +274,21 @@ def test_flat_optimizers_match_torch_path(name, pdtype):
     _lib.set_mode("auto")
     _close(outs[0][0], outs[1][0], 1e-5, 1e-5, f"{name} master")
     _close(outs[0][1], outs[1][1], 1e-2 if pdtype == torch.bfloat16 else 1e-5, 1e-5, f"{name} param")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,k", [(1, 1000, 5), (3, 1000, 5), (4, 37, 3), (2, 4096, 10)])
+def test_softmax_topk(dtype, B, C, k):
+    """Inference post-processing kernel (softmax + top-k, the reference's top-5)."""
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd import ops
+    torch.manual_seed(5)
+    logits = (torch.randn(B, C, device=dev) * 3).to(dtype)
+    p, v, i = ops.softmax_topk(logits, k)
+    pr = torch.softmax(logits.float(), -1)
+    vr, ir = torch.topk(pr, k, -1)
+    _close(p, pr, 1e-6, 1e-5, "probs")
+    _close(v, vr, 1e-6, 1e-5, "top-k values")
+    # indices: equal wherever the reference values are distinct
+    assert torch.equal(i, ir) or torch.allclose(pr.gather(-1, i), vr, atol=1e-7)
