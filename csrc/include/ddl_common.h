@@ -111,9 +111,21 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 
 // ---------------------------------------------------------------- math
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf for the GELU epilogues: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far
+// below bf16 resolution) -- one reciprocal, one exp and a degree-5 Horner chain,
+// branch-free, ~12 VALU ops instead of the ~30 (two-range, branching) of erff.  The
+// FFN GEMM applies it to 128 values per lane per output tile, where it was the
+// epilogue's main cost.
+__device__ __forceinline__ float erf_fast(float x) {
+    const float ax = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+    const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
+                        0.254829592f) * t;
+    return copysignf(1.f - poly * __expf(-ax * ax), x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+    const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f));
     const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
     return cdf + x * pdf;
 }

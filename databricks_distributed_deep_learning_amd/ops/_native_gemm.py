@@ -34,6 +34,17 @@ def set_big_gemm(enabled: bool) -> None:
 
 
 _forced: Optional[str] = None
+# per-call device timing for diagnostics (scripts/debug/gemm_trace.py): list of
+# (signature, (kernel, splits), start event, end event) while enabled
+_trace: Optional[list] = None
+
+
+def trace(enabled: bool = True) -> Optional[list]:
+    """Start (or stop, returning the records) per-GEMM event timing."""
+    global _trace
+    out = _trace
+    _trace = [] if enabled else None
+    return out
 
 
 @contextlib.contextmanager
@@ -296,8 +307,15 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
         conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
     choice = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap,
                      residual, kernel, colstats)
+    if _trace is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     _launch(choice[0], choice[1], mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
             residual, accumulate, colstats)
+    if _trace is not None:
+        e1.record()
+        _trace.append(((mode, M, N, K, tuple(conv) if conv is not None else None, act, bias is not None,
+                        residual is not None, colstats is not None, accumulate), choice, e0, e1))
     if colstats is not None:
         # one partial row per 128 output rows (256x256 tiles: one per wave row)
         return 2 * -(-M // 256) if choice[0] == "big" else -(-M // 128)
