@@ -712,26 +712,57 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             const int vn = vt + gridDim.x;
             const bool next = vn < nwg;
             const int m0c = m0, n0c = n0, tm_c = tm;
+            const bool interior = m0c + TB <= p.M && n0c + TB <= p.N;
+            // Store-behind: when this tile's epilogue issues a KNOWN number of vector-memory
+            // ops (lean bf16 variant: one 8-byte store per site, +8 statistics stores), the
+            // WHOLE next prologue (E and O halves) is issued first and only the E loads are
+            // waited for -- vmcnt(6 + stores) -- so the stores drain under the next tile's
+            // loads and MFMAs instead of being waited for (vmcnt retires in issue order).
+            // Short-K tiles (1x1 convolutions: K = 64..256) are otherwise latency-bound on
+            // load -> compute -> store-drain per tile.
+            const bool behind = next && nK > 0 && interior && p.ek == EK_BF16 && !p.bias && !p.res;
             if (next) {
                 coords(vn);
                 sa.init(p, m0);
                 sb.init(p, n0);
                 if (nK > 0) prologueE();
+                if (behind && nK > 1) {
+                    sa.stage(p, smem, 1, 0, kt0 + 1);
+                    sb.stage(p, smem, 1, 0, kt0 + 1);
+                    sb.stage(p, smem, 1, 1, kt0 + 1);
+                }
             }
             // interior tiles take a lean variant (no bounds checks, one store per site);
             // edge tiles and the rarer epilogue options the general one
-            if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_BF16)
+            if (interior && p.ek == EK_BF16)
                 epi_direct<EK_BF16>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
-            else if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_F32)
+            else if (interior && p.ek == EK_F32)
                 epi_direct<EK_F32>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
-            else if (m0c + TB <= p.M && n0c + TB <= p.N && p.ek == EK_GELU)
+            else if (interior && p.ek == EK_GELU)
                 epi_direct<EK_GELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else
                 epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             if (!next) return;
             zero_acc();
             vt = vn;
-            if (nK > 0) prologueO();
+            if (nK > 0) {
+                if (behind) {
+                    // E landed once at most (O loads) + (epilogue stores) remain outstanding
+                    if (nK > 1) {
+                        if (p.colstats) asm volatile("s_waitcnt vmcnt(46)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+                    } else {
+                        if (p.colstats) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                    }
+                    BARRIER();
+#if DDL_STAGGER
+                    if (wm == 1) BARRIER();
+#endif
+                } else {
+                    prologueO();
+                }
+            }
             continue;
         }
         break;

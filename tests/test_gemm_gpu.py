@@ -203,7 +203,8 @@ def test_strided_dgrad_class_paths(path, N, H, W, C, K, R, pad):
     assert _rel_err(dx, xr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(8292, 2304, 136), (4100, 4200, 768), (520, 264, 1024)])
+@pytest.mark.parametrize("M,N,K", [(8292, 2304, 136), (4100, 4200, 768), (520, 264, 1024), (70000, 512, 64),
+                                   (70000, 256, 128)])
 @pytest.mark.parametrize("variant", ["plain", "bias_bf16_relu", "bias_f32", "acc_f32", "acc_bf16", "residual",
                                      "bias_gelu_aux"])
 def test_big_direct_persistent_epilogue(M, N, K, variant):
