@@ -41,6 +41,7 @@ struct ConvDesc {
     int R, S;                       // taps (after sub-setting for dgrad classes)
     FastDiv fd_PQ, fd_Q, fd_C, fd_S;
     int OH, OW, ostep, oa, ob;      // output pixel (n, p*ostep+oa, q*ostep+ob) in [OH, OW]
+    int bk_dq, bk_dp;               // BK output pixels = bk_dp grid rows + bk_dq columns
 };
 
 struct Params {
@@ -99,6 +100,10 @@ struct Loader {
     bool rowok[4];
     int ctap_r, ctap_s, cci;   // CONVW: column tap decomposition (fixed per thread)
     bool colok;
+    // CONVW: output-pixel state of this thread's rows, advanced by BK per K-step
+    // instead of two divisions per 16-byte chunk (the loader was VALU-bound)
+    int wn_[4], wp_[4], wq_[4];
+    int knext;
 
     __device__ __forceinline__ void init(const Params& p, int origin) {
         const int t = threadIdx.x;
@@ -132,6 +137,7 @@ struct Loader {
             cci = cc - tap * cd.C;
             ctap_r = (int)fdiv((uint32_t)tap, cd.fd_S);
             ctap_s = tap - ctap_r * cd.S;
+            knext = -1;
         }
     }
 
@@ -173,21 +179,40 @@ struct Loader {
             }
         } else {  // CONVW: reduction rows are output pixels m
             const ConvDesc& cd = p.cd;
+            if (k0 != knext) {   // first K-step of this block: full decomposition of each row
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m = k0 + (ROWS == 128 ? (t >> 4) + 16 * i : (t >> 3) + 32 * i);
+                    const int mm = m < K ? m : 0;
+                    wn_[i] = (int)fdiv((uint32_t)mm, cd.fd_PQ);
+                    const int rem = mm - wn_[i] * cd.P * cd.Q;
+                    wp_[i] = (int)fdiv((uint32_t)rem, cd.fd_Q);
+                    wq_[i] = rem - wp_[i] * cd.Q;
+                }
+            }
+            const int hof = cd.h_off + ctap_r * cd.h_step, wof = cd.w_off + ctap_s * cd.w_step;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 if (ROWS != 128 && i >= 2) break;
                 const int m = k0 + (ROWS == 128 ? (t >> 4) + 16 * i : (t >> 3) + 32 * i);
-                bool ok = colok && m < K;
-                const int mm = ok ? m : 0;
-                const int n = (int)fdiv((uint32_t)mm, cd.fd_PQ);
-                const int rem = mm - n * cd.P * cd.Q;
-                const int pp = (int)fdiv((uint32_t)rem, cd.fd_Q);
-                const int qq = rem - pp * cd.Q;
-                const int h = pp * cd.stride + cd.h_off + ctap_r * cd.h_step;
-                const int w = qq * cd.stride + cd.w_off + ctap_s * cd.w_step;
-                ok = ok && (unsigned)h < (unsigned)cd.H && (unsigned)w < (unsigned)cd.W;
-                v[i] = sel(ok, ldg16(ok ? base + (((long)n * cd.H + h) * cd.W + w) * cd.C + cci : base), z);
+                const int h = wp_[i] * cd.stride + hof;
+                const int w = wq_[i] * cd.stride + wof;
+                const bool ok = colok && m < K && (unsigned)h < (unsigned)cd.H && (unsigned)w < (unsigned)cd.W;
+                // 32-bit element offset: activations stay < 2^31 elements (host-checked)
+                const uint32_t off = ((uint32_t)(wn_[i] * cd.H + h) * (uint32_t)cd.W + (uint32_t)w) * (uint32_t)cd.C +
+                                     (uint32_t)cci;
+                v[i] = sel(ok, ldg16(ok ? base + off : base), z);
+                // advance this row by BK output pixels: q += BK % Q (carry into p), p += BK / Q,
+                // then wrap p into the next image(s)
+                int q = wq_[i] + cd.bk_dq, pq = wp_[i] + cd.bk_dp;
+                if (q >= cd.Q) { q -= cd.Q; ++pq; }
+                int nn = wn_[i];
+                while (pq >= cd.P) { pq -= cd.P; ++nn; }
+                wq_[i] = q;
+                wp_[i] = pq;
+                wn_[i] = nn;
             }
+            knext = k0 + BK;
         }
     }
 
@@ -295,20 +320,27 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
         for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     if (kt0 < kt1) {
-        uint4 ra[4], rb[4];
-        la.load(p, kt0 * BK, ra);
-        lb.load(p, kt0 * BK, rb);
-        la.store(smem, ra);
-        lb.store(smem + TILE_BYTES, rb);
+        // two K-steps of global loads in flight (register sets 0 / 1 alternate): the
+        // 128-row tiles do little MFMA work per K-step, so one step of prefetch left
+        // them latency-bound on the operand loads (im2col gathers above all)
+        uint4 ra0[4], rb0[4], ra1[4], rb1[4];
+        la.load(p, kt0 * BK, ra0);
+        lb.load(p, kt0 * BK, rb0);
+        if (kt0 + 1 < kt1) {
+            la.load(p, (kt0 + 1) * BK, ra1);
+            lb.load(p, (kt0 + 1) * BK, rb1);
+        }
+        la.store(smem, ra0);
+        lb.store(smem + TILE_BYTES, rb0);
         __syncthreads();
-        for (int kt = kt0; kt < kt1; ++kt) {
+        // one K-step: (ran, rbn) hold K-step kt+1, (raf, rbf) are free and receive kt+2
+        auto step = [&](int kt, uint4 (&ran)[4], uint4 (&rbn)[4], uint4 (&raf)[4], uint4 (&rbf)[4]) {
             const int cur = (kt - kt0) & 1;
             char* sa = smem + cur * 2 * TILE_BYTES;
             char* sb = sa + TILE_BYTES;
-            const bool more = kt + 1 < kt1;
-            if (more) {
-                la.load(p, (kt + 1) * BK, ra);
-                lb.load(p, (kt + 1) * BK, rb);
+            if (kt + 2 < kt1) {
+                la.load(p, (kt + 2) * BK, raf);
+                lb.load(p, (kt + 2) * BK, rbf);
             }
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
@@ -323,12 +355,16 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
                     for (int j = 0; j < NJ; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
             }
-            if (more) {
+            if (kt + 1 < kt1) {
                 char* na = smem + (cur ^ 1) * 2 * TILE_BYTES;
-                la.store(na, ra);
-                lb.store(na + TILE_BYTES, rb);
+                la.store(na, ran);
+                lb.store(na + TILE_BYTES, rbn);
             }
             __syncthreads();
+        };
+        for (int kt = kt0; kt < kt1; kt += 2) {
+            step(kt, ra1, rb1, ra0, rb0);
+            if (kt + 1 < kt1) step(kt + 1, ra0, rb0, ra1, rb1);
         }
     }
 
@@ -694,6 +730,8 @@ void fill_conv(ConvDesc& cd, const int* d) {
     cd.fd_Q = make_fastdiv((uint32_t)cd.Q);
     cd.fd_C = make_fastdiv((uint32_t)cd.C);
     cd.fd_S = make_fastdiv((uint32_t)std::max(1, cd.S));
+    cd.bk_dq = BK % std::max(1, cd.Q);
+    cd.bk_dp = BK / std::max(1, cd.Q);
 }
 
 }  // namespace
@@ -726,6 +764,8 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
     p.accumulate = accumulate;
     if (conv) fill_conv(p.cd, conv);
     if (M <= 0 || N <= 0) return 0;
+    // the wgrad im2col loader addresses the activation with 32-bit element offsets
+    if ((mode == 4 || mode == 5) && conv && (long)p.cd.N * p.cd.H * p.cd.W * p.cd.C >= (1L << 31)) return -7;
     if (narrow) {   // 128 x 64 tiles: outputs with 64 (or 64 + k*128) columns waste no MFMA work
         switch (mode) {
             case 0: return launch<KC, KC, 64>(p, workspace, ws_elems, splits, st);

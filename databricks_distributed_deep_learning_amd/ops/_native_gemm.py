@@ -88,14 +88,16 @@ def big_splits(M: int, N: int, K: int) -> int:
 
 
 def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
-    """Split-K only when the tile grid cannot fill the chip; each split keeps >= 8 K-steps."""
+    """Split-K only when the tile grid cannot fill the chip; each split keeps >= 8 K-steps.
+    At most 2 blocks per CU fit (LDS), so tiles * splits stays <= 2 * NUM_CU: one more
+    block than that runs in a second round and doubles the time."""
     if force is not None:
         return max(1, force)
     tiles = -(-M // BM) * -(-N // BN)
     nk = -(-K // BK)
     if tiles >= NUM_CU or nk < 16:
         return 1
-    return max(1, min(-(-2 * NUM_CU // tiles), nk // 8))
+    return max(1, min(2 * NUM_CU // tiles, nk // 8))
 
 
 def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr,
