@@ -203,6 +203,30 @@ DDL_API int ddl_lamb_step(int gdtype, const void* grad, float* master, int pdtyp
     DDL_RETURN_LAUNCH();
 }
 
+// LAMB as two launches, for the sharded optimizer: per-tensor norms of a rank's
+// slice are all-reduced between phase 1 (moments + partial norms) and phase 2
+DDL_API int ddl_lamb_phase1(int gdtype, const void* grad, float* master, float* m, float* v, const int* table,
+                            int nblk, const float* scale, float b1, float b2, float eps, float wd, float bc1, float bc2,
+                            float* norms, hipStream_t st) {
+    const int4* t = (const int4*)table;
+    if (gdtype == 1)
+        lamb_phase1_k<bf16_t><<<nblk, OPT_NT, 0, st>>>((const bf16_t*)grad, master, m, v, t, scale, b1, b2, eps, wd, bc1,
+                                                       bc2, norms);
+    else
+        lamb_phase1_k<float><<<nblk, OPT_NT, 0, st>>>((const float*)grad, master, m, v, t, scale, b1, b2, eps, wd, bc1,
+                                                      bc2, norms);
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_lamb_phase2(float* master, int pdtype, void* param, float* m, float* v, const int* table, int nblk,
+                            float lr, float eps, float wd, float bc1, float bc2, const float* norms, hipStream_t st) {
+    const int4* t = (const int4*)table;
+    if (pdtype == 1)
+        lamb_phase2_k<bf16_t><<<nblk, OPT_NT, 0, st>>>(master, (bf16_t*)param, m, v, t, lr, eps, wd, bc1, bc2, norms);
+    else
+        lamb_phase2_k<float><<<nblk, OPT_NT, 0, st>>>(master, (float*)param, m, v, t, lr, eps, wd, bc1, bc2, norms);
+    DDL_RETURN_LAUNCH();
+}
+
 // out (fp32 scalar, zeroed by caller) += sum(x^2); n % 8 == 0
 DDL_API int ddl_sumsq(int dtype, const void* x, long n, float* out, hipStream_t st) {
     if (n % 8) return -1;

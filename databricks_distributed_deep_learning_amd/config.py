@@ -50,6 +50,7 @@ class TrainConfig:
     grad_reduce_dtype: str = "auto"  # auto|fp32|bf16  all-reduce payload dtype
     broadcast_buffers: bool = False
     sync_bn: bool = False            # SyncBatchNorm: BN statistics summed over all ranks (CV models)
+    zero_optimizer: bool = False     # ZeRO-1: fp32 master + optimizer state sharded 1/world per rank
     # ---- runtime ----------------------------------------------------------
     native: str = "auto"             # auto|on|off  HIP kernels (off = stock torch ops)
     cuda_graph: bool = False         # capture the whole train step in a hipGraph

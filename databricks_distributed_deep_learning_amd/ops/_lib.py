@@ -145,6 +145,8 @@ _SIGS = {
     "ddl_adamw_step": [I, P, P, I, P, P, P, P, I, P, F, F, F, F, F, F, F, P],
     "ddl_lamb_step": [I, P, P, I, P, P, P, P, I, P, F, F, F, F, F, F, F, P, P],
     "ddl_sumsq": [I, P, L, P, P],
+    "ddl_lamb_phase1": [I, P, P, P, P, P, I, P, F, F, F, F, F, F, P, P],
+    "ddl_lamb_phase2": [P, I, P, P, P, P, I, F, F, F, F, F, P, P],
 }
 _fns = {}
 

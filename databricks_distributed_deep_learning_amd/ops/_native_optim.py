@@ -9,26 +9,38 @@ _BLOCK = 8192
 
 
 def _table(opt):
+    """Block table over the arena index range this optimizer updates ([lo, hi): the
+    whole arena, or this rank's slice when sharded -- slices start and end on 64-element
+    boundaries, so rows never straddle another rank's elements)."""
     t = getattr(opt, "_native_table", None)
     if t is None:
         rows = []
         for ti, e in enumerate(opt.arena.entries):
-            s = 0
             n8 = (e.numel + 7) // 8 * 8   # pads are zero and inside the arena's aligned slot
-            while s < n8:
-                ln = min(_BLOCK, n8 - s)
-                rows.append((e.offset + s, ln, ti, 1 if e.decay else 0))
+            a, b = max(e.offset, opt.lo), min(e.offset + n8, opt.hi)
+            s = a
+            while s < b:
+                ln = min(_BLOCK, b - s)
+                rows.append((s, ln, ti, 1 if e.decay else 0))
                 s += ln
+        if not rows:
+            rows.append((opt.lo, 0, 0, 0))
         t = torch.tensor(rows, dtype=torch.int32, device=opt.arena.device)
         opt._native_table = t
     return t
 
 
+def _state(t: torch.Tensor, opt) -> int:
+    """Pointer such that ptr[i] is this rank's state for arena index i (state tensors
+    hold [lo, hi) only when the optimizer is sharded)."""
+    return t.data_ptr() - opt.lo * t.element_size()
+
+
 def _targets(opt):
-    """(master fp32, param-copy or None, pdtype)."""
+    """(master fp32 pointer, param-copy or None, pdtype)."""
     if opt.master is not None:
-        return opt.master, opt.arena.flat, dcode(opt.arena.flat)
-    return opt.arena.flat, None, 0
+        return _state(opt.master, opt), opt.arena.flat, dcode(opt.arena.flat)
+    return opt.arena.flat.data_ptr(), None, 0
 
 
 def _scale_tensor(scale, device):
@@ -41,7 +53,7 @@ def sgd(opt, grad, scale):
     tab = _table(opt)
     master, param, pdt = _targets(opt)
     s = _scale_tensor(scale, grad.device)
-    call("ddl_sgd_step", dcode(grad), p(grad), p(master), pdt, p(param), p(opt.buf), p(tab), tab.shape[0], p(s),
+    call("ddl_sgd_step", dcode(grad), p(grad), master, pdt, p(param), _state(opt.buf, opt), p(tab), tab.shape[0], p(s),
          float(opt.lr), float(opt.momentum), float(opt.weight_decay), int(opt.nesterov), int(opt.step_count == 1))
 
 
@@ -50,7 +62,8 @@ def adamw(opt, grad, scale):
     master, param, pdt = _targets(opt)
     s = _scale_tensor(scale, grad.device)
     t = opt.step_count
-    call("ddl_adamw_step", dcode(grad), p(grad), p(master), pdt, p(param), p(opt.m), p(opt.v), p(tab), tab.shape[0],
+    call("ddl_adamw_step", dcode(grad), p(grad), master, pdt, p(param), _state(opt.m, opt), _state(opt.v, opt),
+         p(tab), tab.shape[0],
          p(s), float(opt.lr), float(opt.b1), float(opt.b2), float(opt.eps), float(opt.weight_decay),
          float(1 - opt.b1 ** t), float(1 - opt.b2 ** t))
 
@@ -63,9 +76,19 @@ def lamb(opt, grad, scale):
     norms = torch.zeros(2 * len(opt.arena.entries), dtype=torch.float32, device=grad.device)
     bc1 = (1 - opt.b1 ** t) if opt.bias_correction else 1.0
     bc2 = (1 - opt.b2 ** t) if opt.bias_correction else 1.0
-    call("ddl_lamb_step", dcode(grad), p(grad), p(master), pdt, p(param), p(opt.m), p(opt.v), p(tab), tab.shape[0],
-         p(s), float(opt.lr), float(opt.b1), float(opt.b2), float(opt.eps), float(opt.weight_decay), float(bc1),
-         float(bc2), p(norms))
+    if opt.shard is None:
+        call("ddl_lamb_step", dcode(grad), p(grad), master, pdt, p(param), p(opt.m), p(opt.v), p(tab), tab.shape[0],
+             p(s), float(opt.lr), float(opt.b1), float(opt.b2), float(opt.eps), float(opt.weight_decay), float(bc1),
+             float(bc2), p(norms))
+        return
+    # sharded: the per-tensor norms of every rank's slice are summed between the phases
+    import torch.distributed as dist
+    m, v = _state(opt.m, opt), _state(opt.v, opt)
+    call("ddl_lamb_phase1", dcode(grad), p(grad), master, m, v, p(tab), tab.shape[0], p(s), float(opt.b1),
+         float(opt.b2), float(opt.eps), float(opt.weight_decay), float(bc1), float(bc2), p(norms))
+    dist.all_reduce(norms)
+    call("ddl_lamb_phase2", master, pdt, p(param), m, v, p(tab), tab.shape[0], float(opt.lr), float(opt.eps),
+         float(opt.weight_decay), float(bc1), float(bc2), p(norms))
 
 
 def global_norm(grad):

@@ -45,7 +45,9 @@ def default_no_decay(name: str, p: torch.Tensor) -> bool:
 
 class ParamArena:
     def __init__(self, named_params: Sequence[Tuple[str, nn.Parameter]], align: int = 64,
-                 reverse: bool = True, no_decay_fn=default_no_decay):
+                 reverse: bool = True, no_decay_fn=default_no_decay, pad_multiple: int = 1):
+        """``pad_multiple``: the flat length is rounded up to a multiple of it (a sharded
+        optimizer needs ``world * align`` so every rank owns an equal, aligned slice)."""
         named_params = [(n, p) for n, p in named_params if p.requires_grad]
         if not named_params:
             raise ValueError("ParamArena: no trainable parameters")
@@ -62,7 +64,9 @@ class ParamArena:
             n = p.numel()
             entries.append(ArenaEntry(name, p, off, n, tuple(p.shape), not no_decay_fn(name, p)))
             off += (n + align - 1) // align * align
-        self.numel = off
+        pad = max(1, int(pad_multiple))
+        self.numel = (off + pad - 1) // pad * pad
+        off = self.numel
         self.entries = entries
         self.flat = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad = torch.zeros(off, dtype=self.dtype, device=self.device)

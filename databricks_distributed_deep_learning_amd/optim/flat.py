@@ -23,20 +23,43 @@ from ..ops import _lib
 
 
 class FlatOptimizer:
+    """``shard=(rank, world)`` -- ZeRO-1: this rank keeps the fp32 master copy and the
+    optimizer state only for its contiguous 1/world slice ``[lo, hi)`` of the arena
+    (the arena is padded to ``world * 64`` elements), updates that slice from the
+    all-reduced gradient and all-gathers the updated compute-dtype parameters.  State
+    memory per rank drops by ``world``; the optimizer kernels see the same arena index
+    space (their state pointers are offset by ``-lo``), so no kernel changes."""
     name = "base"
 
     def __init__(self, arena: ParamArena, lr: float, weight_decay: float = 0.0,
-                 max_grad_norm: float = 0.0):
+                 max_grad_norm: float = 0.0, shard=None):
         self.arena = arena
         self.lr = lr
         self.weight_decay = weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
+        self.shard = None
+        self.lo, self.hi = 0, arena.numel
+        if shard is not None and shard[1] > 1:
+            rank, world = shard
+            if arena.numel % (world * 8):
+                raise ValueError("sharded optimizer: build the arena with pad_multiple = world * 64")
+            size = arena.numel // world
+            self.shard = (rank, world)
+            self.lo, self.hi = rank * size, (rank + 1) * size
         self.master: Optional[torch.Tensor] = None
-        if arena.dtype != torch.float32:
-            self.master = arena.flat.detach().float().clone()
+        if arena.dtype != torch.float32 or self.shard is not None:
+            self.master = arena.flat[self.lo:self.hi].detach().float().clone()
         self._decay_mask: Optional[torch.Tensor] = None
         self.last_grad_norm: Optional[torch.Tensor] = None
+
+    @property
+    def state_numel(self) -> int:
+        """Elements of optimizer state this rank holds (the whole arena unless sharded)."""
+        return self.hi - self.lo
+
+    def _zeros_state(self) -> torch.Tensor:
+        return torch.zeros(self.state_numel, dtype=torch.float32, device=self.arena.device)
 
     # ------------------------------------------------------------------
     @property
@@ -45,8 +68,15 @@ class FlatOptimizer:
 
     def decay_mask(self) -> torch.Tensor:
         if self._decay_mask is None:
-            self._decay_mask = self.arena.decay_mask().to(torch.float32)
+            self._decay_mask = self.arena.decay_mask().to(torch.float32)[self.lo:self.hi]
         return self._decay_mask
+
+    def _all_gather_params(self) -> None:
+        """Every rank's updated slice -> the full compute-dtype arena (in place)."""
+        import torch.distributed as dist
+        flat = self.arena.flat
+        dist.all_gather_into_tensor(flat, flat[self.lo:self.hi].clone() if not flat.is_cuda else
+                                    flat[self.lo:self.hi])
 
     def _native(self) -> bool:
         return _lib.use_native(self.arena.flat)
@@ -78,26 +108,52 @@ class FlatOptimizer:
         if self._native():
             self._step_native(grad, scale)
         else:
-            self._step_torch(grad.float() * scale)
+            self._step_torch(grad[self.lo:self.hi].float() * scale)
             if self.master is not None:
-                self.arena.flat.copy_(self.master)
+                self.arena.flat[self.lo:self.hi].copy_(self.master)
+        if self.shard is not None:
+            self._all_gather_params()
 
     # ------------------------------------------------------------------
+    def _full(self, t: torch.Tensor) -> torch.Tensor:
+        """A sharded state tensor gathered to the whole arena (checkpoints stay
+        independent of the world size)."""
+        if self.shard is None:
+            return t
+        import torch.distributed as dist
+        out = torch.empty(self.arena.numel, dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+
     def state_dict(self) -> Dict[str, object]:
+        """Full-arena tensors on every rank (sharded state is all-gathered: collective)."""
         st = {"name": self.name, "step": self.step_count, "lr": self.lr}
         if self.master is not None:
-            st["master"] = self.master
-        st.update(self._state_tensors())
+            st["master"] = self._full(self.master)
+        st.update({k: self._full(v) for k, v in self._state_tensors().items()})
         return st
+
+    def _fit(self, t: torch.Tensor) -> torch.Tensor:
+        """A full-arena tensor from a checkpoint, resized to this arena (the padding
+        differs between world sizes when the optimizer is sharded)."""
+        n = self.arena.numel
+        if t.numel() == n:
+            return t
+        out = torch.zeros(n, dtype=t.dtype, device=t.device)
+        k = min(n, t.numel())
+        out[:k] = t[:k]
+        return out
 
     def load_state_dict(self, st: Dict[str, object]) -> None:
         self.step_count = int(st["step"])
         self.lr = float(st["lr"])
+        lo, hi = self.lo, self.hi
         if self.master is not None and "master" in st:
-            self.master.copy_(st["master"])
-            self.arena.flat.copy_(self.master)
+            full = self._fit(st["master"])
+            self.master.copy_(full[lo:hi])
+            self.arena.flat.copy_(full.to(self.arena.flat.dtype))
         for k, t in self._state_tensors().items():
-            t.copy_(st[k])
+            t.copy_(self._fit(st[k])[lo:hi])
 
     def _state_tensors(self) -> Dict[str, torch.Tensor]:
         return {}
@@ -106,10 +162,11 @@ class FlatOptimizer:
 class FlatSGD(FlatOptimizer):
     name = "sgd"
 
-    def __init__(self, arena, lr=0.1, momentum=0.9, weight_decay=0.0, nesterov=False, max_grad_norm=0.0):
-        super().__init__(arena, lr, weight_decay, max_grad_norm)
+    def __init__(self, arena, lr=0.1, momentum=0.9, weight_decay=0.0, nesterov=False, max_grad_norm=0.0,
+                 shard=None):
+        super().__init__(arena, lr, weight_decay, max_grad_norm, shard)
         self.momentum, self.nesterov = momentum, nesterov
-        self.buf = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
+        self.buf = self._zeros_state()
 
     def _state_tensors(self):
         return {"momentum_buffer": self.buf}
@@ -133,12 +190,13 @@ class FlatSGD(FlatOptimizer):
 class FlatAdamW(FlatOptimizer):
     name = "adamw"
 
-    def __init__(self, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=0.0):
-        super().__init__(arena, lr, weight_decay, max_grad_norm)
+    def __init__(self, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=0.0,
+                 shard=None):
+        super().__init__(arena, lr, weight_decay, max_grad_norm, shard)
         self.b1, self.b2 = betas
         self.eps = eps
-        self.m = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
-        self.v = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
+        self.m = self._zeros_state()
+        self.v = self._zeros_state()
 
     def _state_tensors(self):
         return {"exp_avg": self.m, "exp_avg_sq": self.v}
@@ -164,13 +222,13 @@ class FlatLAMB(FlatOptimizer):
     name = "lamb"
 
     def __init__(self, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01, max_grad_norm=1.0,
-                 bias_correction=True):
-        super().__init__(arena, lr, weight_decay, max_grad_norm)
+                 bias_correction=True, shard=None):
+        super().__init__(arena, lr, weight_decay, max_grad_norm, shard)
         self.b1, self.b2 = betas
         self.eps = eps
         self.bias_correction = bias_correction
-        self.m = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
-        self.v = torch.zeros(arena.numel, dtype=torch.float32, device=arena.device)
+        self.m = self._zeros_state()
+        self.v = self._zeros_state()
         self.u = torch.empty(0)  # scratch for the torch path
 
     def _state_tensors(self):
@@ -186,28 +244,41 @@ class FlatLAMB(FlatOptimizer):
         u = (self.m / bc1) / ((self.v / bc2).sqrt() + self.eps)
         if self.weight_decay:
             u = u + self.weight_decay * self.decay_mask() * p
+        # per-tensor ||p||^2, ||u||^2 over this rank's part of each tensor (summed over ranks when sharded)
+        segs = []
         for e in self.arena.entries:
-            sl = slice(e.offset, e.offset + e.numel)
-            pn = p[sl].norm()
-            un = u[sl].norm()
+            a, b = max(e.offset, self.lo), min(e.offset + e.numel, self.hi)
+            segs.append((a - self.lo, b - self.lo) if a < b else None)
+        sq = torch.zeros(2 * len(segs), dtype=torch.float32, device=p.device)
+        for ti, sg in enumerate(segs):
+            if sg is not None:
+                sq[2 * ti] = p[sg[0]:sg[1]].pow(2).sum()
+                sq[2 * ti + 1] = u[sg[0]:sg[1]].pow(2).sum()
+        if self.shard is not None:
+            import torch.distributed as dist
+            dist.all_reduce(sq)
+        for ti, sg in enumerate(segs):
+            if sg is None:
+                continue
+            pn, un = sq[2 * ti].sqrt(), sq[2 * ti + 1].sqrt()
             ratio = torch.where((pn > 0) & (un > 0), pn / un, torch.ones_like(pn))
-            p[sl].add_(u[sl] * ratio, alpha=-self.lr)
+            p[sg[0]:sg[1]].add_(u[sg[0]:sg[1]] * ratio, alpha=-self.lr)
 
     def _step_native(self, grad, scale):
         from ..ops import _native_optim
         _native_optim.lamb(self, grad, scale)
 
 
-def build_optimizer(name: str, arena: ParamArena, cfg) -> FlatOptimizer:
+def build_optimizer(name: str, arena: ParamArena, cfg, shard=None) -> FlatOptimizer:
     if name == "sgd":
         return FlatSGD(arena, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
-                       nesterov=cfg.nesterov, max_grad_norm=cfg.max_grad_norm)
+                       nesterov=cfg.nesterov, max_grad_norm=cfg.max_grad_norm, shard=shard)
     if name == "adamw":
         return FlatAdamW(arena, lr=cfg.lr, betas=tuple(cfg.betas), eps=cfg.eps, weight_decay=cfg.weight_decay,
-                         max_grad_norm=cfg.max_grad_norm)
+                         max_grad_norm=cfg.max_grad_norm, shard=shard)
     if name == "lamb":
         return FlatLAMB(arena, lr=cfg.lr, betas=tuple(cfg.betas), eps=cfg.eps, weight_decay=cfg.weight_decay,
-                        max_grad_norm=cfg.max_grad_norm or 1.0)
+                        max_grad_norm=cfg.max_grad_norm or 1.0, shard=shard)
     raise KeyError(name)
 
 

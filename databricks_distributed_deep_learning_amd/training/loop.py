@@ -56,13 +56,15 @@ class Trainer:
             convert_sync_batchnorm(model)
         self.model = model
         self.n_params = count_params(model)
-        self.arena = ParamArena(list(model.named_parameters()))
+        zero = cfg.zero_optimizer and self.world > 1
+        self.arena = ParamArena(list(model.named_parameters()), pad_multiple=self.world * 64 if zero else 1)
         accumulate_fp32 = cfg.grad_accum > 1 and self.dtype != torch.float32
         rd = {"auto": None, "fp32": torch.float32, "bf16": torch.bfloat16}[cfg.grad_reduce_dtype]
         self.ddp = DataParallel(model, self.arena, bucket_mb=cfg.bucket_mb, first_bucket_mb=cfg.first_bucket_mb,
                                 reduce_dtype=rd, broadcast_buffers=cfg.broadcast_buffers,
                                 accumulate_fp32=accumulate_fp32, comm=cfg.comm)
-        self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg)
+        self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg,
+                                   shard=(self.rank, self.world) if zero else None)
         self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
         if cfg.batch_size <= 0:
             cfg.batch_size = self._auto_batch()

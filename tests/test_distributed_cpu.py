@@ -168,6 +168,44 @@ def test_sync_batchnorm_matches_full_batch():
     assert max(out.values()) < 1e-4, out
 
 
+def _zero_equivalence(opt_name):
+    """ZeRO-1 (state sharded 1/world, params all-gathered) == replicated optimizer."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.optim import ParamArena
+    from databricks_distributed_deep_learning_amd.optim.flat import FlatAdamW, FlatLAMB, FlatSGD
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    rank, world = dist.get_rank(), dist.get_world_size()
+    cls = {"sgd": FlatSGD, "adamw": FlatAdamW, "lamb": FlatLAMB}[opt_name]
+    kw = {"sgd": dict(lr=0.1, momentum=0.9, weight_decay=1e-3), "adamw": dict(lr=1e-2, weight_decay=0.01),
+          "lamb": dict(lr=1e-2, weight_decay=0.01)}[opt_name]
+    x, y = _data(16)
+    x, y = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+    finals, state = [], []
+    for shard in (None, (rank, world)):
+        model = _tiny_model()
+        arena = ParamArena(list(model.named_parameters()), pad_multiple=world * 64 if shard else 1)
+        ddp = DataParallel(model, arena, bucket_mb=0.0005, first_bucket_mb=0.0002)
+        opt = cls(arena, shard=shard, **kw)
+        for _ in range(3):
+            ddp.zero_grad()
+            torch.nn.functional.cross_entropy(ddp(x), y).backward()
+            opt.step(ddp.finish(), grad_scale=ddp.grad_scale)
+        finals.append(torch.cat([p.detach().flatten() for p in model.parameters()]))
+        state.append(opt.state_numel)
+        sd = opt.state_dict()          # full-arena tensors even when sharded
+    err = (finals[0] - finals[1]).abs().max().item()
+    return {"err": err, "state": state, "sd_master": sd["master"].numel() if "master" in sd else -1,
+            "arena": arena.numel}
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adamw", "lamb"])
+def test_zero1_sharded_optimizer_matches_replicated(opt_name):
+    out = Distributor(num_processes=2, use_gpu=False).run(_zero_equivalence, opt_name)
+    assert out["err"] < 1e-6, out
+    full, sharded = out["state"]
+    assert sharded * 2 == out["arena"] and full < out["arena"] + 64, out
+
+
 def test_distributor_returns_rank0_value():
     out = Distributor(num_processes=2, use_gpu=False).run(_rank_info, "hello")
     assert out == {"tag": "hello", "rank": 0, "world": 2, "sum": 3.0}
