@@ -124,10 +124,16 @@ __device__ __forceinline__ float erf_fast(float x) {
     return copysignf(1.f - poly * __expf(-ax * ax), x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+// GELU'(x) = Phi(x) + x phi(x): the A&S erf of x/sqrt(2) and the normal density share
+// the one exponential exp(-x^2/2)
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f));
-    const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-    return cdf + x * pdf;
+    const float ax = fabsf(x) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+    const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
+                        0.254829592f) * t;
+    const float e = __expf(-0.5f * x * x);
+    const float erf_v = copysignf(1.f - poly * e, x);
+    return 0.5f * (1.f + erf_v) + x * (0.3989422804014327f * e);
 }
 
 // Counter-based hash RNG: uniform 32-bit value from (seed, index) so dropout

@@ -85,7 +85,7 @@ struct BigParams {
     int tiles_m, tiles_n;
     int ek;                   // register-epilogue variant (EK_*), set by the launcher
 };
-enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3 };
+enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3, EK_DGELU = 4 };
 
 __device__ __forceinline__ int half_off(int buf, int x, int h) { return ((buf * 2 + x) * 2 + h) * HALF; }
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -384,7 +384,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 // a persistent block restage the next tile's operands while this tile drains.
 // Covers bias / residual / ReLU / GELU (+pre-activation) / accumulate / fp32 /
 // split-K partial outputs; tanh, dGELU and row remap take the LDS-staged epilogue.
-__device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const f32x4& a, int split) {
+// `fin` receives the four values as stored (for column statistics of the output)
+__device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const f32x4& a, int split, float* fin) {
     if (m >= p.M || n >= p.N) return;
     const bool full = n + 3 < p.N;
     const int nv = p.N - n;
@@ -413,6 +414,11 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
         if (p.aux) store4g(p.aux + (long)m * p.ldc + n, full, nv, v);   // pre-activation for the backward
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+    } else if (p.act == ACT_DGELU) {
+        float z[4];
+        load4g(p.aux + (long)m * p.ldc + n, full, nv, z);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= gelu_erf_grad(z[r]);
     }
     if (p.out_f32) {
         float* cp = (float*)p.C + (long)m * p.ldc + n;
@@ -433,6 +439,8 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
         }
         store4g(cp, full, nv, v);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fin[r] = v[r];
 }
 
 // Register epilogue of one 256x256 tile.  Lane layout: acc[qm][qn][i][j] holds
@@ -440,6 +448,7 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
 // j*16 + 4*(lane >> 4) .. +3.
 //   EK_BF16: interior tile, bf16 out, optional bf16 bias / residual -- one 8-byte store a site
 //   EK_GELU: interior tile, bf16 out = GELU(acc + bf16 bias), pre-activation to aux
+//   EK_DGELU: interior tile, bf16 out = acc * GELU'(aux) (+ column sums for the bias gradient)
 //   EK_F32 : interior tile, fp32 split-K partial or fp32 out (+accumulate) -- one 16-byte store
 //   EK_GEN : anything direct4 covers, with bounds checks (edge tiles)
 // With colstats (EK_BF16 / EK_GEN) the BatchNorm statistics of the bf16 output --
@@ -449,7 +458,7 @@ template <int EK>
 __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
                                            int wm, int wn, int lane, int split) {
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
-    const bool stats = (EK == EK_BF16 || EK == EK_GEN) && p.colstats;
+    const bool stats = (EK == EK_BF16 || EK == EK_GEN || EK == EK_DGELU) && p.colstats;
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
@@ -487,6 +496,24 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                             *reinterpret_cast<uint2*>(p.aux + o) = make_uint2(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]));
                         *reinterpret_cast<uint2*>((bf16_t*)p.C + o) =
                             make_uint2(pack2bf(gelu_erf(z[0]), gelu_erf(z[1])), pack2bf(gelu_erf(z[2]), gelu_erf(z[3])));
+                    } else if (EK == EK_DGELU) {
+                        // dZ = dH * GELU'(z) (z = the Linear's saved pre-activation), and the
+                        // column sums of the stored dZ: that Linear's bias gradient
+                        float z[4];
+                        const long o = (long)m * p.ldc + n;
+                        load4(p.aux + o, z);
+                        const uint32_t lo = pack2bf(a[0] * gelu_erf_grad(z[0]), a[1] * gelu_erf_grad(z[1]));
+                        const uint32_t hi = pack2bf(a[2] * gelu_erf_grad(z[2]), a[3] * gelu_erf_grad(z[3]));
+                        *reinterpret_cast<uint2*>((bf16_t*)p.C + o) = make_uint2(lo, hi);
+                        if (stats) {
+                            const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                                __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                cs[e] += t[e];
+                                cq[e] += t[e] * t[e];
+                            }
+                        }
                     } else if (EK == EK_F32) {
                         if (p.splits > 1) {
                             *reinterpret_cast<f32x4*>((float*)p.C + split * p.split_stride + (long)m * p.ldc + n) = a;
@@ -495,11 +522,12 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                             *cp = p.accumulate ? a + *cp : a;
                         }
                     } else {
-                        direct4(p, m, n, a, split);
+                        float fin[4] = {0.f, 0.f, 0.f, 0.f};
+                        direct4(p, m, n, a, split, fin);
                         if (stats && m < p.M) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
-                                const float t = bf2f(f2bf(a[e]));
+                                const float t = n + e < p.N ? bf2f(f2bf(fin[e])) : 0.f;
                                 cs[e] += t;
                                 cq[e] += t * t;
                             }
@@ -740,6 +768,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 epi_direct<EK_F32>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_GELU)
                 epi_direct<EK_GELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+            else if (interior && p.ek == EK_DGELU)
+                epi_direct<EK_DGELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else
                 epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             if (!next) return;
@@ -940,16 +970,22 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // register epilogue + persistent grid when the epilogue is one direct4 covers
     // (split-K partials always: the reduce kernel applies the real epilogue)
     const bool direct = direct_enabled() &&
-        (splits > 1 || (!p.row_remap && (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU)));
+        (splits > 1 || (!p.row_remap && (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU ||
+                                          (p.act == ACT_DGELU && p.aux))));
     if (splits > 1 || (p.out_f32 && !p.bias && p.act == ACT_NONE))
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_F32 : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16) && !p.row_remap)
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_BF16 : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_GELU && (!p.bias || p.bias_bf16) && !p.row_remap && !p.res)
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_GELU : EK_GEN;
+    else if (!p.out_f32 && !p.accumulate && p.act == ACT_DGELU && p.aux && !p.bias && !p.row_remap && !p.res)
+        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_DGELU : EK_GEN;
     else
         p.ek = EK_GEN;
     kp.ek = p.ek;
+    // the LDS-staged epilogue sums BatchNorm statistics of the raw accumulator: dGELU
+    // column sums exist on the register epilogue only
+    if (p.colstats && p.act == ACT_DGELU && !direct) return -6;
     const int nwg = p.tiles_m * p.tiles_n;
     int gx = nwg;
     if (direct && splits == 1) {
@@ -993,7 +1029,8 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
     p.res = (const bf16_t*)res; p.accumulate = accumulate; p.out_f32 = out_f32;
     p.row_remap = row_remap; p.zero = (const bf16_t*)zero;
     p.colstats = colstats;
-    if (colstats && (out_f32 || accumulate || splits > 1 || bias || act || res)) return -6;
+    // column statistics: plain bf16 outputs (BatchNorm) or dGELU outputs (the Linear's bias gradient)
+    if (colstats && (out_f32 || accumulate || splits > 1 || bias || (act && act != ACT_DGELU) || res)) return -6;
     if (conv) fill_conv(p.cd, conv);
     switch (mode) {
         case 0: return launch_big<KC, KC>(p, workspace, ws_elems, splits, st);

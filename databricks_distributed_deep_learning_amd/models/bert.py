@@ -99,7 +99,8 @@ class BertLayer(nn.Module):
         ctx = ops.attention(qkv, self.num_heads, mask, self.attn_dropout, self.training)
         h = self.attn_ln(self.attn_out(ctx), residual=h, dropout=self.dropout.p, residual_grad_to=br1)
         br2 = _bridge(h)
-        f = self.ffn_out(self.ffn_in(h, grad_residual=br2))
+        # ffn_in's GELU backward runs in ffn_out's dgrad epilogue (ffn_out is its only consumer)
+        f = self.ffn_out(self.ffn_in(h, grad_residual=br2), fuse_dgelu=True)
         return self.ffn_ln(f, residual=h, dropout=self.dropout.p, residual_grad_to=br2)
 
 

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from ._lib import call, dcode, grad_ready, grad_sink, p
-from ._native_gemm import MODE_NN, MODE_NT, MODE_TN, gemm
+from ._native_gemm import MODE_NN, MODE_NT, MODE_TN, gemm, stats_rows_max
 from . import _native_elementwise as E
 
 
@@ -47,9 +47,14 @@ def _transposed(param, w: torch.Tensor) -> torch.Tensor:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, bridge=None):
+    def forward(ctx, x, w, b, act, bridge=None, fuse_dgelu=False):
         ctx.w_param, ctx.b_param = w, b
         ctx.bridge = bridge
+        # GELU chain (FFN): this layer's input is the output of a GELU Linear whose only
+        # consumer is this layer -> the dgrad epilogue applies that layer's dGELU and
+        # column-sums the result (its bias gradient); see ``_DgeluHandoff``
+        pre = getattr(x, "_ddl_gelu_pre", None) if fuse_dgelu else None
+        ctx.gelu_pre = pre
         K = x.shape[-1]
         N = w.shape[0]
         x2 = x.reshape(-1, K)
@@ -66,7 +71,11 @@ class _Linear(torch.autograd.Function):
         ctx.has_bias = b is not None
         ctx.save_for_backward(x2, w, z if act == "gelu" else (y if act in ("tanh", "relu") else None))
         ctx.xshape = x.shape
-        return y.view(*x.shape[:-1], N)
+        out = y.view(*x.shape[:-1], N)
+        if z is not None:
+            ctx.gelu_token = object()
+            out._ddl_gelu_pre = (z, ctx.gelu_token)
+        return out
 
     @staticmethod
     def backward(ctx, dy):
@@ -77,7 +86,17 @@ class _Linear(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         bias_done = False
-        if ctx.act == "gelu":
+        handoff = getattr(dy, "_ddl_dgelu_done", None) if ctx.act == "gelu" else None
+        if handoff is not None and (handoff.token is not getattr(ctx, "gelu_token", None)
+                                    or handoff.version != dy._version):
+            handoff = None
+        if handoff is not None:
+            # the consumer's dgrad already produced dZ = dH * GELU'(z) and its column sums
+            dz = dy2
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                db_ret = handoff.bias_grad(ctx.b_param, N)
+                bias_done = True
+        elif ctx.act == "gelu":
             dz = torch.empty_like(dy2)
             if ctx.has_bias and ctx.needs_input_grad[2]:
                 # dGELU and the bias gradient (column sums of dz) in one pass
@@ -111,13 +130,28 @@ class _Linear(torch.autograd.Function):
                 res = res.reshape(M, K)
                 if not res.is_contiguous() or res.dtype != dx.dtype:
                     res = res.contiguous().to(dx.dtype)
-            if _DGRAD_NT and M >= 4 * K:
+            pre = ctx.gelu_pre
+            fused = None
+            if pre is not None and res is None and pre[0].shape == (M, K) and _dgelu_fusable(K):
+                # dx := dZ of the producing GELU Linear (dGELU + its bias column sums in the epilogue)
+                part = torch.empty(stats_rows_max(M) * 2 * K, dtype=torch.float32, device=dx.device)
+                if _DGRAD_NT and M >= 4 * K:
+                    nrows = gemm(MODE_NT, dz, N, _transposed(ctx.w_param, w), N, dx, K, M, K, N, act="dgelu",
+                                 aux=pre[0], colstats=part, kernel="big")
+                else:
+                    nrows = gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N, act="dgelu", aux=pre[0], colstats=part,
+                                 kernel="big")
+                fused = _DgeluHandoff(pre[1], part, nrows, K)
+            elif _DGRAD_NT and M >= 4 * K:
                 # dx = dz W as an NT GEMM against W^T (both operands k-contiguous: ds_read_b128
                 # fragments instead of transposed reads); the weight copy is tiny next to dz
                 gemm(MODE_NT, dz, N, _transposed(ctx.w_param, w), N, dx, K, M, K, N, residual=res)
             else:
                 gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N, residual=res)
             dx = dx.view(ctx.xshape)
+            if fused is not None:
+                fused.version = dx._version
+                dx._ddl_dgelu_done = fused
         elif ctx.bridge is not None:
             ctx.bridge.take()
         if ctx.needs_input_grad[1]:
@@ -147,13 +181,42 @@ class _Linear(torch.autograd.Function):
             else:
                 db = torch.empty(N, dtype=w.dtype, device=w.device)
                 E.colsum(dz, db)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
+
+
+def _dgelu_fusable(K: int) -> bool:
+    """dGELU + column sums exist on the 256x256 kernel's register epilogue only."""
+    from . import _native_gemm as NG
+    return os.environ.get("DDL_GEMM_DIRECT", "1") != "0" and NG._big_allowed(MODE_NT, K) and K % 4 == 0
+
+
+class _DgeluHandoff:
+    """Rides on the gradient a GELU-chain consumer returns: the gradient is already
+    dZ = dH * GELU'(z) of the producing Linear, whose bias gradient is the column sum
+    held in ``part`` (one [sum | sumsq] row per 128 output rows).  ``token`` ties it to
+    that producer's forward, ``version`` guards against autograd accumulating anything
+    else into the tensor."""
+    __slots__ = ("token", "part", "nrows", "width", "version")
+
+    def __init__(self, token, part, nrows, width):
+        self.token, self.part, self.nrows, self.width, self.version = token, part, nrows, width, -1
+
+    def bias_grad(self, b_param, N: int):
+        row = torch.empty(2 * self.width, dtype=torch.float32, device=self.part.device)
+        ws = torch.empty(-(-self.nrows // 32) * 2 * self.width, dtype=torch.float32, device=self.part.device)
+        call("ddl_bn_rows_sum", p(self.part), self.nrows, 2 * self.width, p(row), p(ws))
+        sink = grad_sink(b_param)
+        if sink is not None:
+            call("ddl_acc_f32", dcode(sink), p(sink), p(row), N)
+            grad_ready(b_param)
+            return None
+        return row[:N].to(b_param.dtype)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str],
-           bridge=None) -> torch.Tensor:
+           bridge=None, fuse_dgelu: bool = False) -> torch.Tensor:
     if not _ok(x, w) or (b is not None and b.dtype != w.dtype):
         from .bridge import join
         from .linear import linear_reference
         return linear_reference(join(x, bridge), w, b, act)
-    return _Linear.apply(x, w, b, act, bridge)
+    return _Linear.apply(x, w, b, act, bridge, fuse_dgelu)

@@ -253,3 +253,29 @@ def test_big_direct_persistent_epilogue(M, N, K, variant):
         NG.gemm(0, a, K, w, K, c2, N, M, N, K, kernel="big", **kw)
         assert not torch.isnan(c2).any()
         assert torch.equal(c2, c)
+
+
+@pytest.mark.parametrize("M", [4096, 1000])
+def test_ffn_dgelu_handoff(M):
+    """FFN: Linear(gelu) -> Linear(fuse_dgelu=True).  The second layer's dgrad epilogue
+    applies the first layer's dGELU and column-sums its bias gradient; every gradient
+    must match an fp32 reference (M=1000 leaves edge tiles on the general path)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    torch.manual_seed(12)
+    H, I = 768, 3072
+    x = torch.randn(M, H, device=dev).to(torch.bfloat16)
+    w1 = (torch.randn(I, H, device=dev) / H ** 0.5).to(torch.bfloat16)
+    b1 = (torch.randn(I, device=dev) * 0.1).to(torch.bfloat16)
+    w2 = (torch.randn(H, I, device=dev) / I ** 0.5).to(torch.bfloat16)
+    b2 = (torch.randn(H, device=dev) * 0.1).to(torch.bfloat16)
+    a = [t.clone().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    f = [t.float().clone().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    y = ops.linear(ops.linear(a[0], a[1], a[2], "gelu"), a[3], a[4], None, fuse_dgelu=True)
+    yr = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(f[0], f[1], f[2])), f[3], f[4])
+    assert _rel_err(y, yr) < 2e-2
+    dy = torch.randn(M, H, device=dev)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy)
+    for t, r, name in zip(a, f, ("dx", "dw1", "db1", "dw2", "db2")):
+        assert _rel_err(t.grad, r.grad) < 3e-2, name
