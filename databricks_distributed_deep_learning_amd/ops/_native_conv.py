@@ -8,8 +8,10 @@ dgrad   : stride 1 -> a stride-1 conv of dy with the flipped, transposed weight
           zero-insertion, no wasted MFMA work)
 wgrad   : dW[k, (r,s,c)] = sum_m dy[m, k] * im2col(x)[m, (r,s,c)]      mode CONVW,
           split-K over the N*P*Q output pixels with fp32 partial slabs
-Inputs whose channel count is not a multiple of 8 (the RGB stem) are zero-padded
-to 8 channels so every gathered chunk is one 16-byte load.
+Inputs whose channel count is not a multiple of 8 are zero-padded to 8 channels so
+every gathered chunk is one 16-byte load -- except the stride-2 RGB stem, which runs
+as a stride-1 conv of its 2x2 space-to-depth transform (16 channels, 4x4 taps:
+reduction 256 instead of 392; ``_StemConvS2D``).
 """
 from __future__ import annotations
 
@@ -230,10 +232,85 @@ class _Conv(torch.autograd.Function):
         return dx, dw, None, None, None, None
 
 
+def _s2d_input(x, pad):
+    """[N, H, W, C<=4] -> space-to-depth [N, (H+2p)/2, (W+2p)/2, 16]: channel index
+    (dy, dx, c) of the 2x2 pixel block, c padded to 4 (odd padded extents padded by one)."""
+    N, H, W_, C = x.shape
+    Hp, Wp = H + 2 * pad, W_ + 2 * pad
+    Hp2, Wp2 = Hp + Hp % 2, Wp + Wp % 2
+    xp = F.pad(x, (0, 4 - C, pad, pad + Wp2 - Wp, pad, pad + Hp2 - Hp))
+    return xp.view(N, Hp2 // 2, 2, Wp2 // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, Hp2 // 2, Wp2 // 2, 16)
+
+
+def _s2d_weight(w):
+    """[K, R, S, C<=4] (R, S odd) -> [K, ceil(R/2), ceil(S/2), 16] for the stride-1 conv on
+    the space-to-depth input (taps past R / S are zero)."""
+    K, R, S, C = w.shape
+    R2, S2 = (R + 1) // 2, (S + 1) // 2
+    wp = F.pad(w, (0, 4 - C, 0, 2 * S2 - S, 0, 2 * R2 - R))
+    return wp.view(K, R2, 2, S2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(K, R2, S2, 16)
+
+
+def _s2d_weight_grad(dws, w_shape):
+    """Inverse of _s2d_weight for a gradient: [K, R2, S2, 16] -> [K, R, S, C]."""
+    K, R, S, C = w_shape
+    R2, S2 = dws.shape[1], dws.shape[2]
+    d = dws.view(K, R2, S2, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(K, 2 * R2, 2 * S2, 4)
+    return d[:, :R, :S, :C]
+
+
+class _StemConvS2D(torch.autograd.Function):
+    """Stride-2 convolution of a <=4-channel image (the ResNet stem, 7x7/2 on RGB) as a
+    stride-1 convolution of its 2x2 space-to-depth transform: 16 channels (16-byte
+    gathers, no 3->8 channel padding) and a 4x4 kernel, so the implicit GEMM's reduction
+    is 4*4*16 = 256 instead of 7*7*8 = 392.  The input gradient is never needed (image)."""
+
+    @staticmethod
+    def forward(ctx, x, w, pad, stats=None):
+        ctx.w_param = w
+        xs = _s2d_input(x, pad)
+        ws = _s2d_weight(w.contiguous())
+        ctx.save_for_backward(xs)
+        ctx.ws_shape = ws.shape
+        ctx.w_shape = w.shape
+        # output extent: (H + 2p - R) / 2 + 1 = s2d extent - R2 + 1 for R = 2 R2 - 1
+        y = _fwd(xs, ws, 1, 0, stats=stats)
+        N, H, W_, _ = x.shape
+        K, R, S, _ = w.shape
+        P, Q = (H + 2 * pad - R) // 2 + 1, (W_ + 2 * pad - S) // 2 + 1
+        return y if y.shape[1] == P and y.shape[2] == Q else y[:, :P, :Q].contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xs,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dw = None
+        if ctx.needs_input_grad[1]:
+            _, P, Q, _ = dy.shape
+            if xs.shape[1] - ctx.ws_shape[1] + 1 != P or xs.shape[2] - ctx.ws_shape[2] + 1 != Q:
+                xs = xs[:, :P + ctx.ws_shape[1] - 1, :Q + ctx.ws_shape[2] - 1].contiguous()
+            dws = _wgrad(dy, xs, ctx.ws_shape, 1, 0)
+            g = _s2d_weight_grad(dws, ctx.w_shape)
+            sink = grad_sink(ctx.w_param)
+            if sink is not None and sink.shape == g.shape:
+                sink.add_(g)
+                grad_ready(ctx.w_param)
+            else:
+                dw = g.contiguous()
+        return None, dw, None, None
+
+
+_STEM_S2D = os.environ.get("DDL_STEM_S2D", "1") != "0"
+
+
 def conv2d(x, w, stride, padding, bridge=None, stats=None):
     from .bridge import join
     from .conv import conv2d_reference
     C = x.shape[-1]
+    if (_STEM_S2D and stride == 2 and C <= 4 and w.shape[1] % 2 == 1 and w.shape[2] % 2 == 1 and
+            x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and
+            not x.requires_grad and bridge is None):
+        return _StemConvS2D.apply(x, w, padding, stats)
     if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.shape[0] % 8 or C % 8:
         # the bridge attaches to the caller's tensor (before any channel padding)
         x, bridge = join(x, bridge), None

@@ -279,3 +279,23 @@ def test_ffn_dgelu_handoff(M):
     yr.backward(dy)
     for t, r, name in zip(a, f, ("dx", "dw1", "db1", "dw2", "db2")):
         assert _rel_err(t.grad, r.grad) < 3e-2, name
+
+
+@pytest.mark.parametrize("H,W", [(224, 224), (57, 61)])
+def test_stem_space_to_depth(H, W):
+    """7x7/2 RGB stem through the space-to-depth path: forward and weight gradient
+    against fp32 F.conv2d (odd extents exercise the padded block row / column)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    torch.manual_seed(13)
+    x = torch.randn(4, H, W, 3, device=dev).to(torch.bfloat16)
+    w = (torch.randn(64, 7, 7, 3, device=dev) * 0.1).to(torch.bfloat16).requires_grad_(True)
+    y = ops.conv2d(x, w, 2, 3)
+    wr = w.detach().float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    yr = F.conv2d(x.float().permute(0, 3, 1, 2), wr, stride=2, padding=3).permute(0, 2, 3, 1)
+    assert y.shape == yr.shape
+    assert _rel_err(y, yr) < 1e-2
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy)
+    assert _rel_err(w.grad, wr.grad.permute(0, 2, 3, 1)) < 2e-2
