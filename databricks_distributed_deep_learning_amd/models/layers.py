@@ -27,8 +27,9 @@ class Conv2d(nn.Module):
         std = math.sqrt(2.0 / (cout * k * k))
         nn.init.normal_(self.weight, 0.0, std)
 
-    def forward(self, x, grad_residual=None, bn_stats=None):
-        return ops.conv2d(x, self.weight, self.stride, self.padding, grad_residual=grad_residual, bn_stats=bn_stats)
+    def forward(self, x, grad_residual=None, bn_stats=None, grad_to=None):
+        return ops.conv2d(x, self.weight, self.stride, self.padding, grad_residual=grad_residual, bn_stats=bn_stats,
+                          grad_to=grad_to)
 
     def extra_repr(self):
         return f"{self.cin}, {self.cout}, k={self.k}, stride={self.stride}, padding={self.padding}"
@@ -109,11 +110,12 @@ class Linear(nn.Module):
         return f"{self.fin}, {self.fout}, bias={self.bias is not None}, act={self.act}"
 
 
-def conv_bn(conv: "Conv2d", bn: "BatchNorm2d", x, residual=None, grad_residual=None, residual_grad_to=None):
+def conv_bn(conv: "Conv2d", bn: "BatchNorm2d", x, residual=None, grad_residual=None, residual_grad_to=None,
+            grad_to=None):
     """conv -> BatchNorm(+ReLU)(+residual) with the BN statistics produced by the conv's
     GEMM epilogue in training mode (no separate statistics pass over the conv output)."""
     st = BNStats() if bn.training else None
-    y = conv(x, grad_residual=grad_residual, bn_stats=st)
+    y = conv(x, grad_residual=grad_residual, bn_stats=st, grad_to=grad_to)
     return bn(y, residual=residual, residual_grad_to=residual_grad_to, stats=st)
 
 

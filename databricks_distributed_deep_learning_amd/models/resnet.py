@@ -48,8 +48,9 @@ class BasicBlock(nn.Module):
             br = _bridge(x, self.training)
             out = conv_bn(self.conv1, self.bn1, x, grad_residual=br)
             return conv_bn(self.conv2, self.bn2, out, residual=x, residual_grad_to=br)
-        identity = self.downsample(x)
-        out = conv_bn(self.conv1, self.bn1, x)
+        br = _bridge(x, self.training)
+        identity = self.downsample(x, grad_residual=br)
+        out = conv_bn(self.conv1, self.bn1, x, grad_to=br)
         return conv_bn(self.conv2, self.bn2, out, residual=identity)
 
 
@@ -75,8 +76,11 @@ class Bottleneck(nn.Module):
             out = conv_bn(self.conv1, self.bn1, x, grad_residual=br)
             out = conv_bn(self.conv2, self.bn2, out)
             return conv_bn(self.conv3, self.bn3, out, residual=x, residual_grad_to=br)
-        identity = self.downsample(x)
-        out = conv_bn(self.conv1, self.bn1, x)
+        # downsample block: conv1 offers its input gradient to the downsample conv,
+        # whose dgrad epilogue adds it (autograd runs the longer conv1 branch first)
+        br = _bridge(x, self.training)
+        identity = self.downsample(x, grad_residual=br)
+        out = conv_bn(self.conv1, self.bn1, x, grad_to=br)
         out = conv_bn(self.conv2, self.bn2, out)
         return conv_bn(self.conv3, self.bn3, out, residual=identity)
 
@@ -89,8 +93,8 @@ class Downsample(nn.Module):
         self.add_module("0", Conv2d(cin, cout, 1, stride, 0))
         self.add_module("1", BatchNorm2d(cout, relu=False))
 
-    def forward(self, x):
-        return conv_bn(self._modules["0"], self._modules["1"], x)
+    def forward(self, x, grad_residual=None):
+        return conv_bn(self._modules["0"], self._modules["1"], x, grad_residual=grad_residual)
 
 
 class ResNet(nn.Module):

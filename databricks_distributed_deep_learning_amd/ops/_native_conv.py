@@ -88,7 +88,8 @@ def _w_dgrad(w, rs, ss):
 
 
 def _dgrad(dy, w, x_shape, stride, pad, residual=None):
-    """dx (+ ``residual``, added in the GEMM epilogue; stride-1 paths only)."""
+    """dx (+ ``residual``, added in the GEMM epilogue; strided convs add it in place,
+    so there ``residual`` must be a tensor the caller owns)."""
     N, H, W_, C = x_shape
     K, R, S, _ = w.shape
     _, P, Q, _ = dy.shape
@@ -106,8 +107,6 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
              conv=_desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_),
              residual=residual)
         return dx
-    if residual is not None:
-        return _dgrad(dy, w, x_shape, stride, pad).add_(residual)
     # stride s: output-parity classes (a, b); taps r = a+pad (mod s)
     classes = []
     empty = False
@@ -121,7 +120,13 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
                 empty = True
                 continue
             classes.append((a, b, rs, ss, Ho, Wo))
-    dx = (torch.zeros if empty else torch.empty)(N, H, W_, C, dtype=dy.dtype, device=dy.device)
+    if residual is not None:
+        # every output pixel belongs to at most one parity class: each class GEMM adds
+        # the residual in place (epilogue reads res[p] and writes dx[p] in the same
+        # lane); pixels of empty classes keep the residual (their dgrad is zero)
+        dx = residual if residual.is_contiguous() else residual.contiguous()
+    else:
+        dx = (torch.zeros if empty else torch.empty)(N, H, W_, C, dtype=dy.dtype, device=dy.device)
     probs = []
     for a, b, rs, ss, Ho, Wo in classes:
         wc = _w_dgrad(w, rs, ss)                                     # [C, R', S', K]
@@ -131,9 +136,9 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
         probs.append((wc, N * Ho * Wo, Rp * Sp * K,
                       _desc(N, P, Q, K, Ho, Wo, 1, h_off, w_off, -1, -1, Rp, Sp, H, W_, stride, a, b)))
 
-    def serial(out):
+    def serial(out, res=None):
         for wc, Mc, Kc, desc in probs:
-            gemm(MODE_CONV, dy, 0, wc, Kc, out, C, Mc, C, Kc, conv=desc, row_remap=True)
+            gemm(MODE_CONV, dy, 0, wc, Kc, out, C, Mc, C, Kc, conv=desc, row_remap=True, residual=res)
 
     def multi(out, narrow):
         bs = (ctypes.c_void_p * len(probs))(*[pr[0].data_ptr() for pr in probs])
@@ -145,7 +150,9 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None):
         if rc != 0:
             raise RuntimeError(f"ddl_gemm_conv_multi failed: {rc}")
 
-    if 1 < len(probs) <= 4:
+    if residual is not None:
+        serial(dx, dx)
+    elif 1 < len(probs) <= 4:
         key = (tuple(dy.shape), tuple(w.shape), stride, pad)
         choice = _MULTI_CHOICE.get(key)
         if choice is None:
@@ -203,9 +210,10 @@ def _wgrad(dy, x, w_shape, stride, pad, out=None):
 
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, bridge=None, stats=None):
+    def forward(ctx, x, w, stride, pad, bridge=None, stats=None, grad_to=None):
         ctx.w_param = w
         ctx.bridge = bridge
+        ctx.grad_to = grad_to
         x = x.contiguous()
         w = w.contiguous()
         ctx.stride, ctx.pad = stride, pad
@@ -222,6 +230,8 @@ class _Conv(torch.autograd.Function):
             if res is not None:
                 res = res.contiguous().view(x.shape)
             dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad, residual=res)
+            if ctx.grad_to is not None and ctx.grad_to.offer(dx):
+                dx = None       # the sibling conv's dgrad epilogue adds it
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
             if sink is not None and sink.shape == w.shape:
@@ -229,7 +239,7 @@ class _Conv(torch.autograd.Function):
                 grad_ready(ctx.w_param)
             else:
                 dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def _s2d_input(x, pad):
@@ -303,7 +313,7 @@ class _StemConvS2D(torch.autograd.Function):
 _STEM_S2D = os.environ.get("DDL_STEM_S2D", "1") != "0"
 
 
-def conv2d(x, w, stride, padding, bridge=None, stats=None):
+def conv2d(x, w, stride, padding, bridge=None, stats=None, grad_to=None):
     from .bridge import join
     from .conv import conv2d_reference
     C = x.shape[-1]
@@ -320,7 +330,8 @@ def conv2d(x, w, stride, padding, bridge=None, stats=None):
         c8 = (C + 7) // 8 * 8
         x = F.pad(x, (0, c8 - C))
         w = F.pad(w, (0, c8 - C))
-    return _Conv.apply(x, w, stride, padding, bridge, stats)
+        grad_to = None      # the gradient would be the padded tensor's
+    return _Conv.apply(x, w, stride, padding, bridge, stats, grad_to)
 
 
 def conv2d_bias_act(x, w, b, stride, padding, relu=False, residual=None):

@@ -12,6 +12,12 @@ gradient of its output, which only exists after the last BN's backward ran.
 A consumer that finds the bridge empty adds nothing (the producer then returned
 the gradient to autograd as usual), so mixing native and reference ops stays
 correct.
+
+Sibling branches (a downsample block: ``conv1`` and the downsample conv both read
+the block input) have no data dependence between their backward passes, so the
+producer *offers* its gradient: the offer is refused once the consumer has already
+run (``take`` closes the bridge), and the producer then returns the gradient to
+autograd itself.  Either execution order sums both gradients exactly once.
 """
 from __future__ import annotations
 
@@ -21,18 +27,27 @@ import torch
 
 
 class GradBridge:
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "closed")
 
     def __init__(self):
         self.grad: Optional[torch.Tensor] = None
+        self.closed = False
 
     def put(self, g: torch.Tensor) -> None:
         if self.grad is not None:
             raise RuntimeError("GradBridge: gradient already pending (bridge reused within one backward?)")
         self.grad = g
 
+    def offer(self, g: torch.Tensor) -> bool:
+        """Hand ``g`` to the consumer unless it already ran (then the caller keeps it)."""
+        if self.closed:
+            return False
+        self.put(g)
+        return True
+
     def take(self) -> Optional[torch.Tensor]:
         g, self.grad = self.grad, None
+        self.closed = True
         return g
 
 

@@ -25,14 +25,16 @@ def conv2d_reference(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding:
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 0,
-           grad_residual=None, bn_stats=None) -> torch.Tensor:
+           grad_residual=None, bn_stats=None, grad_to=None) -> torch.Tensor:
     """``grad_residual``: a :class:`ops.bridge.GradBridge` whose pending gradient is
     added to this conv's input gradient (fused into the dgrad GEMM epilogue).
+    ``grad_to``: a bridge this conv *offers* its input gradient to (a sibling conv of
+    the same input adds it in its own dgrad epilogue; native path only).
     ``bn_stats``: a :class:`ops.bridge.BNStats` that receives BatchNorm statistics
     partials of the output from the GEMM epilogue (for the BN that follows)."""
     if _lib.use_native(x):
         from . import _native_conv
-        return _native_conv.conv2d(x, w, stride, padding, grad_residual, bn_stats)
+        return _native_conv.conv2d(x, w, stride, padding, grad_residual, bn_stats, grad_to)
     from .bridge import join
     return conv2d_reference(join(x, grad_residual), w, stride, padding)
 

@@ -113,3 +113,19 @@ def test_cast_params_keeps_bn_stats_fp32():
     M.cast_params(m, torch.bfloat16)
     assert all(p.dtype == torch.bfloat16 for p in m.parameters())
     assert m.bn1.running_mean.dtype == torch.float32
+
+
+def test_grad_bridge_offer_either_order():
+    """GradBridge.offer/take: a sibling producer's gradient is summed exactly once
+    whether the consumer runs after it (offer accepted) or before it (offer refused)."""
+    from databricks_distributed_deep_learning_amd.ops.bridge import GradBridge
+    g_prod, g_cons = torch.full((3,), 2.0), torch.full((3,), 5.0)
+    b = GradBridge()                      # producer first
+    assert b.offer(g_prod)
+    r = b.take()
+    total = g_cons + r
+    assert torch.equal(total, torch.full((3,), 7.0))
+    b = GradBridge()                      # consumer first: nothing pending, bridge closes
+    assert b.take() is None
+    assert not b.offer(g_prod)            # producer keeps its gradient for autograd
+    assert b.grad is None

@@ -153,3 +153,33 @@ def test_residual_grad_bridge_matches_autograd_sum():
         assert _rel(out[True][n], out[False][n]) < 3e-2, n
     for n in out[True]:
         assert _rel(out[True][n], out[False][n]) < 0.15, n
+
+
+@pytest.mark.parametrize("kind,stride", [("bottleneck", 1), ("bottleneck", 2), ("basic", 2)])
+def test_downsample_sibling_bridge(kind, stride):
+    """Downsample blocks: conv1 offers its input gradient to the downsample conv, whose
+    dgrad epilogue adds it (in place over the strided parity class for stride 2); the
+    block input's gradient equals autograd's separate sum."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.models import resnet as R
+    from databricks_distributed_deep_learning_amd.models.layers import cast_params
+    torch.manual_seed(3)
+    cin, planes = 64, 32
+    if kind == "bottleneck":
+        blk = R.Bottleneck(cin, planes, stride, R.Downsample(cin, planes * 4, stride))
+    else:
+        blk = R.BasicBlock(cin, planes, stride, R.Downsample(cin, planes, stride))
+    blk = cast_params(blk, torch.bfloat16).to(dev).train()
+    x0 = torch.randn(4, 20, 20, cin, device=dev, dtype=torch.bfloat16)
+    grads = {}
+    for flag in (True, False):
+        R._BRIDGE = flag
+        try:
+            b = copy.deepcopy(blk)
+            x = x0.clone().requires_grad_(True)
+            y = b(x)
+            y.backward(torch.ones_like(y) * 0.01 + (y.detach() * 0.1))
+            grads[flag] = x.grad.float()
+        finally:
+            R._BRIDGE = True
+    assert _rel(grads[True], grads[False]) < 1e-2
