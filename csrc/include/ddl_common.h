@@ -159,6 +159,30 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t 
 
 // Fast unsigned division by a runtime constant (magic multiply), for index math
 // in hot loops: q = umulhi(n, mul) >> shift, exact for n < 2^31.
+// BatchNorm-backward GEMM epilogue (ACT_BNB) side arguments: the BN's ReLU bit mask
+// (nullable), saved mean and inverse std.  Set on the launching host thread by
+// ddl_gemm_bnb(), consumed by the next GEMM entry call (gemm.hip / gemm_big.hip).
+struct BnbArgs {
+    const uint8_t* mask;
+    const float* mean;
+    const float* istd;
+};
+BnbArgs ddl_take_bnb();
+
+// Sum over the 16 lanes of a DPP row (every lane of the row gets the total):
+// xor 1, xor 2 (quad_perm), then half-row and row mirrors -- four DPP adds, no LDS.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                                     false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);   // row_half_mirror
+    return dpp_add<0x140>(v);   // row_mirror
+}
+
 struct FastDiv {
     uint32_t d, mul, shift;
 };

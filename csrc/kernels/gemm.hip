@@ -32,7 +32,7 @@ constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;   // 16 KB per operand tile
 
 enum Layout { KC = 0, KO = 1, CONV = 2, CONVW = 3 };
-enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4 };
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4, ACT_BNB = 5 };
 
 struct ConvDesc {
     int N, H, W, C;                 // input NHWC
@@ -65,6 +65,12 @@ struct Params {
     long ldw;         // split-K slab row stride
     const bf16_t* res;  // optional residual added before the activation (same layout as C)
     int accumulate;     // C += result (gradient accumulation straight into the parameter-grad arena)
+    // ACT_BNB (BatchNorm backward fused into the dgrad that produces the BN output's
+    // gradient): C = (acc + res) * relu_mask, colstats = [sum C | sum C * xhat] with
+    // xhat = (aux - bn_mean) * bn_istd -- the BN backward's reduction pass
+    const uint8_t* bn_mask;
+    const float* bn_mean;
+    const float* bn_istd;
     ConvDesc cd;
     int tiles_m, tiles_n;
 };
@@ -288,7 +294,9 @@ __device__ __forceinline__ long out_row(const Params& p, int m) {
     return ((long)n * cd.OH + pp * cd.ostep + cd.oa) * cd.OW + qq * cd.ostep + cd.ob;
 }
 
-template <int LA, int LB, int BNT>
+// BNB: the BatchNorm-backward epilogue variant (own instantiation: its registers
+// never weigh on the other epilogues)
+template <int LA, int LB, int BNT, bool BNB = false>
 __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
     constexpr int WN = BNT / 2;        // wave tile N extent (64 or 32)
     constexpr int NJ = WN / 16;        // MFMA column tiles per wave
@@ -375,8 +383,55 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) st_s[j][r] = st_q[j][r] = 0.f;
+    if constexpr (BNB) {
+        // BatchNorm backward (N % 8 == 0: a site is whole or outside): dz = (acc + res) *
+        // relu_mask stored, column sums of dz and dz * xhat.  Pass 1 puts every site's
+        // loads in flight at once (clamped addresses; out-of-range sites are dropped in
+        // pass 2) -- one site at a time the epilogue is load-latency bound.
+        uint2 xr[4][NJ], rr[4][NJ];
+        uint32_t mb[4][NJ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long mc = min(m0 + wm * 64 + i * 16 + (lane & 15), p.M - 1);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int nc = min(n0 + wn * WN + j * 16 + 4 * g, p.N - 4);
+                const long o = mc * p.ldc + nc;
+                xr[i][j] = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + o);
+                rr[i][j] = p.res ? *reinterpret_cast<const uint2*>(p.res + o) : make_uint2(0u, 0u);
+                mb[i][j] = p.bn_mask ? (uint32_t)p.bn_mask[o >> 3] >> (nc & 4) : 0xfu;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WN + j * 16 + 4 * g;
+            float mu[4], is[4];
+            load4(p.bn_mean + min(n, p.N - 4), mu);
+            load4(p.bn_istd + min(n, p.N - 4), is);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+                if (m >= p.M || n >= p.N) continue;
+                const float xv[4] = {__uint_as_float(xr[i][j].x << 16), __uint_as_float(xr[i][j].x & 0xffff0000u),
+                                     __uint_as_float(xr[i][j].y << 16), __uint_as_float(xr[i][j].y & 0xffff0000u)};
+                const float rv[4] = {__uint_as_float(rr[i][j].x << 16), __uint_as_float(rr[i][j].x & 0xffff0000u),
+                                     __uint_as_float(rr[i][j].y << 16), __uint_as_float(rr[i][j].y & 0xffff0000u)};
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = ((mb[i][j] >> r) & 1u) ? acc[i][j][r] + rv[r] : 0.f;
+                store4((bf16_t*)p.C + (long)m * p.ldc + n, v);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float q = bf2f(f2bf(v[r]));     // what the BN backward reads
+                    st_s[j][r] += q;
+                    st_q[j][r] += q * (xv[r] - mu[r]) * is[r];
+                }
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+        if constexpr (BNB) break;
         const int m = m0 + wm * 64 + i * 16 + (lane & 15);
         if (m >= p.M) continue;
         const long orow = out_row(p, m);
@@ -506,12 +561,8 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float a = st_s[j][r], b = st_q[j][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    a += __shfl_xor(a, o);
-                    b += __shfl_xor(b, o);
-                }
+                // the 16 lanes holding these columns are one DPP row
+                const float a = row16_sum(st_s[j][r]), b = row16_sum(st_q[j][r]);
                 if ((lane & 15) == 0) {
                     const int col = wn * WN + j * 16 + 4 * g + r;
                     atomicAdd(&red[col], a);
@@ -529,10 +580,10 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
     }
 }
 
-template <int LA, int LB, int BNT>
+template <int LA, int LB, int BNT, bool BNB = false>
 __global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
     __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
-    gemm_body<LA, LB, BNT>(p, smem);
+    gemm_body<LA, LB, BNT, BNB>(p, smem);
 }
 
 // Several independent GEMMs of one shape class in one launch (blockIdx.z picks the
@@ -698,6 +749,13 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
         p.accumulate = 0;
     }
     dim3 grid(p.tiles_m * p.tiles_n, splits);
+    if (p.act == ACT_BNB) {
+        if constexpr (LB == KC && (LA == KC || LA == CONV)) {   // dgrad operand layouts
+            hipLaunchKernelGGL((gemm_k<LA, LB, BNT, true>), grid, dim3(NT), 0, st, p);
+            return (int)hipGetLastError();
+        }
+        return -8;
+    }
     hipLaunchKernelGGL((gemm_k<LA, LB, BNT>), grid, dim3(NT), 0, st, p);
     if (splits > 1) {
         const long total = (long)p.M * p.N;
@@ -759,7 +817,16 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
     mode &= 15;
     if (p.trans_out && (bias || act || res || row_remap)) return -5;
     p.colstats = colstats;
-    if (colstats && (p.trans_out || out_f32 || accumulate || (splits > 1) || bias || act || res)) return -6;
+    if (act == ACT_BNB) {
+        const BnbArgs bn = ddl_take_bnb();
+        // whole-K tiles writing a dense bf16 [M, C] gradient: the mask is indexed by element
+        if (!colstats || !aux || !bn.mean || !bn.istd || ldc != N || N % 8 || p.trans_out || out_f32 || accumulate ||
+            splits > 1 || bias || row_remap)
+            return -8;
+        p.bn_mask = bn.mask; p.bn_mean = bn.mean; p.bn_istd = bn.istd;
+    } else if (colstats && (p.trans_out || out_f32 || accumulate || (splits > 1) || bias || act || res)) {
+        return -6;
+    }
     p.res = (const bf16_t*)res;
     p.accumulate = accumulate;
     if (conv) fill_conv(p.cd, conv);
@@ -789,6 +856,20 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
 }
 
 
+
+static thread_local BnbArgs t_bnb{};
+
+BnbArgs ddl_take_bnb() {
+    const BnbArgs a = t_bnb;
+    t_bnb = BnbArgs{};
+    return a;
+}
+
+// ACT_BNB side arguments for the next GEMM call on this thread (see BnbArgs)
+DDL_API int ddl_gemm_bnb(const void* mask, const float* mean, const float* istd) {
+    t_bnb = BnbArgs{(const uint8_t*)mask, mean, istd};
+    return 0;
+}
 
 // colstats (nullable): BN statistics partials of the output, one row pair per 128-row tile
 DDL_API int ddl_gemm(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,

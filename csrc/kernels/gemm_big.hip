@@ -48,7 +48,7 @@ constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
 
 enum Layout { KC = 0, KO = 1, CONV = 2, CONVW = 3 };
-enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4 };
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4, ACT_BNB = 5 };
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_v4;
@@ -84,8 +84,11 @@ struct BigParams {
     ConvDesc cd;
     int tiles_m, tiles_n;
     int ek;                   // register-epilogue variant (EK_*), set by the launcher
+    const uint8_t* bn_mask;   // ACT_BNB: BatchNorm backward reduction fused into the dgrad (gemm.hip Params)
+    const float* bn_mean;
+    const float* bn_istd;
 };
-enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3, EK_DGELU = 4 };
+enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3, EK_DGELU = 4, EK_BNB = 5, EK_BNBC = 6 };
 
 __device__ __forceinline__ int half_off(int buf, int x, int h) { return ((buf * 2 + x) * 2 + h) * HALF; }
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -364,19 +367,6 @@ __device__ __forceinline__ void epilogue4(const BigParams& p, long orow, int n, 
     }
 }
 
-// Sum over the 16 lanes of a DPP row (every lane of the row gets the total):
-// xor 1, xor 2 (quad_perm), then half-row and row mirrors -- four DPP adds, no LDS.
-template <int CTRL>
-__device__ __forceinline__ float dpp_add(float v) {
-    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
-                                                                     false));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-    v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
-    v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
-    v = dpp_add<0x141>(v);   // row_half_mirror
-    return dpp_add<0x140>(v);   // row_mirror
-}
 
 // Direct epilogue site: the MFMA output layout gives a lane 4 consecutive
 // columns of one row, so a site is finished in registers and written with one
@@ -458,15 +448,64 @@ template <int EK>
 __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
                                            int wm, int wn, int lane, int split) {
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
-    const bool stats = (EK == EK_BF16 || EK == EK_GEN || EK == EK_DGELU) && p.colstats;
+    const bool stats = (EK == EK_BF16 || EK == EK_GEN || EK == EK_DGELU || EK == EK_BNB || EK == EK_BNBC) &&
+                       p.colstats;
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int n = n0 + qn * 128 + wn * 32 + j * 16 + g4;
-            float bv[4] = {0.f, 0.f, 0.f, 0.f};
+            float bv[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
             if ((EK == EK_BF16 || EK == EK_GELU) && p.bias) load4((const bf16_t*)p.bias + n, bv);
+            if (EK == EK_BNB || EK == EK_BNBC) {   // BN mean / inverse std of these 4 channels
+                load4(p.bn_mean + min(n, p.N - 4), bv);
+                load4(p.bn_istd + min(n, p.N - 4), rs);
+            }
             float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+            if (EK == EK_BNB || EK == EK_BNBC) {
+                // BatchNorm backward (N % 8 == 0: a site is whole or outside): dz = (acc + res) *
+                // relu_mask stored, column sums of dz and dz * xhat.  The column group's 8
+                // sites issue their loads together (clamped addresses, out-of-range sites
+                // dropped afterwards): one site at a time the epilogue is load-latency bound.
+                const int nc = min(n, p.N - 4);
+                uint2 xr[2][4], rr[2][4];
+                uint32_t mb[2][4];
+#pragma unroll
+                for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const long mc = min(m0 + qm * 128 + wm * 64 + i * 16 + r16, p.M - 1);
+                        const long o = mc * p.ldc + nc;
+                        xr[qm][i] = *reinterpret_cast<const uint2*>(p.aux + o);
+                        rr[qm][i] = p.res ? *reinterpret_cast<const uint2*>(p.res + o) : make_uint2(0u, 0u);
+                        mb[qm][i] = p.bn_mask ? (uint32_t)p.bn_mask[o >> 3] >> (nc & 4) : 0xfu;
+                    }
+#pragma unroll
+                for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = m0 + qm * 128 + wm * 64 + i * 16 + r16;
+                        if (EK == EK_BNBC && (m >= p.M || n >= p.N)) continue;
+                        const f32x4& a = acc[qm][qn][i][j];
+                        const uint2 x2 = xr[qm][i], r2 = rr[qm][i];
+                        const float xv[4] = {__uint_as_float(x2.x << 16), __uint_as_float(x2.x & 0xffff0000u),
+                                             __uint_as_float(x2.y << 16), __uint_as_float(x2.y & 0xffff0000u)};
+                        const float rv[4] = {__uint_as_float(r2.x << 16), __uint_as_float(r2.x & 0xffff0000u),
+                                             __uint_as_float(r2.y << 16), __uint_as_float(r2.y & 0xffff0000u)};
+                        float v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = ((mb[qm][i] >> e) & 1u) ? a[e] + rv[e] : 0.f;
+                        const uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+                        *reinterpret_cast<uint2*>((bf16_t*)p.C + (long)m * p.ldc + n) = make_uint2(lo, hi);
+                        const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                            __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            cs[e] += t[e];
+                            cq[e] += t[e] * (xv[e] - bv[e]) * rs[e];
+                        }
+                    }
+            } else
 #pragma unroll
             for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -559,7 +598,9 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
 // stages the next tile's first K-tile, stores this tile from registers, then
 // stages the rest of the prologue, so the result stores drain under the next
 // tile's loads instead of in a chip-wide burst between waves of blocks.
-template <int LA, int LB, bool KTAIL, bool DIRECT>
+// BNB: the BatchNorm-backward epilogue variant (its own instantiation, so the extra
+// registers it needs never weigh on the other epilogues)
+template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
     const int nwg = p.tiles_m * p.tiles_n;
@@ -762,7 +803,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             }
             // interior tiles take a lean variant (no bounds checks, one store per site);
             // edge tiles and the rarer epilogue options the general one
-            if (interior && p.ek == EK_BF16)
+            if (BNB)   // checked on every tile: a lean interior twin spills (measured slower)
+                epi_direct<EK_BNBC>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+            else if (interior && p.ek == EK_BF16)
                 epi_direct<EK_BF16>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_F32)
                 epi_direct<EK_F32>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
@@ -971,7 +1014,7 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // (split-K partials always: the reduce kernel applies the real epilogue)
     const bool direct = direct_enabled() &&
         (splits > 1 || (!p.row_remap && (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU ||
-                                          (p.act == ACT_DGELU && p.aux))));
+                                          (p.act == ACT_DGELU && p.aux) || p.act == ACT_BNB)));
     if (splits > 1 || (p.out_f32 && !p.bias && p.act == ACT_NONE))
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_F32 : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16) && !p.row_remap)
@@ -986,6 +1029,7 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     // the LDS-staged epilogue sums BatchNorm statistics of the raw accumulator: dGELU
     // column sums exist on the register epilogue only
     if (p.colstats && p.act == ACT_DGELU && !direct) return -6;
+    if (p.act == ACT_BNB && (!direct || splits > 1)) return -8;   // register epilogue only
     const int nwg = p.tiles_m * p.tiles_n;
     int gx = nwg;
     if (direct && splits == 1) {
@@ -997,6 +1041,14 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     }
     const dim3 grid(gx, splits);
     if (direct) {
+        if constexpr (LB == KC && (LA == KC || LA == CONV)) {   // dgrad operand layouts
+            if (p.act == ACT_BNB) {
+                if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true, true>), grid, dim3(NTH), 0, st, kp);
+                else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true, true>), grid, dim3(NTH), 0, st, kp);
+                return (int)hipGetLastError();
+            }
+        }
+        if (p.act == ACT_BNB) return -8;
         if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true>), grid, dim3(NTH), 0, st, kp);
         else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true>), grid, dim3(NTH), 0, st, kp);
     } else {
@@ -1030,7 +1082,15 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
     p.row_remap = row_remap; p.zero = (const bf16_t*)zero;
     p.colstats = colstats;
     // column statistics: plain bf16 outputs (BatchNorm) or dGELU outputs (the Linear's bias gradient)
-    if (colstats && (out_f32 || accumulate || splits > 1 || bias || (act && act != ACT_DGELU) || res)) return -6;
+    if (act == ACT_BNB) {
+        const BnbArgs bn = ddl_take_bnb();
+        if (!colstats || !aux || !bn.mean || !bn.istd || ldc != N || N % 8 || out_f32 || accumulate || splits > 1 ||
+            bias || row_remap)
+            return -8;
+        p.bn_mask = bn.mask; p.bn_mean = bn.mean; p.bn_istd = bn.istd;
+    } else if (colstats && (out_f32 || accumulate || splits > 1 || bias || (act && act != ACT_DGELU) || res)) {
+        return -6;
+    }
     if (conv) fill_conv(p.cd, conv);
     switch (mode) {
         case 0: return launch_big<KC, KC>(p, workspace, ws_elems, splits, st);

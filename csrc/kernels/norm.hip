@@ -880,9 +880,10 @@ DDL_API int ddl_bn_bwd_partials(int dtype, const void* dy, const void* mask, con
 // coefficients use the global row count M_total, the apply walks the local M rows
 template <typename T>
 static void bn_bwd_finish_t(const T* dy, const uint8_t* mk, const T* x, const float* mean, const float* invstd,
-                            const T* gamma, long M, long M_total, int C, int relu, const float* row, T* dgamma,
-                            T* dbeta, float* coef, T* dx, T* dres, int acc, hipStream_t st) {
-    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(row, 1, C, M_total, gamma, invstd, dgamma, dbeta, coef, acc);
+                            const T* gamma, long M, long M_total, int C, int relu, const float* row, int nrows,
+                            T* dgamma, T* dbeta, float* coef, T* dx, T* dres, int acc, hipStream_t st) {
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(row, nrows, C, M_total, gamma, invstd, dgamma, dbeta, coef,
+                                                         acc);
     if (rows_ok(C)) {
         const int gr = rows_grid(M, C);
         if (relu) {
@@ -903,9 +904,25 @@ DDL_API int ddl_bn_bwd_finish(int dtype, const void* dy, const void* mask, const
     const uint8_t* mk = (const uint8_t*)mask;
     if (dtype == 1)
         bn_bwd_finish_t((const bf16_t*)dy, mk, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M, M_total, C,
-                        relu, row, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
+                        relu, row, 1, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
     else
         bn_bwd_finish_t((const float*)dy, mk, (const float*)x, mean, invstd, (const float*)gamma, M, M_total, C,
-                        relu, row, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st);
+                        relu, row, 1, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st);
+    DDL_RETURN_LAUNCH();
+}
+
+// backward from [sum dz | sum dz*xhat] partial rows written by the dgrad GEMM that
+// produced dz (ACT_BNB epilogue: dz already carries the ReLU mask); ws: ceil(nrows/32) * 2C
+// floats for the 32:1 collapse (may be null when nrows <= 256)
+DDL_API int ddl_bn_bwd_from_partials(int dtype, const float* part, int nrows, float* ws, long ws_elems,
+                                     const void* dz, const void* x, const float* mean, const float* invstd,
+                                     const void* gamma, long M, int C, void* dgamma, void* dbeta, float* coef, void* dx,
+                                     void* dres, int acc_params, hipStream_t st) {
+    if (!rows_ok(C) || dtype != 1) return -1;
+    const long need = ddl_bn_partials_ws(nrows, C);
+    if (need > 0 && (!ws || ws_elems < need)) return -2;
+    const float* fin = need > 0 ? collapse_partials(part, nrows, 2 * C, st, ws) : part;
+    bn_bwd_finish_t((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M, M, C, 0, fin,
+                    nrows, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
     DDL_RETURN_LAUNCH();
 }

@@ -24,13 +24,14 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import grad_ready, grad_sink
 from ._native_gemm import MODE_CONV, MODE_CONVW, MODE_NN, MODE_NT, MODE_TN, gemm, plan, stats_rows_max
+from ._native_norm import _BN_BWD_EPI, _BN_BWD_EPI_RES
 
 
 def _desc(N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep=1, oa=0, ob=0):
     return [N, H, W, C, P, Q, stride, h_off, w_off, h_step, w_step, R, S, OH, OW, ostep, oa, ob]
 
 
-STATS_MIN_K = int(os.environ.get("DDL_BN_STATS_MIN_K", "2048"))
+STATS_MIN_K = int(os.environ.get("DDL_BN_STATS_MIN_K", "0"))
 STATS_EPILOGUE = os.environ.get("DDL_BN_STATS_EPI", "1") != "0"   # 0: always a separate statistics pass
 _DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
@@ -50,10 +51,10 @@ def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
     desc = None if plain11 else _desc(N, H, W_, C, P, Q, stride, -pad, -pad, 1, 1, R, S, P, Q)
     if STATS_EPILOGUE and stats is not None and bias is None and act is None and residual is None and x.is_cuda:
         # BatchNorm statistics from the GEMM epilogue instead of a separate read pass
-        # over y: nearly free in the 256x256 kernel's register epilogue (a 16-lane
-        # shuffle reduction per tile), so taken whenever that is this shape's tuned
-        # kernel; the 128-row kernels' LDS-staged statistics only pay off on long K
-        # loops (scripts/debug/stats_overhead.py: break-even near K=1152)
+        # over y: nearly free in the 256x256 kernel's register epilogue and, since the
+        # 128-row kernels reduce with DPP row sums too, on every tuned kernel
+        # (DDL_BN_STATS_MIN_K=0 measured +0.3% on ResNet-50 over 2048; a positive value
+        # restricts shorter reductions to shapes whose tuned kernel is the 256x256 one)
         if R * S * C >= STATS_MIN_K:
             use = True
         elif plain11:
@@ -87,25 +88,46 @@ def _w_dgrad(w, rs, ss):
     return out
 
 
-def _dgrad(dy, w, x_shape, stride, pad, residual=None):
+def _bnb_dgrad(mode, dy, lda, wt, ldb, dx, M, C, K, conv, residual, hint):
+    """The dgrad GEMM with the consumer BatchNorm's backward reduction in its epilogue
+    (``hint``: ops.bridge.BNBackward) when the tuned plain kernel runs whole-K tiles;
+    returns False (nothing launched) otherwise."""
+    kind, splits = plan(mode, dy, lda, wt, ldb, dx, C, M, C, K, conv=conv, residual=residual, full=True)
+    if splits != 1 or kind.startswith("t"):
+        return False
+    rows = stats_rows_max(M)
+    part = torch.empty((rows + -(-rows // 32)) * 2 * C, dtype=torch.float32, device=dx.device)
+    # the fused epilogue moves the balance toward memory: its kernel is tuned on its own
+    nrows = gemm(mode, dy, lda, wt, ldb, dx, C, M, C, K, act="bnb", aux=hint.x, conv=conv, residual=residual,
+                 colstats=part, bnb=(hint.mask, hint.mean, hint.istd))
+    hint.set(dx, part, nrows)
+    return True
+
+
+def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
     """dx (+ ``residual``, added in the GEMM epilogue; strided convs add it in place,
     so there ``residual`` must be a tensor the caller owns)."""
     N, H, W_, C = x_shape
     K, R, S, _ = w.shape
     _, P, Q, _ = dy.shape
+    bnb = bnb if (_BN_BWD_EPI and bnb is not None and dy.dtype == torch.bfloat16 and C % 8 == 0
+                  and tuple(bnb.x.shape) == tuple(x_shape) and (residual is None or _BN_BWD_EPI_RES)) else None
     if R == 1 and S == 1 and stride == 1 and pad == 0:
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
         if _DGRAD_NT:   # NT against W^T (k-contiguous operands; the weight copy is tiny)
-            gemm(MODE_NT, dy, K, _w_dgrad(w, [0], [0]).view(C, K), K, dx, C, N * H * W_, C, K, residual=residual)
+            wt = _w_dgrad(w, [0], [0]).view(C, K)
+            if bnb is None or not _bnb_dgrad(MODE_NT, dy, K, wt, K, dx, N * H * W_, C, K, None, residual, bnb):
+                gemm(MODE_NT, dy, K, wt, K, dx, C, N * H * W_, C, K, residual=residual)
         else:
             gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K, residual=residual)
         return dx
     if stride == 1:
         wt = _w_dgrad(w, list(range(R - 1, -1, -1)), list(range(S - 1, -1, -1)))   # flipped [C, R, S, K]
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
-        gemm(MODE_CONV, dy, 0, wt, R * S * K, dx, C, N * H * W_, C, R * S * K,
-             conv=_desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_),
-             residual=residual)
+        desc = _desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_)
+        if bnb is None or not _bnb_dgrad(MODE_CONV, dy, 0, wt, R * S * K, dx, N * H * W_, C, R * S * K, desc,
+                                         residual, bnb):
+            gemm(MODE_CONV, dy, 0, wt, R * S * K, dx, C, N * H * W_, C, R * S * K, conv=desc, residual=residual)
         return dx
     # stride s: output-parity classes (a, b); taps r = a+pad (mod s)
     classes = []
@@ -214,6 +236,9 @@ class _Conv(torch.autograd.Function):
         ctx.w_param = w
         ctx.bridge = bridge
         ctx.grad_to = grad_to
+        # input is a training BatchNorm's output: its backward reduction can ride this dgrad
+        # (not when the gradient is offered to a sibling conv, which adds unmasked terms)
+        ctx.bnb = getattr(x, "_ddl_bnb", None) if grad_to is None else None
         x = x.contiguous()
         w = w.contiguous()
         ctx.stride, ctx.pad = stride, pad
@@ -229,7 +254,8 @@ class _Conv(torch.autograd.Function):
             res = ctx.bridge.take() if ctx.bridge is not None else None
             if res is not None:
                 res = res.contiguous().view(x.shape)
-            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad, residual=res)
+            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad, residual=res, bnb=ctx.bnb)
+            ctx.bnb = None
             if ctx.grad_to is not None and ctx.grad_to.offer(dx):
                 dx = None       # the sibling conv's dgrad epilogue adds it
         if ctx.needs_input_grad[1]:

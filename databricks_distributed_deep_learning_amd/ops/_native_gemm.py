@@ -14,12 +14,13 @@ from ._lib import I, L, P
 
 _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_n64": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
-               "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P]})
+               "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
+               "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
 MODE_CONVW_A = 5      # conv wgrad with the im2col operand on the M side (computes dW^T)
 TRANS_OUT = 16        # flag: the kernel stores C^T
-ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4}
+ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4, "bnb": 5}
 BM = BN = 128
 BK = 64
 NUM_CU = 256
@@ -101,7 +102,7 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
 
 
 def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr,
-            row_remap, residual, accumulate, colstats=None) -> None:
+            row_remap, residual, accumulate, colstats=None, bnb=None) -> None:
     if kind.startswith("t"):
         # weight-gradient GEMMs computed transposed (operands swapped, C^T stored): a
         # 64-wide output-channel side lands on the tile's N extent (128x64 tiles)
@@ -116,6 +117,8 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
             ACT[act], _lib.p(aux), out_f32, s, _lib.p(ws), 0 if ws is None else ws.numel(), conv_arr,
             int(row_remap), _lib.p(residual), int(accumulate))
     cs = _lib.p(colstats)
+    if bnb is not None:   # ACT_BNB side arguments (mask, mean, invstd), consumed by this launch
+        _lib.fn("ddl_gemm_bnb")(_lib.p(bnb[0]), _lib.p(bnb[1]), _lib.p(bnb[2]))
     if kind == "big":
         rc = _lib.fn("ddl_gemm_big2")(*args, _zero_page(C.device).data_ptr(), cs, _lib.stream())
     elif kind == "narrow":
@@ -207,7 +210,7 @@ def _time_runs(run, reps: int) -> float:
 
 
 def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap, residual,
-          colstats=None):
+          colstats=None, bnb=None):
     plain = bias is None and act is None and residual is None and aux is None and not row_remap
     cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain)
     cs_s = None
@@ -223,7 +226,7 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     timed = []
     for kind, s in cands:
         run = lambda: _launch(kind, s, mode, A, lda, B, ldb, Cs, ldc, M, N, K, bias, act, aux_s,  # noqa: E731
-                              conv_arr, row_remap, residual, False, cs_s)
+                              conv_arr, row_remap, residual, False, cs_s, bnb)
         run()
         t = _time_runs(run, 2)
         if t < 0.25:                      # short kernels: average more runs (timer noise)
@@ -236,7 +239,7 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
         final = []
         for _, kind, s in timed[:2]:
             run = lambda: _launch(kind, s, mode, A, lda, B, ldb, Cs, ldc, M, N, K, bias, act, aux_s,  # noqa: E731
-                                  conv_arr, row_remap, residual, False, cs_s)
+                                  conv_arr, row_remap, residual, False, cs_s, bnb)
             reps = min(48, max(6, int(3.0 / max(timed[0][0], 1e-3))))
             final.append((_time_runs(run, reps), kind, s))
         final.sort()
@@ -245,7 +248,7 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
 
 
 def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap, residual,
-            kernel, colstats):
+            kernel, colstats, bnb=None):
     """(kernel kind, splits) for one GEMM call: forced, explicit, tuned (cached) or heuristic."""
     kernel = kernel or _forced
     if kernel is not None:
@@ -266,14 +269,14 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
         choice = ("small", 1 if row_remap else pick_splits(M, N, K, splits))
     elif _TUNE and not _force_small and C.is_cuda:
         key = f"{mode}|{M}|{N}|{K}|{lda}|{ldb}|{ldc}|{tuple(conv) if conv is not None else ''}|{int(row_remap)}|" \
-              f"{act}|{C.dtype}|{int(bias is not None)}|{int(colstats is not None)}"
+              f"{act}|{C.dtype}|{int(bias is not None)}|{int(colstats is not None)}|{int(residual is not None)}"
         choice = _tuned.get(key)
         if choice is None:
             if torch.cuda.is_current_stream_capturing():   # cannot time inside a graph capture
                 choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
             else:
                 choice = _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
-                               residual, colstats)
+                               residual, colstats, bnb)
                 _tuned[key] = choice
                 _save_cache()
     else:
@@ -284,11 +287,14 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
 
 
 def plan(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
-         M: int, N: int, K: int, conv: Optional[Sequence[int]] = None) -> str:
-    """The kernel kind a plain call of this signature runs (tuning it now if needed)."""
+         M: int, N: int, K: int, conv: Optional[Sequence[int]] = None, residual: Optional[torch.Tensor] = None,
+         full: bool = False):
+    """The kernel kind (``full``: the (kind, splits) pair) a plain call of this signature
+    runs, tuning it now if needed."""
     conv_arr = None if conv is None else (ctypes.c_int * len(conv))(*[int(v) for v in conv])
-    return _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, None, None, None, None, conv, conv_arr, False, None,
-                   None, None)[0]
+    ch = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, None, None, None, None, conv, conv_arr, False, residual,
+                 None, None)
+    return ch if full else ch[0]
 
 
 def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: torch.Tensor, ldc: int,
@@ -296,24 +302,28 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          aux: Optional[torch.Tensor] = None, splits: Optional[int] = None,
          conv: Optional[Sequence[int]] = None, row_remap: bool = False,
          residual: Optional[torch.Tensor] = None, accumulate: bool = False,
-         kernel: Optional[str] = None, colstats: Optional[torch.Tensor] = None):
+         kernel: Optional[str] = None, colstats: Optional[torch.Tensor] = None, bnb=None):
     """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
     "narrow" (128x64) or "tnarrow" (weight gradient computed transposed on 128x64 tiles).
 
     ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm
     statistics partials of the bf16 output; the function then returns the number of
     partial rows written (one per M-tile).  Otherwise it returns ``C``.
+
+    ``act="bnb"`` with ``bnb=(relu_mask or None, mean, invstd)`` and ``aux`` = the BatchNorm's
+    input: the BatchNorm backward's reduction in the epilogue -- ``C`` receives
+    dz = (result + residual) * mask and ``colstats`` rows [sum dz | sum dz * xhat].
     """
     conv_arr = None
     if conv is not None:
         conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
     choice = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap,
-                     residual, kernel, colstats)
+                     residual, kernel, colstats, bnb)
     if _trace is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
     _launch(choice[0], choice[1], mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
-            residual, accumulate, colstats)
+            residual, accumulate, colstats, bnb)
     if _trace is not None:
         e1.record()
         _trace.append(((mode, M, N, K, tuple(conv) if conv is not None else None, act, bias is not None,

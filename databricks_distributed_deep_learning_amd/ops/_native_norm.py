@@ -1,6 +1,7 @@
 """Autograd bindings for the HIP BatchNorm / LayerNorm kernels (csrc/kernels/norm.hip)."""
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -8,6 +9,12 @@ import torch
 from . import _lib
 from ._native_elementwise import new_seed
 from ._lib import call, dcode, grad_ready, grad_sink, p
+
+# BatchNorm backward reduction in the dgrad epilogue of the conv that consumes the BN
+# output (ops/bridge.py BNBackward); DDL_BN_BWD_EPI=0 keeps the separate partial pass
+_BN_BWD_EPI = os.environ.get("DDL_BN_BWD_EPI", "1") != "0"
+# ... also when the dgrad adds a bridged residual gradient (three extra streams per site)
+_BN_BWD_EPI_RES = os.environ.get("DDL_BN_BWD_EPI", "1") not in ("0", "nores")
 
 
 def _bn_supported(C: int) -> bool:
@@ -74,6 +81,12 @@ class _BatchNormTrain(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.params = (weight, bias)
         ctx.save_for_backward(x, mask, weight, stats)
+        ctx.bnb = None
+        if _BN_BWD_EPI and x.dtype == torch.bfloat16:
+            # the conv consuming y may run this BN's backward reduction in its dgrad epilogue
+            from .bridge import BNBackward
+            ctx.bnb = BNBackward(x, mask, stats[0], stats[1])
+            y._ddl_bnb = ctx.bnb
         return y
 
     @staticmethod
@@ -96,7 +109,23 @@ class _BatchNormTrain(torch.autograd.Function):
         else:
             dgamma = torch.empty_like(weight) if weight is not None else None
             dbeta = torch.empty_like(weight) if weight is not None else None
-        if ctx.group is not None:
+        given = ctx.bnb.take_for(dy) if ctx.bnb is not None else None
+        ctx.bnb = None
+        if given is not None:
+            # dy is dz (ReLU mask applied) and [sum dz | sum dz*xhat] came from the dgrad epilogue
+            gpart, nrows = given
+            if ctx.group is not None:
+                row = torch.empty(2 * C, **f32)
+                call("ddl_bn_rows_sum", p(gpart), nrows, 2 * C, p(row), None)
+                _group_sum(row, ctx.group)
+                call("ddl_bn_bwd_finish", dcode(x), p(dy), None, p(x), p(stats[0]), p(stats[1]), p(weight), M,
+                     ctx.m_total, C, 0, p(row), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+            else:
+                ws = gpart[nrows * 2 * C:]
+                call("ddl_bn_bwd_from_partials", dcode(x), p(gpart), nrows, p(ws), ws.numel(), p(dy), p(x),
+                     p(stats[0]), p(stats[1]), p(weight), M, C, p(dgamma), p(dbeta), p(coef), p(dx), p(dres),
+                     int(direct))
+        elif ctx.group is not None:
             # SyncBatchNorm: [sum dz | sum dz*xhat] summed over the group before the finalize
             call("ddl_bn_bwd_partials", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), M, C,
                  int(ctx.relu), p(part))

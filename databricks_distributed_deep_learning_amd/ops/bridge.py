@@ -92,3 +92,32 @@ class BNStats:
         part, nblk = self.part, self.nblk
         self.part = None
         return part, nblk
+
+
+class BNBackward:
+    """Carries a BatchNorm's backward reduction from the dgrad GEMM that produces the
+    gradient of the BN output (backward-time side channel, ``gemm(act="bnb")``).
+
+    Set on the BN output in training; the conv that consumes that output finds it on its
+    input, applies the BN's ReLU mask in its dgrad epilogue and sums [dz | dz * xhat] per
+    column.  The BN uses the partials only if its incoming gradient is exactly that dgrad
+    output.  The hint keeps a reference to it, which also stops autograd from accumulating
+    a second gradient contribution into it in place (the sum is then a new tensor, the
+    pointers differ and the BN computes its own reduction, masking is idempotent)."""
+    __slots__ = ("x", "mask", "mean", "istd", "dz", "part", "nrows")
+
+    def __init__(self, x: torch.Tensor, mask: Optional[torch.Tensor], mean: torch.Tensor, istd: torch.Tensor):
+        self.x, self.mask, self.mean, self.istd = x, mask, mean, istd
+        self.dz = None
+        self.part = None
+        self.nrows = 0
+
+    def set(self, dz: torch.Tensor, part: torch.Tensor, nrows: int) -> None:
+        self.dz, self.part, self.nrows = dz, part, nrows
+
+    def take_for(self, g: torch.Tensor):
+        dz, part, nrows = self.dz, self.part, self.nrows
+        self.dz = self.part = None
+        if dz is None or dz.data_ptr() != g.data_ptr() or dz.numel() != g.numel():
+            return None
+        return part, nrows
