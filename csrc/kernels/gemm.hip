@@ -32,6 +32,13 @@ constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;   // 16 KB per operand tile
 
 enum Layout { KC = 0, KO = 1, CONV = 2, CONVW = 3 };
+// LDS bytes of one pipeline stage (A image + B image).  A 64-row KC B image (narrow
+// tiles: NT / conv-forward / dgrad operands) fills only the first 8 KB of its 128-row
+// layout, so its stage packs to 24 KB: 48 KB a block, three blocks (12 waves) a CU.
+template <int LB, int BNT>
+constexpr int stage_bytes() { return TILE_BYTES + ((BNT == 64 && LB == KC) ? TILE_BYTES / 2 : TILE_BYTES); }
+template <int LB, int BNT>
+constexpr int waves_per_eu() { return (BNT == 64 && LB == KC) ? 3 : 2; }
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4, ACT_BNB = 5 };
 
 struct ConvDesc {
@@ -344,7 +351,7 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
         // one K-step: (ran, rbn) hold K-step kt+1, (raf, rbf) are free and receive kt+2
         auto step = [&](int kt, uint4 (&ran)[4], uint4 (&rbn)[4], uint4 (&raf)[4], uint4 (&rbf)[4]) {
             const int cur = (kt - kt0) & 1;
-            char* sa = smem + cur * 2 * TILE_BYTES;
+            char* sa = smem + cur * stage_bytes<LB, BNT>();
             char* sb = sa + TILE_BYTES;
             if (kt + 2 < kt1) {
                 la.load(p, (kt + 2) * BK, raf);
@@ -364,7 +371,7 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
             }
             if (kt + 1 < kt1) {
-                char* na = smem + (cur ^ 1) * 2 * TILE_BYTES;
+                char* na = smem + (cur ^ 1) * stage_bytes<LB, BNT>();
                 la.store(na, ran);
                 lb.store(na + TILE_BYTES, rbn);
             }
@@ -581,8 +588,8 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
 }
 
 template <int LA, int LB, int BNT, bool BNB = false>
-__global__ __launch_bounds__(NT, 2) void gemm_k(Params p) {
-    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+__global__ __launch_bounds__(NT, (waves_per_eu<LB, BNT>())) void gemm_k(Params p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * stage_bytes<LB, BNT>()];
     gemm_body<LA, LB, BNT, BNB>(p, smem);
 }
 
@@ -595,8 +602,8 @@ struct ParamsMC {
 };
 
 template <int LA, int LB, int BNT>
-__global__ __launch_bounds__(NT, 2) void gemm_mc_k(ParamsMC pm) {
-    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+__global__ __launch_bounds__(NT, (waves_per_eu<LB, BNT>())) void gemm_mc_k(ParamsMC pm) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * stage_bytes<LB, BNT>()];
     const Params& p = pm.c[blockIdx.z];
     if ((int)blockIdx.x >= p.tiles_m * p.tiles_n) return;   // this class has fewer tiles
     gemm_body<LA, LB, BNT>(p, smem);
