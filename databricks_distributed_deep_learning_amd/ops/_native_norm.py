@@ -12,9 +12,11 @@ from ._lib import call, dcode, grad_ready, grad_sink, p
 
 # BatchNorm backward reduction in the dgrad epilogue of the conv that consumes the BN
 # output (ops/bridge.py BNBackward); DDL_BN_BWD_EPI=0 keeps the separate partial pass
-_BN_BWD_EPI = os.environ.get("DDL_BN_BWD_EPI", "1") != "0"
-# ... also when the dgrad adds a bridged residual gradient (three extra streams per site)
-_BN_BWD_EPI_RES = os.environ.get("DDL_BN_BWD_EPI", "1") not in ("0", "nores")
+_BN_BWD_EPI = os.environ.get("DDL_BN_BWD_EPI", "nores") != "0"
+# ... also when the dgrad adds a bridged residual gradient ("1"): three extra operand
+# streams per output site made those K=64..256 GEMMs slower than GEMM + partial pass
+# (profiles/bn_bwd_epilogue_ab.log, kernels_r50.md), so the default ("nores") skips them
+_BN_BWD_EPI_RES = os.environ.get("DDL_BN_BWD_EPI", "nores") not in ("0", "nores")
 
 
 def _bn_supported(C: int) -> bool:

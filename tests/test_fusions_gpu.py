@@ -99,14 +99,16 @@ def test_bn_backward_epilogue_model_gradients(arch):
     x = torch.randn(8, 64, 64, 3, device=dev, dtype=torch.bfloat16)
     y = torch.randint(0, 10, (8,), device=dev)
     grads = {}
+    saved = (NC._BN_BWD_EPI, NC._BN_BWD_EPI_RES, NN._BN_BWD_EPI)
     for flag in (True, False):
-        NC._BN_BWD_EPI = NN._BN_BWD_EPI = flag
+        # fused run: every eligible dgrad, the residual-adding ones included
+        NC._BN_BWD_EPI = NC._BN_BWD_EPI_RES = NN._BN_BWD_EPI = flag
         try:
             mm = copy.deepcopy(m)
             ops.cross_entropy(mm(x).float(), y).backward()
             grads[flag] = {n: q.grad.float() for n, q in mm.named_parameters() if q.grad is not None}
         finally:
-            NC._BN_BWD_EPI = NN._BN_BWD_EPI = True
+            NC._BN_BWD_EPI, NC._BN_BWD_EPI_RES, NN._BN_BWD_EPI = saved
     assert grads[True].keys() == grads[False].keys() and len(grads[True]) > 20
     rel = {n: ((grads[True][n] - grads[False][n]).norm() / grads[False][n].norm().clamp_min(1e-12)).item()
            for n in grads[True]}
