@@ -13,6 +13,7 @@
 // fused residual add, fp32 statistics saved for backward; backward computes dx
 // per row and per-block dgamma/dbeta partials reduced by a second kernel.
 #include "ddl_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -777,7 +778,15 @@ DDL_API int ddl_ln_fwd(int dtype, const void* x, const void* res, long res_rows,
     DDL_RETURN_LAUNCH();
 }
 
-DDL_API int ddl_ln_bwd_nblk(long rows) { return (int)std::max<long>(1, std::min<long>(1024, (rows + 15) / 16)); }
+// rows per block (DDL_LN_BWD_ROWS, default 16) and block cap (DDL_LN_BWD_MAXBLK, default 1024)
+static int ln_env(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && atoi(v) > 0 ? atoi(v) : dflt;
+}
+DDL_API int ddl_ln_bwd_nblk(long rows) {
+    static const int rpb = ln_env("DDL_LN_BWD_ROWS", 16), cap = ln_env("DDL_LN_BWD_MAXBLK", 1024);
+    return (int)std::max<long>(1, std::min<long>(cap, (rows + rpb - 1) / rpb));
+}
 
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
