@@ -32,13 +32,13 @@ constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;   // 16 KB per operand tile
 
 enum Layout { KC = 0, KO = 1, CONV = 2, CONVW = 3 };
-// LDS bytes of one pipeline stage (A image + B image).  A 64-row KC B image (narrow
-// tiles: NT / conv-forward / dgrad operands) fills only the first 8 KB of its 128-row
-// layout, so its stage packs to 24 KB: 48 KB a block, three blocks (12 waves) a CU.
+// LDS bytes of one pipeline stage (A image + B image).  A narrow tile's 64-row B image
+// is 8 KB (KC: the first half of the 128-row layout; k-major: packed 128-byte rows), so
+// its stage packs to 24 KB: 48 KB a block, three blocks (12 waves) a CU.
 template <int LB, int BNT>
-constexpr int stage_bytes() { return TILE_BYTES + ((BNT == 64 && LB == KC) ? TILE_BYTES / 2 : TILE_BYTES); }
+constexpr int stage_bytes() { return TILE_BYTES + (BNT == 64 ? TILE_BYTES / 2 : TILE_BYTES); }
 template <int LB, int BNT>
-constexpr int waves_per_eu() { return (BNT == 64 && LB == KC) ? 3 : 2; }
+constexpr int waves_per_eu() { return BNT == 64 ? 3 : 2; }
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_DGELU = 4, ACT_BNB = 5 };
 
 struct ConvDesc {
@@ -91,14 +91,19 @@ __device__ __forceinline__ uint4 sel(bool ok, uint4 a, uint4 z) {
 }
 
 __device__ __forceinline__ int swz_ko(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+// 64-column k-major image (narrow B operand), 128-byte rows: a fragment read touches rows
+// 8g + q (g, q < 4), two chunks each; rows of one parity share a bank half, so the chunk
+// pair is XORed with (q >> 1) | (g & 1) << 1 -- the same 2-way (g, g + 2) overlap as the
+// 256-byte layout
+__device__ __forceinline__ int swz_kon(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
 
 // ------------------------------------------------------------------ loaders
 // Each thread stages 4 chunks (16 B) of each operand per K-step.
 template <int L, bool IS_A, int ROWS = 128>
 struct Loader {
-    // ROWS = 64 (narrow B tile): KC rows (t>>3) + 32 i for i < 2; KO/CONVW chunk c = t&7
-    // and k-rows (t>>3) + 32 i.  The LDS images keep the 128-row layouts (only
-    // the first 64 rows / columns are filled), so fragment reads are unchanged.
+    // ROWS = 64 (narrow B tile): KC rows (t>>3) + 32 i for i < 2 (the first half of the
+    // 128-row image, fragment reads unchanged); KO/CONVW chunk c = t&7 and k-rows
+    // (t>>3) + 32 i into packed 128-byte rows (read_frag<L, true>).
     static constexpr int NCH = ROWS / 32;   // 16-B chunks per thread
     // KC / CONV: thread -> chunk c = t&7, rows (t>>3) + 32 i
     // KO / CONVW: thread -> chunk c = t&15, k-rows (t>>4) + 16 i
@@ -245,12 +250,12 @@ struct Loader {
                 const int r = (t >> 4) + 16 * i;
                 *reinterpret_cast<uint4*>(lds + r * 256 + ((c ^ swz_ko(r)) << 4)) = v[i];
             }
-        } else {
+        } else {   // 64-column k-major image, packed 128-byte rows (read_frag<L, true>)
             const int c = t & 7;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int r = (t >> 3) + 32 * i;
-                *reinterpret_cast<uint4*>(lds + r * 256 + ((c ^ swz_ko(r)) << 4)) = v[i];
+                *reinterpret_cast<uint4*>(lds + r * 128 + ((c ^ swz_kon(r)) << 4)) = v[i];
             }
         }
     }
@@ -258,7 +263,7 @@ struct Loader {
 
 // Fragment for rows [rbase, rbase+16) of the tile, k-subtile kk (0/1):
 // lane l gets row rbase + (l&15), k = 32 kk + 8 (l>>4) + 0..7.
-template <int L>
+template <int L, bool NARROW = false>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rbase, int kk) {
     const int l = threadIdx.x & 63;
     if (L == KC || L == CONV) {
@@ -272,8 +277,10 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rbase, int kk) 
         const int r_a = kk * 32 + 8 * g + q;
         const int r_b = r_a + 4;
         typedef __attribute__((address_space(3))) s16x4 lds_v4;
-        const char* pa = lds + r_a * 256 + ((chunk ^ swz_ko(r_a)) << 4) + (pq & 1) * 8;
-        const char* pb = lds + r_b * 256 + ((chunk ^ swz_ko(r_b)) << 4) + (pq & 1) * 8;
+        const char* pa = NARROW ? lds + r_a * 128 + ((chunk ^ swz_kon(r_a)) << 4) + (pq & 1) * 8
+                                : lds + r_a * 256 + ((chunk ^ swz_ko(r_a)) << 4) + (pq & 1) * 8;
+        const char* pb = NARROW ? lds + r_b * 128 + ((chunk ^ swz_kon(r_b)) << 4) + (pq & 1) * 8
+                                : lds + r_b * 256 + ((chunk ^ swz_ko(r_b)) << 4) + (pq & 1) * 8;
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pa);
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pb);
         typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -363,7 +370,7 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) af[i] = read_frag<LA>(sa, wm * 64 + i * 16, kk);
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<LB>(sb, wn * WN + j * 16, kk);
+                for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<LB, BNT == 64>(sb, wn * WN + j * 16, kk);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
