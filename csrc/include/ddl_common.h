@@ -157,8 +157,6 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t 
     return hash_u32(seed, idx) >= thresh;   // P(keep) = 1 - thresh / 2^32
 }
 
-// Fast unsigned division by a runtime constant (magic multiply), for index math
-// in hot loops: q = umulhi(n, mul) >> shift, exact for n < 2^31.
 // BatchNorm-backward GEMM epilogue (ACT_BNB) side arguments: the BN's ReLU bit mask
 // (nullable), saved mean and inverse std.  Set on the launching host thread by
 // ddl_gemm_bnb(), consumed by the next GEMM entry call (gemm.hip / gemm_big.hip).
@@ -183,6 +181,8 @@ __device__ __forceinline__ float row16_sum(float v) {
     return dpp_add<0x140>(v);   // row_mirror
 }
 
+// Fast unsigned division by a runtime constant (magic multiply), for index math
+// in hot loops: q = umulhi(n, mul) >> shift, exact for n < 2^31.
 struct FastDiv {
     uint32_t d, mul, shift;
 };
