@@ -510,17 +510,25 @@ DDL_API int ddl_embedding_bwd(int dtype, const int64_t* ids, const void* dy, flo
 struct TapMap {
     int r[8], s[8];
 };
+// 32x32 (k, c) tiles per tap through LDS: reads coalesce along c (w's contiguous
+// dimension), writes along k (out's); 32-bit index math (weights < 2^31 elements)
 __global__ __launch_bounds__(256) void conv_w_dgrad_k(const bf16_t* __restrict__ w, bf16_t* __restrict__ out, int K,
                                                       int R, int S, int C, int Rp, int Sp, TapMap tm) {
-    const long total = (long)C * Rp * Sp * K;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int k = (int)(i % K);
-        long t = i / K;
-        const int sp = (int)(t % Sp);
-        t /= Sp;
-        const int rp = (int)(t % Rp);
-        const int c = (int)(t / Rp);
-        out[i] = w[(((long)k * R + tm.r[rp]) * S + tm.s[sp]) * C + c];
+    __shared__ bf16_t tile[32][33];
+    const int k0 = blockIdx.x * 32, c0 = blockIdx.y * 32, tap = blockIdx.z;
+    const int rp = tap / Sp, sp = tap - rp * Sp;
+    const int r = tm.r[rp], s_ = tm.s[sp];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = k0 + ty + 8 * i, c = c0 + tx;
+        if (k < K && c < C) tile[ty + 8 * i][tx] = w[((k * R + r) * S + s_) * C + c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = c0 + ty + 8 * i, k = k0 + tx;
+        if (k < K && c < C) out[((c * Rp + rp) * Sp + sp) * K + k] = tile[tx][ty + 8 * i];
     }
 }
 
@@ -530,8 +538,9 @@ DDL_API int ddl_conv_w_dgrad(const void* w, void* out, int K, int R, int S, int 
     TapMap tm{};
     for (int i = 0; i < Rp; ++i) tm.r[i] = rmap[i];
     for (int i = 0; i < Sp; ++i) tm.s[i] = smap[i];
-    const long total = (long)C * Rp * Sp * K;
-    conv_w_dgrad_k<<<grid_for(total), 256, 0, st>>>((const bf16_t*)w, (bf16_t*)out, K, R, S, C, Rp, Sp, tm);
+    if ((long)K * R * S * C >= (1L << 31)) return -2;
+    const dim3 grid((K + 31) / 32, (C + 31) / 32, Rp * Sp);
+    conv_w_dgrad_k<<<grid, 256, 0, st>>>((const bf16_t*)w, (bf16_t*)out, K, R, S, C, Rp, Sp, tm);
     DDL_RETURN_LAUNCH();
 }
 

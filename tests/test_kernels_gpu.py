@@ -292,3 +292,16 @@ def test_softmax_topk(dtype, B, C, k):
     _close(v, vr, 1e-6, 1e-5, "top-k values")
     # indices: equal wherever the reference values are distinct
     assert torch.equal(i, ir) or torch.allclose(pr.gather(-1, i), vr, atol=1e-7)
+
+
+@pytest.mark.parametrize("K,R,S,C,rs,ss", [(64, 3, 3, 64, [2, 1, 0], [2, 1, 0]), (256, 1, 1, 1024, [0], [0]),
+                                           (48, 3, 3, 40, [1], [0, 2]), (2048, 1, 1, 512, [0], [0]),
+                                           (70, 7, 7, 33, [6, 4, 2, 0], [5, 3, 1])])
+def test_conv_dgrad_weight_layout(K, R, S, C, rs, ss):
+    """ddl_conv_w_dgrad: out[c][r'][s'][k] = w[k][rs[r']][ss[s']][c] (tiled transpose, odd tails)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops._native_conv import _w_dgrad
+    w = torch.randn(K, R, S, C, device=dev).bfloat16()
+    out = _w_dgrad(w, rs, ss)
+    ref = w[:, rs][:, :, ss].permute(3, 1, 2, 0).contiguous()
+    assert torch.equal(out, ref)
