@@ -44,6 +44,10 @@ namespace {
 #define DDL_GROUP_M 8      // tile rows per L2 group (tile order inside an XCD's share)
 #endif
 constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
+#ifndef DDL_RES_BEHIND
+#define DDL_RES_BEHIND 0     // 1: store-behind also for residual tiles (measured neutral to -8%)
+#endif
+constexpr bool kResBehind = DDL_RES_BEHIND;
 constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
 
@@ -505,7 +509,19 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                             cq[e] += t[e] * (xv[e] - bv[e]) * rs[e];
                         }
                     }
-            } else
+            } else {
+            // bf16 residual: the column group's 8 sites load together before any store
+            // (p.C may alias p.res for all the compiler knows, so it would otherwise wait
+            // out one load latency per site -- residual-adding dgrads ran at ~2-3 TB/s)
+            uint2 rb[2][4];
+            if (EK == EK_BF16 && p.res) {
+#pragma unroll
+                for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        rb[qm][i] = *reinterpret_cast<const uint2*>(
+                            p.res + (long)(m0 + qm * 128 + wm * 64 + i * 16 + r16) * p.ldc + n);
+            }
 #pragma unroll
             for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -514,7 +530,13 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                     const f32x4& a = acc[qm][qn][i][j];
                     if (EK == EK_BF16) {
                         float rv[4] = {0.f, 0.f, 0.f, 0.f};
-                        if (p.res) load4(p.res + (long)m * p.ldc + n, rv);
+                        if (p.res) {
+                            const uint2 r2 = rb[qm][i];
+                            rv[0] = __uint_as_float(r2.x << 16);
+                            rv[1] = __uint_as_float(r2.x & 0xffff0000u);
+                            rv[2] = __uint_as_float(r2.y << 16);
+                            rv[3] = __uint_as_float(r2.y & 0xffff0000u);
+                        }
                         const uint32_t lo = pack2bf(a[0] + bv[0] + rv[0], a[1] + bv[1] + rv[1]);
                         const uint32_t hi = pack2bf(a[2] + bv[2] + rv[2], a[3] + bv[3] + rv[3]);
                         *reinterpret_cast<uint2*>((bf16_t*)p.C + (long)m * p.ldc + n) = make_uint2(lo, hi);
@@ -573,6 +595,7 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         }
                     }
                 }
+            }
             if (stats) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -789,7 +812,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // loads and MFMAs instead of being waited for (vmcnt retires in issue order).
             // Short-K tiles (1x1 convolutions: K = 64..256) are otherwise latency-bound on
             // load -> compute -> store-drain per tile.
-            const bool behind = next && nK > 0 && interior && p.ek == EK_BF16 && !p.bias && !p.res;
+            // (a residual's loads retire in order behind the next prologue's, so the counts
+            // below stay upper bounds)
+            const bool behind = next && nK > 0 && interior && p.ek == EK_BF16 && !p.bias && (!p.res || kResBehind);
             if (next) {
                 coords(vn);
                 sa.init(p, m0);

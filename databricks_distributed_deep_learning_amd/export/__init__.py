@@ -179,6 +179,17 @@ def top5(logits: torch.Tensor, categories: Optional[List[str]] = None):
     return [(names[int(k)], float(s)) for k, s in zip(i[0], v[0])]
 
 
+def _ort_session(path: Optional[str]):
+    """ONNX Runtime CPU session of ``path``; None when onnx / onnxruntime are not installed."""
+    if path is None:
+        return None
+    try:
+        import onnxruntime
+    except ImportError:
+        return None
+    return onnxruntime.InferenceSession(path, providers=["CPUExecutionProvider"])
+
+
 def bench_runtimes(model: ResNet, x: torch.Tensor, iters: int = 50, warmup: int = 5,
                    categories: Optional[List[str]] = None, workdir: str = "/tmp/ddl_export",
                    rtol: float = 1e-5, atol: float = 1e-4) -> Dict[str, object]:
@@ -200,6 +211,20 @@ def bench_runtimes(model: ResNet, x: torch.Tensor, iters: int = 50, warmup: int 
     with torch.no_grad():
         out, ms = _timed(ts, x.float(), iters, warmup, device)
     results["torchscript_fp32"] = {"ms": ms, "out": out}
+    # torch.export program of the same fp32 model (the ahead-of-time graph path)
+    ep_path = export_model(ref_model, x.float(), "torch_export", os.path.join(workdir, "resnet.pt2"))
+    ep = torch.export.load(ep_path).module()
+    with torch.no_grad():
+        out, ms = _timed(ep, x.float(), iters, warmup, device)
+    results["torch_export_fp32"] = {"ms": ms, "out": out}
+    # ONNX Runtime CPU EP, as the reference's session (cv/onnx:77-83, 91-101), when installed
+    onnx_path = export_model(copy.deepcopy(ref_model).cpu(), x.float().cpu(), "onnx",
+                             os.path.join(workdir, "resnet50.onnx"))
+    sess = _ort_session(onnx_path)
+    if sess is not None:
+        out, ms = _timed(lambda a: torch.from_numpy(sess.run([], {"input": a.cpu().numpy()})[0]).to(device),
+                         x.float(), iters, warmup, device)
+        results["onnxruntime_cpu_fp32"] = {"ms": ms, "out": out}
     ops.set_native_mode(prev_mode)
     if device.type == "cuda" and ops.native_available():
         nat = copy.deepcopy(model).to(device)
@@ -231,6 +256,7 @@ def bench_runtimes(model: ResNet, x: torch.Tensor, iters: int = 50, warmup: int 
                                     os.path.join(workdir, "model.safetensors")),
         "state_dict": export_model(model.cpu().float(), x.float().cpu(), "state_dict",
                                    os.path.join(workdir, "model_state.pt")),
-        "onnx": export_model(model.cpu().float(), x.float().cpu(), "onnx", os.path.join(workdir, "resnet50.onnx")),
+        "onnx": onnx_path,
+        "torch_export": ep_path,
     }
     return {"runtimes": results, "artifact_bytes": artifact_sizes(paths)}

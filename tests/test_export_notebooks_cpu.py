@@ -50,6 +50,14 @@ def test_folded_resnet_matches_eval_model_cpu():
         torch.testing.assert_close(f(x), m(x), rtol=1e-4, atol=1e-4)
 
 
+def _has(mod):
+    try:
+        __import__(mod)
+        return True
+    except ImportError:
+        return False
+
+
 def test_bench_runtimes_cpu(tmp_path):
     from databricks_distributed_deep_learning_amd.export import bench_runtimes
     from databricks_distributed_deep_learning_amd.models import resnet18
@@ -57,7 +65,10 @@ def test_bench_runtimes_cpu(tmp_path):
     rep = bench_runtimes(resnet18(num_classes=10), torch.randn(1, 32, 32, 3), iters=1, warmup=1,
                          workdir=str(tmp_path))
     rt = rep["runtimes"]
-    assert rt["torchscript_fp32"]["allclose_ref_tol"] and rt["torchscript_fp32"]["top1_agrees"]
+    for name in ("torchscript_fp32", "torch_export_fp32"):
+        assert rt[name]["allclose_ref_tol"] and rt[name]["top1_agrees"], name
+    # ONNX Runtime runs only where onnx + onnxruntime are installed (neither is in this image)
+    assert ("onnxruntime_cpu_fp32" in rt) == (rep["artifact_bytes"]["onnx"] is not None and _has("onnxruntime"))
     assert len(rt["pytorch_eager_fp32"]["top5"]) == 5
     assert rep["artifact_bytes"]["onnx"] is None or rep["artifact_bytes"]["onnx"] > 0
 
