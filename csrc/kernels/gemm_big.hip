@@ -44,10 +44,6 @@ namespace {
 #define DDL_GROUP_M 8      // tile rows per L2 group (tile order inside an XCD's share)
 #endif
 constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
-#ifndef DDL_RES_BEHIND
-#define DDL_RES_BEHIND 0     // 1: store-behind also for residual tiles (measured neutral to -8%)
-#endif
-constexpr bool kResBehind = DDL_RES_BEHIND;
 constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
 
@@ -88,10 +84,12 @@ struct BigParams {
     ConvDesc cd;
     int tiles_m, tiles_n;
     int ek;                   // register-epilogue variant (EK_*), set by the launcher
+    int behind_mask;          // store-behind beyond plain bf16 tiles: BEHIND_* bits (DDL_GEMM_BEHIND)
     const uint8_t* bn_mask;   // ACT_BNB: BatchNorm backward reduction fused into the dgrad (gemm.hip Params)
     const float* bn_mean;
     const float* bn_istd;
 };
+enum BehindBits { BEHIND_BIAS = 1, BEHIND_GELU = 2, BEHIND_RES = 4 };
 enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3, EK_DGELU = 4, EK_BNB = 5, EK_BNBC = 6 };
 
 __device__ __forceinline__ int half_off(int buf, int x, int h) { return ((buf * 2 + x) * 2 + h) * HALF; }
@@ -454,13 +452,31 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
     const bool stats = (EK == EK_BF16 || EK == EK_GEN || EK == EK_DGELU || EK == EK_BNB || EK == EK_BNBC) &&
                        p.colstats;
+    // interior bf16 / GELU tiles: the bias of all four column groups up front, so no
+    // load sits between this tile's stores (a load's wait also waits out every store
+    // issued before it: vmcnt counts both)
+    uint2 bpre[2][2];
+    if ((EK == EK_BF16 || EK == EK_GELU) && p.bias) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                bpre[qn][j] = *reinterpret_cast<const uint2*>((const bf16_t*)p.bias + n0 + qn * 128 + wn * 32 +
+                                                              j * 16 + g4);
+    }
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int n = n0 + qn * 128 + wn * 32 + j * 16 + g4;
             float bv[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
-            if ((EK == EK_BF16 || EK == EK_GELU) && p.bias) load4((const bf16_t*)p.bias + n, bv);
+            if ((EK == EK_BF16 || EK == EK_GELU) && p.bias) {
+                const uint2 b2 = bpre[qn][j];
+                bv[0] = __uint_as_float(b2.x << 16);
+                bv[1] = __uint_as_float(b2.x & 0xffff0000u);
+                bv[2] = __uint_as_float(b2.y << 16);
+                bv[3] = __uint_as_float(b2.y & 0xffff0000u);
+            }
             if (EK == EK_BNB || EK == EK_BNBC) {   // BN mean / inverse std of these 4 channels
                 load4(p.bn_mean + min(n, p.N - 4), bv);
                 load4(p.bn_istd + min(n, p.N - 4), rs);
@@ -513,14 +529,16 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
             // bf16 residual: the column group's 8 sites load together before any store
             // (p.C may alias p.res for all the compiler knows, so it would otherwise wait
             // out one load latency per site -- residual-adding dgrads ran at ~2-3 TB/s)
+            // (dGELU: the saved pre-activation likewise)
             uint2 rb[2][4];
-            if (EK == EK_BF16 && p.res) {
+            const bf16_t* pre = EK == EK_BF16 ? p.res : (EK == EK_DGELU ? (const bf16_t*)p.aux : nullptr);
+            if ((EK == EK_BF16 || EK == EK_DGELU) && pre) {
 #pragma unroll
                 for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         rb[qm][i] = *reinterpret_cast<const uint2*>(
-                            p.res + (long)(m0 + qm * 128 + wm * 64 + i * 16 + r16) * p.ldc + n);
+                            pre + (long)(m0 + qm * 128 + wm * 64 + i * 16 + r16) * p.ldc + n);
             }
 #pragma unroll
             for (int qm = 0; qm < 2; ++qm)
@@ -560,9 +578,10 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                     } else if (EK == EK_DGELU) {
                         // dZ = dH * GELU'(z) (z = the Linear's saved pre-activation), and the
                         // column sums of the stored dZ: that Linear's bias gradient
-                        float z[4];
                         const long o = (long)m * p.ldc + n;
-                        load4(p.aux + o, z);
+                        const uint2 z2 = rb[qm][i];
+                        const float z[4] = {__uint_as_float(z2.x << 16), __uint_as_float(z2.x & 0xffff0000u),
+                                            __uint_as_float(z2.y << 16), __uint_as_float(z2.y & 0xffff0000u)};
                         const uint32_t lo = pack2bf(a[0] * gelu_erf_grad(z[0]), a[1] * gelu_erf_grad(z[1]));
                         const uint32_t hi = pack2bf(a[2] * gelu_erf_grad(z[2]), a[3] * gelu_erf_grad(z[3]));
                         *reinterpret_cast<uint2*>((bf16_t*)p.C + o) = make_uint2(lo, hi);
@@ -814,7 +833,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // load -> compute -> store-drain per tile.
             // (a residual's loads retire in order behind the next prologue's, so the counts
             // below stay upper bounds)
-            const bool behind = next && nK > 0 && interior && p.ek == EK_BF16 && !p.bias && (!p.res || kResBehind);
+            const bool behind = next && nK > 0 && interior &&
+                ((p.ek == EK_BF16 && (!p.bias || (p.behind_mask & BEHIND_BIAS)) &&
+                  (!p.res || (p.behind_mask & BEHIND_RES))) ||
+                 (p.ek == EK_GELU && (p.behind_mask & BEHIND_GELU)));
             if (next) {
                 coords(vn);
                 sa.init(p, m0);
@@ -845,8 +867,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             vt = vn;
             if (nK > 0) {
                 if (behind) {
-                    // E landed once at most (O loads) + (epilogue stores) remain outstanding
-                    if (nK > 1) {
+                    // E landed once at most (O loads) + (epilogue stores) remain outstanding;
+                    // GELU tiles store twice per site (output + pre-activation): the 6-bit
+                    // counter's maximum is a stronger wait than needed, never a weaker one
+                    if (p.ek == EK_GELU) {
+                        asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+                    } else if (nK > 1) {
                         if (p.colstats) asm volatile("s_waitcnt vmcnt(46)" ::: "memory");
                         else asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
                     } else {
@@ -1016,8 +1042,20 @@ bool direct_enabled() {
     return on;
 }
 
+// DDL_GEMM_BEHIND: BEHIND_* bits -- which register epilogues besides plain bf16 let
+// their stores drain under the next tile's prologue.  Measured neutral (bias, GELU:
+// profiles/epilogue_behind_ab.log) to -8 % (residual), so all off by default
+int behind_mask() {
+    static const int m = [] {
+        const char* e = getenv("DDL_GEMM_BEHIND");
+        return e ? atoi(e) : 0;
+    }();
+    return m;
+}
+
 template <int LA, int LB>
 int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st) {
+    p.behind_mask = behind_mask();
     p.tiles_m = (p.M + TB - 1) / TB;
     p.tiles_n = (p.N + TB - 1) / TB;
     const int nk = (p.K + BK - 1) / BK;
