@@ -76,14 +76,37 @@ class ThroughputMeter:
         return 1000.0 * self.seconds / self.steps if self.steps else 0.0
 
 
+def _mlflow_module(flag: Optional[bool]):
+    """``mlflow`` when requested (``flag`` or DDL_MLFLOW=1) and importable, else None:
+    the Databricks-native tracking sink, absent from this image, so strictly optional."""
+    if flag is None:
+        flag = os.environ.get("DDL_MLFLOW", "0") == "1"
+    if not flag:
+        return None
+    try:
+        import mlflow
+    except ImportError:
+        return None
+    return mlflow
+
+
 class JsonlLogger:
-    def __init__(self, path: str = "", enabled: bool = True):
+    """Rank-0 structured log: one JSON object per record; numeric fields
+    are mirrored to MLflow (``log_metrics(step=record["step"])``) when enabled."""
+
+    def __init__(self, path: str = "", enabled: bool = True, mlflow: Optional[bool] = None):
         self.path = path
         self.enabled = enabled and bool(path)
         if self.enabled:
             os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        self._mlflow = _mlflow_module(mlflow) if enabled else None
 
     def log(self, record: Dict) -> None:
+        if self._mlflow is not None:
+            nums = {k: float(v) for k, v in record.items()
+                    if isinstance(v, (int, float)) and not isinstance(v, bool) and k != "step"}
+            if nums:
+                self._mlflow.log_metrics(nums, step=int(record.get("step", 0)))
         if not self.enabled:
             return
         record = dict(record, ts=time.time())
