@@ -651,23 +651,56 @@ __global__ __launch_bounds__(256) void gemm_reduce_k(const float* __restrict__ p
 // Vectorised split-K reduce: a thread owns 4 consecutive output elements along the
 // output's contiguous dimension (n, or m for the transposed store), 16-byte slab
 // loads when the slab dimension is contiguous, no 64-bit division per element.
+// SG threads share one output quad (splits g, g+SG, ..., summed through LDS): weight
+// gradients have small outputs (64x256) and up to 256 slabs, so one thread per quad
+// left a few dozen blocks each walking hundreds of dependent load latencies.
+template <int SG>
 __global__ __launch_bounds__(256) void gemm_reduce4_k(const float* __restrict__ part, int splits, long split_stride,
                                                       long ldw, int M, int N, long ldc, void* out, int out_f32,
                                                       const void* bias, int bias_bf16, int act, void* aux,
                                                       const bf16_t* __restrict__ res, int accumulate, int trans,
                                                       FastDiv fd_w, int w4, int total4) {
+    constexpr int QPB = 256 / SG;   // output quads per block
+    __shared__ float4 s_part[SG > 1 ? SG - 1 : 1][QPB];
+    const int ql = threadIdx.x % QPB, g = threadIdx.x / QPB;
     // plain: i = m * (N/4) + n/4;   transposed: i = (m/4) * N + n
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+    // (block-uniform trip count: the LDS combine below has barriers)
+    for (int base = blockIdx.x * QPB; base < total4; base += gridDim.x * QPB) {
+        const bool live = base + ql < total4;
+        const int i = live ? base + ql : total4 - 1;   // dead lanes re-read a valid quad
         const int row = (int)fdiv((uint32_t)i, fd_w);
         float v[4] = {0.f, 0.f, 0.f, 0.f};
         if (!trans) {
             // row = m, columns c4..c4+3 (consecutive threads: consecutive column groups)
             const int c4 = (i - row * w4) * 4;
             const float* src = part + (long)row * ldw + c4;
-            for (int s = 0; s < splits; ++s) {
-                const float4 t = *reinterpret_cast<const float4*>(src + s * split_stride);
+            float u[4] = {0.f, 0.f, 0.f, 0.f};
+            int s = g;
+            for (; s + SG < splits; s += 2 * SG) {   // two independent chains
+                const float4 t0 = *reinterpret_cast<const float4*>(src + (long)s * split_stride);
+                const float4 t1 = *reinterpret_cast<const float4*>(src + (long)(s + SG) * split_stride);
+                v[0] += t0.x; v[1] += t0.y; v[2] += t0.z; v[3] += t0.w;
+                u[0] += t1.x; u[1] += t1.y; u[2] += t1.z; u[3] += t1.w;
+            }
+            if (s < splits) {
+                const float4 t = *reinterpret_cast<const float4*>(src + (long)s * split_stride);
                 v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += u[r];
+            if (SG > 1) {
+                if (g > 0) s_part[g - 1][ql] = make_float4(v[0], v[1], v[2], v[3]);
+                __syncthreads();
+                if (g == 0) {
+#pragma unroll
+                    for (int k = 0; k < SG - 1; ++k) {
+                        const float4 t = s_part[k][ql];
+                        v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+                    }
+                }
+                __syncthreads();
+            }
+            if (g != 0 || !live) continue;
             const long o = (long)row * ldc + c4;
             if (bias) {
                 float bv[4];
@@ -714,9 +747,22 @@ __global__ __launch_bounds__(256) void gemm_reduce4_k(const float* __restrict__ 
             // the slab reads coalesce); stored as 4 consecutive elements of C^T row n
             const int n = i - row * w4, m4 = row * 4;
             const float* src = part + (long)m4 * ldw + n;
-            for (int s = 0; s < splits; ++s)
+            for (int s = g; s < splits; s += SG)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += src[s * split_stride + r * ldw];
+                for (int r = 0; r < 4; ++r) v[r] += src[(long)s * split_stride + r * ldw];
+            if (SG > 1) {
+                if (g > 0) s_part[g - 1][ql] = make_float4(v[0], v[1], v[2], v[3]);
+                __syncthreads();
+                if (g == 0) {
+#pragma unroll
+                    for (int k = 0; k < SG - 1; ++k) {
+                        const float4 t = s_part[k][ql];
+                        v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+                    }
+                }
+                __syncthreads();
+            }
+            if (g != 0 || !live) continue;
             const long o = (long)n * ldc + m4;
             if (out_f32) {
                 if (accumulate) {
@@ -779,10 +825,23 @@ int launch(Params& p, float* workspace, long ws_elems, int splits, hipStream_t s
         if (vec) {
             const int w4 = p.trans_out ? p.N : p.N / 4;     // index divisor: i = row * w4 + col
             const int total4 = (int)(total / 4);
-            const int g = std::min(8192, (total4 + 255) / 256);
-            gemm_reduce4_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out,
-                                               final_f32, p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final,
-                                               p.trans_out, make_fastdiv((uint32_t)w4), w4, total4);
+            // threads per output quad: enough to put ~1024 blocks on the chip, >= 4 slabs each
+            int sg = 1;
+            while (sg < 16 && sg * 4 <= splits && (long)total4 * sg < 256L * 1024) sg *= 2;
+            const int g = std::min(8192, (total4 + 256 / sg - 1) / (256 / sg));
+            const FastDiv fd = make_fastdiv((uint32_t)w4);
+#define DDL_REDUCE4(SG_)                                                                                        \
+    gemm_reduce4_k<SG_><<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out, \
+                                           final_f32, p.bias, p.bias_bf16, p.act, p.aux, p.res, acc_final,       \
+                                           p.trans_out, fd, w4, total4)
+            switch (sg) {
+                case 1: DDL_REDUCE4(1); break;
+                case 2: DDL_REDUCE4(2); break;
+                case 4: DDL_REDUCE4(4); break;
+                case 8: DDL_REDUCE4(8); break;
+                default: DDL_REDUCE4(16); break;
+            }
+#undef DDL_REDUCE4
         } else {
             const int g = (int)std::min<long>(8192, (total + 255) / 256);
             gemm_reduce_k<<<g, 256, 0, st>>>(workspace, splits, p.split_stride, p.ldw, p.M, p.N, p.ldc, final_out,
