@@ -246,14 +246,17 @@ template <typename TP>
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
                                   const TP* __restrict__ gamma, const float* __restrict__ invstd,
                                   TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef,
-                                  int acc) {
+                                  int acc, const float* __restrict__ prow = nullptr) {
     __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
     const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
     if (threadIdx.x >= 64 || c >= C) return;
-    if (dgamma) dgamma[c] = from_f<TP>((float)q + (acc ? to_f(dgamma[c]) : 0.f));
-    if (dbeta) dbeta[c] = from_f<TP>((float)s + (acc ? to_f(dbeta[c]) : 0.f));
+    // SyncBatchNorm: the coefficients need the group-summed row, but dgamma / dbeta are
+    // this rank's partials (the data-parallel reducer sums them across ranks afterwards)
+    const float ps = prow ? prow[c] : (float)s, pq = prow ? prow[C + c] : (float)q;
+    if (dgamma) dgamma[c] = from_f<TP>(pq + (acc ? to_f(dgamma[c]) : 0.f));
+    if (dbeta) dbeta[c] = from_f<TP>(ps + (acc ? to_f(dbeta[c]) : 0.f));
     const float g = gamma ? to_f(gamma[c]) : 1.f;
     coef[c] = g * invstd[c];                 // k1
     coef[C + c] = (float)(s / (double)M);    // mean(dz)
@@ -885,14 +888,16 @@ DDL_API int ddl_bn_bwd_partials(int dtype, const void* dy, const void* mask, con
     DDL_RETURN_LAUNCH();
 }
 
-// backward finish from ONE (all-reduced) row [sum dz | sum dz*xhat]: dgamma / dbeta and the
-// coefficients use the global row count M_total, the apply walks the local M rows
+// backward finish from ONE (all-reduced) row [sum dz | sum dz*xhat]: the coefficients use it
+// and the global row count M_total, the apply walks the local M rows; dgamma / dbeta come from
+// local_row (this rank's own [sum dz | sum dz*xhat], taken before the all-reduce) when given
 template <typename T>
 static void bn_bwd_finish_t(const T* dy, const uint8_t* mk, const T* x, const float* mean, const float* invstd,
                             const T* gamma, long M, long M_total, int C, int relu, const float* row, int nrows,
-                            T* dgamma, T* dbeta, float* coef, T* dx, T* dres, int acc, hipStream_t st) {
+                            T* dgamma, T* dbeta, float* coef, T* dx, T* dres, int acc, hipStream_t st,
+                            const float* prow = nullptr) {
     bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(row, nrows, C, M_total, gamma, invstd, dgamma, dbeta, coef,
-                                                         acc);
+                                                         acc, prow);
     if (rows_ok(C)) {
         const int gr = rows_grid(M, C);
         if (relu) {
@@ -907,16 +912,18 @@ static void bn_bwd_finish_t(const T* dy, const uint8_t* mk, const T* x, const fl
 
 DDL_API int ddl_bn_bwd_finish(int dtype, const void* dy, const void* mask, const void* x, const float* mean,
                               const float* invstd, const void* gamma, long M, long M_total, int C, int relu,
-                              const float* row, void* dgamma, void* dbeta, float* coef, void* dx, void* dres,
-                              int acc_params, hipStream_t st) {
+                              const float* row, const float* local_row, void* dgamma, void* dbeta, float* coef,
+                              void* dx, void* dres, int acc_params, hipStream_t st) {
     if (!rows_ok(C) || (relu && !mask)) return -1;
     const uint8_t* mk = (const uint8_t*)mask;
     if (dtype == 1)
         bn_bwd_finish_t((const bf16_t*)dy, mk, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M, M_total, C,
-                        relu, row, 1, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
+                        relu, row, 1, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st,
+                        local_row);
     else
         bn_bwd_finish_t((const float*)dy, mk, (const float*)x, mean, invstd, (const float*)gamma, M, M_total, C,
-                        relu, row, 1, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st);
+                        relu, row, 1, (float*)dgamma, (float*)dbeta, coef, (float*)dx, (float*)dres, acc_params, st,
+                        local_row);
     DDL_RETURN_LAUNCH();
 }
 

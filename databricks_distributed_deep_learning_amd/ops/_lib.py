@@ -111,7 +111,7 @@ _SIGS = {
     "ddl_bn_rows_sum": [P, I, I, P, P, P],
     "ddl_bn_stats_partials": [I, P, L, I, P, P],
     "ddl_bn_bwd_partials": [I, P, P, P, P, P, L, I, I, P, P],
-    "ddl_bn_bwd_finish": [I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P, P, I, P],
+    "ddl_bn_bwd_finish": [I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P, P, P, I, P],
     "ddl_bn_bwd_from_partials": [I, P, I, P, L, P, P, P, P, P, L, I, P, P, P, P, P, I, P],
     "ddl_bn_partials_ws": [I, I],
     "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],

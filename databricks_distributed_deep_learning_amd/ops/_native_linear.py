@@ -32,10 +32,13 @@ _DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
 
 def _transposed(param, w: torch.Tensor) -> torch.Tensor:
-    """W^T for the NT dgrad, cached on the parameter until the weights change (the
-    optimizer's in-place update bumps the shared version counter): one transpose per
-    optimizer step instead of one per backward."""
-    key = (w.data_ptr(), w._version, tuple(w.shape))
+    """W^T for the NT dgrad, cached on the parameter until the weights change: one
+    transpose per optimizer step instead of one per backward.  An in-place torch update
+    bumps ``w._version``; the flat optimizers write the arena behind the views' version
+    counters and bump the arena's ``generation`` instead, so the key holds both."""
+    ref = getattr(param, "_ddl_arena", None) if param is not None else None
+    arena = ref() if ref is not None else None
+    key = (w.data_ptr(), w._version, tuple(w.shape), arena.generation if arena is not None else -1)
     c = getattr(param, "_ddl_wt", None) if param is not None else None
     if c is not None and c[0] == key:
         return c[1]

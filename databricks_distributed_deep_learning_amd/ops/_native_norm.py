@@ -119,9 +119,10 @@ class _BatchNormTrain(torch.autograd.Function):
             if ctx.group is not None:
                 row = torch.empty(2 * C, **f32)
                 call("ddl_bn_rows_sum", p(gpart), nrows, 2 * C, p(row), None)
+                local = row.clone()             # dgamma / dbeta stay this rank's partials
                 _group_sum(row, ctx.group)
                 call("ddl_bn_bwd_finish", dcode(x), p(dy), None, p(x), p(stats[0]), p(stats[1]), p(weight), M,
-                     ctx.m_total, C, 0, p(row), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+                     ctx.m_total, C, 0, p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
             else:
                 ws = gpart[nrows * 2 * C:]
                 call("ddl_bn_bwd_from_partials", dcode(x), p(gpart), nrows, p(ws), ws.numel(), p(dy), p(x),
@@ -133,9 +134,13 @@ class _BatchNormTrain(torch.autograd.Function):
                  int(ctx.relu), p(part))
             row = torch.empty(2 * C, **f32)
             call("ddl_bn_rows_sum", p(part), nblk, 2 * C, p(row), None)
+            # the group sum feeds the dx coefficients only: dgamma / dbeta are per-rank partials
+            # (the data-parallel reducer sums them), as in the CPU reference
+            local = row.clone()
             _group_sum(row, ctx.group)
             call("ddl_bn_bwd_finish", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M,
-                 ctx.m_total, C, int(ctx.relu), p(row), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+                 ctx.m_total, C, int(ctx.relu), p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres),
+                 int(direct))
         else:
             call("ddl_bn_bwd", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M, C,
                  int(ctx.relu), p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))

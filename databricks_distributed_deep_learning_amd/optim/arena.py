@@ -18,6 +18,7 @@ bf16 and fp32 never straddle tensors.
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -70,13 +71,22 @@ class ParamArena:
         self.entries = entries
         self.flat = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad = torch.zeros(off, dtype=self.dtype, device=self.device)
+        # Bumped by every write to ``flat`` that bypasses the parameters' own version
+        # counters (the flat optimizers write through raw pointers / the arena tensor,
+        # whose counter is not the views'): caches derived from a weight key on it.
+        self.generation = 0
         with torch.no_grad():
             for e in entries:
                 view = self.flat[e.offset:e.offset + e.numel].view(e.shape)
                 view.copy_(e.param.data)
                 e.param.data = view
                 e.param.grad = self.grad[e.offset:e.offset + e.numel].view(e.shape)
+                e.param._ddl_arena = weakref.ref(self)
         self._tables: Dict[Tuple[str, int], torch.Tensor] = {}
+
+    def bump(self) -> None:
+        """Record that the parameters changed (invalidates weight-derived caches)."""
+        self.generation += 1
 
     # ------------------------------------------------------------------
     def rebind_grads(self) -> None:

@@ -42,8 +42,9 @@ class FlatOptimizer:
         self.lo, self.hi = 0, arena.numel
         if shard is not None and shard[1] > 1:
             rank, world = shard
-            if arena.numel % (world * 8):
-                raise ValueError("sharded optimizer: build the arena with pad_multiple = world * 64")
+            if arena.numel % (world * 64):
+                raise ValueError("sharded optimizer: build the arena with pad_multiple = world * 64 "
+                                 "(64-element-aligned slice boundaries)")
             size = arena.numel // world
             self.shard = (rank, world)
             self.lo, self.hi = rank * size, (rank + 1) * size
@@ -113,6 +114,7 @@ class FlatOptimizer:
                 self.arena.flat[self.lo:self.hi].copy_(self.master)
         if self.shard is not None:
             self._all_gather_params()
+        self.arena.bump()
 
     # ------------------------------------------------------------------
     def _full(self, t: torch.Tensor) -> torch.Tensor:
@@ -154,6 +156,7 @@ class FlatOptimizer:
             self.arena.flat.copy_(full.to(self.arena.flat.dtype))
         for k, t in self._state_tensors().items():
             t.copy_(self._fit(st[k])[lo:hi])
+        self.arena.bump()
 
     def _state_tensors(self) -> Dict[str, torch.Tensor]:
         return {}

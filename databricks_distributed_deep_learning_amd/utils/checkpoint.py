@@ -8,7 +8,8 @@ no optimizer state and no load path.  Here a checkpoint is a directory:
 * ``optim.safetensors``  - flat optimizer state (fp32 master, moments)
 * ``meta.json``          - step, config, optimizer scalars, RNG seeds
 
-Rank 0 writes, every rank barriers, every rank loads (collective C5).
+Every rank gathers the optimizer state (collective when it is sharded), rank 0
+writes, every rank barriers, every rank loads (collective C5).
 """
 from __future__ import annotations
 
@@ -28,14 +29,16 @@ def _cpu(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
 def save(path: str, model: torch.nn.Module, optimizer=None, step: int = 0, config: Optional[Dict] = None,
          extra: Optional[Dict[str, Any]] = None) -> None:
     from safetensors.torch import save_file
+    # every rank takes the optimizer state: a sharded (ZeRO-1) optimizer all-gathers its
+    # slices inside state_dict(), a collective all ranks must enter in the same order
+    st = optimizer.state_dict() if optimizer is not None else None
     if ddist.is_main():
         os.makedirs(path, exist_ok=True)
         msd = model.state_dict()
         # safetensors refuses shared storage; clone so views of the arena are independent
         save_file({k: v.clone() for k, v in _cpu(msd).items()}, os.path.join(path, "model.safetensors"))
         meta: Dict[str, Any] = {"step": step, "config": config or {}, "extra": extra or {}}
-        if optimizer is not None:
-            st = optimizer.state_dict()
+        if st is not None:
             tensors = {k: v for k, v in st.items() if isinstance(v, torch.Tensor)}
             scalars = {k: v for k, v in st.items() if not isinstance(v, torch.Tensor)}
             save_file(_cpu(tensors), os.path.join(path, "optim.safetensors"))
@@ -45,6 +48,7 @@ def save(path: str, model: torch.nn.Module, optimizer=None, step: int = 0, confi
         with open(tmp, "w") as f:
             json.dump(meta, f, indent=1, sort_keys=True, default=str)
         os.replace(tmp, os.path.join(path, "meta.json"))
+    del st
     ddist.barrier()
 
 

@@ -120,6 +120,28 @@ def _train_resnet18_gloo(tmpdir):
     return {"summary": s, "resumed_step": resumed_step, "loss2": s2["final_loss"]}
 
 
+def _train_zero_checkpoint(tmpdir):
+    """ZeRO-1 + checkpointing: state_dict() all-gathers the sharded state, so every rank
+    must take it (a rank-0-only call deadlocks against the others' barrier)."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    cfg = get_preset("resnet18_gloo", batch_size=2, image_size=32, steps=2, warmup_steps=0, optimizer="adamw",
+                     lr=1e-3, checkpoint_dir=os.path.join(tmpdir, "ckz"), checkpoint_every=1, num_classes=10,
+                     zero_optimizer=True)
+    t = Trainer(cfg)
+    assert t.opt.shard is not None
+    s = t.run()
+    master, m, v = t.opt.master.clone(), t.opt.m.clone(), t.opt.v.clone()
+    t2 = Trainer(cfg.replace(resume=True, steps=1))
+    err = max((t2.opt.master - master).abs().max().item(), (t2.opt.m - m).abs().max().item(),
+              (t2.opt.v - v).abs().max().item())
+    resumed = t2.step
+    s2 = t2.run()
+    return {"rank": dist.get_rank(), "err": err, "resumed_step": resumed, "loss": s["final_loss"],
+            "loss2": s2["final_loss"]}
+
+
 def _broadcast_init_check():
     import torch.distributed as dist
     from databricks_distributed_deep_learning_amd.parallel import DataParallel
@@ -257,3 +279,10 @@ def test_notebook_train_resnet18_gloo_world2_with_resume(tmp_path):
     assert s["samples_per_sec"] > 0 and s["final_loss"] == s["final_loss"]
     assert out["resumed_step"] == 3
     assert out["loss2"] == out["loss2"]
+
+
+def test_zero1_checkpoint_save_and_resume_world2(tmp_path):
+    out = Distributor(num_processes=2, use_gpu=False, timeout_s=600).run(_train_zero_checkpoint, str(tmp_path))
+    assert out["err"] == 0.0, out
+    assert out["resumed_step"] == 2, out
+    assert out["loss2"] == out["loss2"], out

@@ -28,3 +28,28 @@ def test_mlflow_off_by_default(tmp_path, monkeypatch):
     off = JsonlLogger(str(tmp_path / "b.jsonl"), enabled=False, mlflow=True)
     off.log({"step": 0, "loss": 2.0})
     assert not (tmp_path / "b.jsonl").exists() and off._mlflow is None
+
+
+def test_transposed_weight_cache_follows_flat_optimizer():
+    """W^T cached for the NT dgrad is keyed on the arena generation the flat optimizers
+    bump (their writes bypass the parameter views' version counters)."""
+    import torch
+    from databricks_distributed_deep_learning_amd.ops._native_linear import _transposed
+    from databricks_distributed_deep_learning_amd.optim import FlatAdamW, FlatSGD, ParamArena
+    for cls in (FlatSGD, FlatAdamW):
+        torch.manual_seed(0)
+        lin = torch.nn.Linear(16, 8)
+        arena = ParamArena(list(lin.named_parameters()))
+        opt = cls(arena, lr=0.5)
+        for _ in range(3):
+            assert torch.equal(_transposed(lin.weight, lin.weight), lin.weight.t())
+            arena.grad.normal_()
+            before = lin.weight.detach().clone()
+            opt.step()
+            assert not torch.equal(before, lin.weight)
+        st = opt.state_dict()
+        _transposed(lin.weight, lin.weight)
+        arena.grad.normal_()
+        opt.step()
+        opt.load_state_dict(st)           # weights restored from the master copy
+        assert torch.equal(_transposed(lin.weight, lin.weight), lin.weight.t())
