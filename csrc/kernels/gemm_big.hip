@@ -34,6 +34,7 @@
 #include "ddl_common.h"
 
 #include <cstdlib>
+#include <mutex>
 
 namespace {
 
@@ -88,7 +89,10 @@ struct BigParams {
     const uint8_t* bn_mask;   // ACT_BNB: BatchNorm backward reduction fused into the dgrad (gemm.hip Params)
     const float* bn_mean;
     const float* bn_istd;
+    int* sched;               // persistent grid: per-XCD tile tickets (null: static tile striding)
 };
+// tile-ticket slot layout: 8 per-XCD counters + one exit counter, 128 B apart
+constexpr int SCHED_STRIDE = 32;
 enum BehindBits { BEHIND_BIAS = 1, BEHIND_GELU = 2, BEHIND_RES = 4 };
 enum EpiKind { EK_GEN = 0, EK_BF16 = 1, EK_F32 = 2, EK_GELU = 3, EK_DGELU = 4, EK_BNB = 5, EK_BNBC = 6 };
 
@@ -249,6 +253,16 @@ struct Stager {
     }
 };
 
+// Transposed LDS read through a restrict-qualified parameter: inlined, the read
+// carries alias-scope metadata, which is what keeps the compiler's LDS-DMA tracking
+// from putting an `s_waitcnt vmcnt(0)` in front of every ds_read_b64_tr_b16 (a bare
+// builtin read has no alias info, so it waited out ALL in-flight operand DMA -- the
+// whole 3-half-tile prefetch of the reduction-outer (NN / TN) kernels, every phase).
+// The schedule's own counted vmcnt waits + barriers order DMA and reads.
+__device__ __forceinline__ s16x4 ds_read_tr(lds_v4* __restrict__ p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+}
+
 // fragment: operand rows rbase..rbase+15 of half h, k = 32 kk + 8 (lane>>4) + 0..7
 template <int L>
 __device__ __forceinline__ bf16x8 frag(const char* hbase, int rbase, int kk) {
@@ -263,8 +277,8 @@ __device__ __forceinline__ bf16x8 frag(const char* hbase, int rbase, int kk) {
         const int ra = kk * 32 + 8 * g + q, rb = ra + 4;
         const char* pa = hbase + ra * 256 + ((chunk ^ swz_ko(ra)) << 4) + (pq & 1) * 8;
         const char* pb = hbase + rb * 256 + ((chunk ^ swz_ko(rb)) << 4) + (pq & 1) * 8;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pa);
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pb);
+        s16x4 lo = ds_read_tr((lds_v4*)pa);
+        s16x4 hi = ds_read_tr((lds_v4*)pb);
         typedef short s16x8 __attribute__((ext_vector_type(8)));
         s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8, r);
@@ -644,7 +658,9 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
 // registers it needs never weigh on the other epilogues)
 template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[8 * HALF];
+    // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
+    // makes the compiler's LDS-DMA alias tracking wait vmcnt(0) before fragment reads)
+    __shared__ __attribute__((aligned(16))) char smem[8 * HALF + 16];
     const int nwg = p.tiles_m * p.tiles_n;
     int tm, tn, m0, n0;
     // XCD-aware bijective remap: an XCD (blockIdx & 7) owns a contiguous range of
@@ -664,8 +680,29 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         m0 = tm * TB;
         n0 = tn * TB;
     };
+    // Tile order.  Static: block b walks tiles b, b + gridDim.x, ... (same XCD range).
+    // Dynamic (p.sched, gridDim.x % 8 == 0): the first tile is static, every further one
+    // a ticket from this XCD's counter, so a block that starts late (its CU held by a
+    // concurrent RCCL collective, whose resident blocks leave no room for this kernel's
+    // 256-VGPR waves) takes fewer tiles instead of extending the GEMM by its whole static
+    // share.  Thread 0 asks for the ticket of the tile after next once a tile's
+    // coordinates are known, before that tile's prologue loads, and publishes it through
+    // LDS after the prologue wait that retired it (the main loop's barriers order the
+    // publication before the read at the end of the tile).
+    // (not in the BatchNorm-backward instantiations: their register budget has no room,
+    // and their dgrad shapes have fewer tiles than CUs)
+    constexpr bool DYN = DIRECT && !BNB;
+    int& s_tick = *reinterpret_cast<int*>(smem + 8 * HALF);
+    int tick = 0;
+    auto ask = [&]() {
+        if (DYN && p.sched && threadIdx.x == 0) tick = atomicAdd(p.sched + (blockIdx.x & 7) * SCHED_STRIDE, 1);
+    };
+    auto publish = [&]() {
+        if (DYN && p.sched && threadIdx.x == 0) s_tick = tick;
+    };
     int vt = blockIdx.x;
     coords(vt);
+    ask();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = w >> 2, wn = w & 3;
     const int split = blockIdx.y;
@@ -778,6 +815,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         prologueE();
         prologueO();
     }
+    publish();
     for (;;) {
         if (nK > 0) {
             const int pairs = nK / 2;
@@ -820,7 +858,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
 #endif
         }
         if (DIRECT) {
-            const int vn = vt + gridDim.x;
+            // dynamic: ticket t of XCD x is its range's tile gridDim.x/8 + t, i.e. the
+            // static-order id 8 * (gridDim.x/8 + t) + x
+            const int vn = (DYN && p.sched) ? (int)((((gridDim.x >> 3) + s_tick) << 3) + (blockIdx.x & 7))
+                                             : vt + (int)gridDim.x;
             const bool next = vn < nwg;
             const int m0c = m0, n0c = n0, tm_c = tm;
             const bool interior = m0c + TB <= p.M && n0c + TB <= p.N;
@@ -839,6 +880,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                  (p.ek == EK_GELU && (p.behind_mask & BEHIND_GELU)));
             if (next) {
                 coords(vn);
+                ask();
                 sa.init(p, m0);
                 sb.init(p, n0);
                 if (nK > 0) prologueE();
@@ -862,7 +904,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 epi_direct<EK_DGELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else
                 epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
-            if (!next) return;
+            if (!next) {
+                if constexpr (DYN) break;    // the ticket slot's exit bookkeeping below the loop
+                return;
+            }
             zero_acc();
             vt = vn;
             if (nK > 0) {
@@ -886,10 +931,27 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 } else {
                     prologueO();
                 }
+            } else {
+                BARRIER();
             }
+            // on every path (the compiler's wait for the ticket then lands here, not in
+            // the next main loop), after a barrier that follows every wave's read of s_tick
+            publish();
             continue;
         }
         break;
+    }
+    if constexpr (DYN) {
+        if (p.sched && threadIdx.x == 0) {
+            // the last block out re-arms the ticket slot for its next launch
+            int* done = p.sched + 8 * SCHED_STRIDE;
+            if (atomicAdd(done, 1) == (int)gridDim.x - 1) {
+#pragma unroll 1
+                for (int i = 0; i < 8; ++i) atomicExch(p.sched + i * SCHED_STRIDE, 0);
+                atomicExch(done, 0);
+            }
+        }
+        return;
     }
 
     // ---------------- LDS-staged epilogue (general: every epilogue option)
@@ -1042,6 +1104,39 @@ bool direct_enabled() {
     return on;
 }
 
+// DDL_GEMM_DYNAMIC=0 keeps the static tile striding of the persistent grid (A/B timing)
+bool dynamic_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_DYNAMIC");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Tile-ticket slots of the persistent kernel, per device: SLOTS launches in flight at
+// most (the launching stream orders the rest), each slot zero at launch and re-armed by
+// the launch's last block.  Null while a stream is being captured before the first
+// allocation (the kernel then strides statically).
+int* sched_slot(hipStream_t st) {
+    constexpr int SLOTS = 64, DEVS = 16;
+    constexpr size_t SLOT_INTS = 9 * SCHED_STRIDE;
+    static int* base[DEVS] = {};
+    static unsigned next[DEVS] = {};
+    static std::mutex mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= DEVS) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!base[dev]) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        int* b = nullptr;
+        if (hipMalloc(&b, SLOTS * SLOT_INTS * sizeof(int)) != hipSuccess) return nullptr;
+        if (hipMemsetAsync(b, 0, SLOTS * SLOT_INTS * sizeof(int), st) != hipSuccess) return nullptr;
+        base[dev] = b;
+    }
+    return base[dev] + (size_t)(next[dev]++ % SLOTS) * SLOT_INTS;
+}
+
 // DDL_GEMM_BEHIND: BEHIND_* bits -- which register epilogues besides plain bf16 let
 // their stores drain under the next tile's prologue.  Measured neutral (bias, GELU:
 // profiles/epilogue_behind_ab.log) to -8 % (residual), so all off by default
@@ -1101,6 +1196,7 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
         // one block per (tile, split) -- a capped grid would leave tiles for a second round
         const int cap = std::max(8, num_cus() & ~7);
         gx = std::min(nwg, cap);
+        if (gx < nwg && p.act != ACT_BNB && dynamic_enabled()) kp.sched = sched_slot(st);
     }
     const dim3 grid(gx, splits);
     if (direct) {

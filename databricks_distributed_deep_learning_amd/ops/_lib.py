@@ -23,7 +23,8 @@ from typing import Optional
 import torch
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_DIR, "_native", "libddl_kernels.so")
+# DDL_NATIVE_LIB: load another build of the library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("DDL_NATIVE_LIB") or os.path.join(_PKG_DIR, "_native", "libddl_kernels.so")
 
 _lib: Optional[ctypes.CDLL] = None
 _load_error: Optional[str] = None

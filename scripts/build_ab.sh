@@ -1,0 +1,22 @@
+#!/bin/bash
+# Build an A/B variant of the kernel library with ONE source file taken from a git revision:
+#   scripts/build_ab.sh <rev> <csrc/kernels/file.hip> <name>
+# -> databricks_distributed_deep_learning_amd/_native/ab/libddl_<name>.so (load with DDL_NATIVE_LIB=...)
+set -euo pipefail
+rev=$1; src=$2; name=$3
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/databricks_distributed_deep_learning_amd/_native/ab
+tmp=$(mktemp -d)
+mkdir -p "$out"
+python "$root/csrc/build.py" >/dev/null
+git -C "$root" show "$rev:$src" > "$tmp/$(basename "$src")"
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I "$root/csrc/include" -Wno-unused-result \
+    -ffp-contract=fast -munsafe-fp-atomics -c "$tmp/$(basename "$src")" -o "$tmp/variant.o"
+objs=()
+for o in "$root"/build/native/*.o; do
+  [ "$(basename "$o")" = "$(basename "$src").o" ] && objs+=("$tmp/variant.o") || objs+=("$o")
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 "${objs[@]}" -o "$out/libddl_$name.so" \
+    -L/opt/rocm/lib -Wl,--no-as-needed -lamdhip64 -ldl
+rm -rf "$tmp"
+echo "$out/libddl_$name.so"
