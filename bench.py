@@ -33,7 +33,7 @@ def run_one(model: str, args, world: int):
     else:
         cfg = get_preset("bert_base_ddp", batch_size=args.bert_batch or 128, dropout=0.1)
     cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
-                      bucket_mb=args.bucket_mb, cuda_graph=args.cuda_graph, backend=args.backend,
+                      bucket_mb=args.bucket_mb, backend=args.backend,
                       zero_optimizer=args.zero, sync_bn=args.sync_bn)
     tr = Trainer(cfg)
     s = tr.run()
@@ -51,7 +51,6 @@ def main() -> int:
     ap.add_argument("--bert-batch", type=int, default=0, help="BERT-base per-GPU batch (default 128)")
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--bucket-mb", type=float, default=25.0)
-    ap.add_argument("--cuda-graph", action="store_true")
     ap.add_argument("--zero", action="store_true", help="ZeRO-1: shard fp32 master + optimizer state over ranks")
     ap.add_argument("--sync-bn", action="store_true", help="SyncBatchNorm (CV models)")
     ap.add_argument("--backend", default=os.environ.get("DDL_BACKEND", "auto"),

@@ -101,15 +101,23 @@ ncclDataType_t dtype_of(int code) {
     }
 }
 
+constexpr int RING = 64;
+
 struct Engine {
     ncclComm_t comm = nullptr;
     hipStream_t stream = nullptr;    // collectives run here, concurrent with compute
     hipEvent_t produced = nullptr;   // compute -> comm ordering
     hipEvent_t drained = nullptr;    // comm -> compute ordering
+    hipEvent_t done[RING] = {};      // done[i % RING]: recorded after all-reduce number i + 1
     int rank = 0, world = 1, device = 0;
     long launched = 0;
     long bytes = 0;
 };
+
+// all-reduce number e->launched just went onto the comm stream: mark its completion
+bool mark_done(Engine* e) {
+    return hok(hipEventRecord(e->done[(e->launched - 1) % RING], e->stream), "hipEventRecord");
+}
 
 // compute stream -> comm stream dependency (the event is re-recorded per call;
 // hipStreamWaitEvent binds to the record that precedes it)
@@ -146,6 +154,11 @@ DDL_API void* ddl_comm_create(const char* rccl_path, const char* id_bytes, int w
         delete e;
         return nullptr;
     }
+    for (int i = 0; i < RING; ++i)
+        if (!hok(hipEventCreateWithFlags(&e->done[i], hipEventDisableTiming), "hipEventCreate")) {
+            delete e;
+            return nullptr;
+        }
     ncclUniqueId id;
     std::memcpy(id.internal, id_bytes, NCCL_UNIQUE_ID_BYTES);
     if (!ok(g_rccl.commInitRank(&e->comm, world, id, rank), "ncclCommInitRank")) {
@@ -165,7 +178,7 @@ DDL_API int ddl_comm_allreduce(void* h, void* buf, long count, int dtype, int av
         return -2;
     e->launched += 1;
     e->bytes += count * (dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2);
-    return 0;
+    return mark_done(e) ? 0 : -3;
 }
 
 // several buckets that became ready together: one fused RCCL group launch
@@ -175,6 +188,7 @@ DDL_API int ddl_comm_allreduce_many(void* h, void** bufs, const long* counts, in
     if (!e) return -1;
     if (!order_after(e, compute)) return -3;
     if (!ok(g_rccl.groupStart(), "ncclGroupStart")) return -2;
+    const long before = e->launched;
     for (int i = 0; i < n; ++i) {
         if (counts[i] <= 0) continue;
         if (!ok(g_rccl.allReduce(bufs[i], bufs[i], (size_t)counts[i], dtype_of(dtype), avg ? ncclAvg : ncclSum,
@@ -185,7 +199,11 @@ DDL_API int ddl_comm_allreduce_many(void* h, void** bufs, const long* counts, in
         }
         e->launched += 1;
     }
-    return ok(g_rccl.groupEnd(), "ncclGroupEnd") ? 0 : -2;
+    if (!ok(g_rccl.groupEnd(), "ncclGroupEnd")) return -2;
+    // every number of the group completes at the same point of the comm stream
+    for (long k = before; k < e->launched; ++k)
+        if (!hok(hipEventRecord(e->done[k % RING], e->stream), "hipEventRecord")) return -3;
+    return 0;
 }
 
 DDL_API int ddl_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t compute) {
@@ -230,6 +248,16 @@ DDL_API int ddl_comm_wait(void* h, hipStream_t compute) {
                : -3;
 }
 
+// compute stream waits for all-reduce number `seq` (1-based, as counted by ddl_comm_stats(h, 0))
+// and, the comm stream being in order, everything issued before it.  A number more than
+// RING behind the newest waits for a later one instead (still correct, just later).
+DDL_API int ddl_comm_wait_upto(void* h, long seq, hipStream_t compute) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e || seq < 1 || seq > e->launched) return -1;
+    if (e->launched - seq >= RING) seq = e->launched;
+    return hok(hipStreamWaitEvent(compute, e->done[(seq - 1) % RING], 0), "hipStreamWaitEvent") ? 0 : -3;
+}
+
 DDL_API int ddl_comm_synchronize(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
@@ -252,6 +280,8 @@ DDL_API void ddl_comm_destroy(void* h, int abort) {
             g_rccl.commDestroy(e->comm);
         }
     }
+    for (int i = 0; i < RING; ++i)
+        if (e->done[i]) hipEventDestroy(e->done[i]);
     if (e->produced) hipEventDestroy(e->produced);
     if (e->drained) hipEventDestroy(e->drained);
     if (e->stream) hipStreamDestroy(e->stream);

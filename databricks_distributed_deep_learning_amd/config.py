@@ -51,9 +51,9 @@ class TrainConfig:
     broadcast_buffers: bool = False
     sync_bn: bool = False            # SyncBatchNorm: BN statistics summed over all ranks (CV models)
     zero_optimizer: bool = False     # ZeRO-1: fp32 master + optimizer state sharded 1/world per rank
+    overlap_optimizer: bool = True   # world > 1: per-bucket optimizer updates as each all-reduce completes
     # ---- runtime ----------------------------------------------------------
     native: str = "auto"             # auto|on|off  HIP kernels (off = stock torch ops)
-    cuda_graph: bool = False         # capture the whole train step in a hipGraph
     seed: int = 1234
     log_every: int = 10
     log_file: str = ""               # JSONL metrics (rank 0)

@@ -1,6 +1,8 @@
 """Fused flat-arena optimizer launches (csrc/kernels/optim.hip)."""
 from __future__ import annotations
 
+import bisect
+
 import torch
 
 from ._lib import call, dcode, p
@@ -27,7 +29,19 @@ def _table(opt):
             rows.append((opt.lo, 0, 0, 0))
         t = torch.tensor(rows, dtype=torch.int32, device=opt.arena.device)
         opt._native_table = t
+        opt._native_starts = [r[0] for r in rows]
     return t
+
+
+def _rows(opt, rng):
+    """(table pointer, row count) for the whole table or the rows of arena range [lo, hi)
+    (range steps: bucket boundaries are tensor boundaries, so whole rows)."""
+    tab = _table(opt)
+    if rng is None:
+        return tab.data_ptr(), tab.shape[0]
+    starts = opt._native_starts
+    r0, r1 = bisect.bisect_left(starts, rng[0]), bisect.bisect_left(starts, rng[1])
+    return tab.data_ptr() + r0 * tab.stride(0) * tab.element_size(), r1 - r0
 
 
 def _state(t: torch.Tensor, opt) -> int:
@@ -49,38 +63,46 @@ def _scale_tensor(scale, device):
     return torch.full((1,), float(scale), dtype=torch.float32, device=device)
 
 
-def sgd(opt, grad, scale):
-    tab = _table(opt)
+def sgd(opt, grad, scale, rng=None):
+    tab, nrow = _rows(opt, rng)
     master, param, pdt = _targets(opt)
     s = _scale_tensor(scale, grad.device)
-    call("ddl_sgd_step", dcode(grad), p(grad), master, pdt, p(param), _state(opt.buf, opt), p(tab), tab.shape[0], p(s),
+    call("ddl_sgd_step", dcode(grad), p(grad), master, pdt, p(param), _state(opt.buf, opt), tab, nrow, p(s),
          float(opt.lr), float(opt.momentum), float(opt.weight_decay), int(opt.nesterov), int(opt.step_count == 1))
 
 
-def adamw(opt, grad, scale):
-    tab = _table(opt)
+def adamw(opt, grad, scale, rng=None):
+    tab, nrow = _rows(opt, rng)
     master, param, pdt = _targets(opt)
     s = _scale_tensor(scale, grad.device)
     t = opt.step_count
     call("ddl_adamw_step", dcode(grad), p(grad), master, pdt, p(param), _state(opt.m, opt), _state(opt.v, opt),
-         p(tab), tab.shape[0],
+         tab, nrow,
          p(s), float(opt.lr), float(opt.b1), float(opt.b2), float(opt.eps), float(opt.weight_decay),
          float(1 - opt.b1 ** t), float(1 - opt.b2 ** t))
 
 
-def lamb(opt, grad, scale):
-    tab = _table(opt)
+def lamb(opt, grad, scale, rng=None):
     master, param, pdt = _targets(opt)
     s = _scale_tensor(scale, grad.device)
     t = opt.step_count
-    norms = torch.zeros(2 * len(opt.arena.entries), dtype=torch.float32, device=grad.device)
+    if rng is None:
+        norms = torch.zeros(2 * len(opt.arena.entries), dtype=torch.float32, device=grad.device)
+    else:   # one zeroed per-tensor norm buffer per range-stepped step (each range fills its own tensors)
+        scratch = opt._range_scratch
+        norms = scratch.get("norms")
+        if norms is None:
+            norms = scratch["norms"] = torch.zeros(2 * len(opt.arena.entries), dtype=torch.float32,
+                                                   device=grad.device)
     bc1 = (1 - opt.b1 ** t) if opt.bias_correction else 1.0
     bc2 = (1 - opt.b2 ** t) if opt.bias_correction else 1.0
     if opt.shard is None:
-        call("ddl_lamb_step", dcode(grad), p(grad), master, pdt, p(param), p(opt.m), p(opt.v), p(tab), tab.shape[0],
+        tp, nrow = _rows(opt, rng)
+        call("ddl_lamb_step", dcode(grad), p(grad), master, pdt, p(param), p(opt.m), p(opt.v), tp, nrow,
              p(s), float(opt.lr), float(opt.b1), float(opt.b2), float(opt.eps), float(opt.weight_decay), float(bc1),
              float(bc2), p(norms))
         return
+    tab = _table(opt)
     # sharded: the per-tensor norms of every rank's slice are summed between the phases
     import torch.distributed as dist
     m, v = _state(opt.m, opt), _state(opt.v, opt)

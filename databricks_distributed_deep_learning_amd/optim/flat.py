@@ -98,6 +98,39 @@ class FlatOptimizer:
             return clip * grad_scale
         return torch.full((), grad_scale, dtype=torch.float32, device=grad.device)
 
+    # ------------------------------------------------------------------ range steps
+    # The data-parallel reducer can hand the optimizer one bucket (a contiguous range of
+    # whole tensors) at a time, as each bucket's all-reduce completes: begin_step(),
+    # step_range() per bucket, end_step() is the same update as one step() when no
+    # global quantity (clip norm) couples the ranges and the state is not sharded.
+    def supports_ranges(self) -> bool:
+        return self.shard is None and not (self.max_grad_norm and self.max_grad_norm > 0)
+
+    def begin_step(self, lr: Optional[float] = None) -> None:
+        if not self.supports_ranges():
+            raise RuntimeError(f"{self.name}: range steps need an unsharded optimizer without gradient clipping")
+        self.step_count += 1
+        if lr is not None:
+            self.lr = lr
+        self._range_scratch: Dict[str, object] = {}
+
+    @torch.no_grad()
+    def step_range(self, grad: torch.Tensor, grad_scale: float, lo: int, hi: int) -> None:
+        """Update arena elements [lo, hi) (tensor-aligned) from the full-arena ``grad``."""
+        if hi <= lo:
+            return
+        if self._native():
+            self._step_native(grad, self._range_scratch.setdefault(
+                "scale", torch.full((1,), float(grad_scale), dtype=torch.float32, device=grad.device)), (lo, hi))
+        else:
+            self._step_torch(grad[lo:hi].float() * grad_scale, lo, hi)
+            if self.master is not None:
+                self.arena.flat[lo:hi].copy_(self.master[lo:hi])
+
+    def end_step(self) -> None:
+        self._range_scratch = {}
+        self.arena.bump()
+
     @torch.no_grad()
     def step(self, grad: Optional[torch.Tensor] = None, grad_scale: float = 1.0, lr: Optional[float] = None):
         if grad is None:
@@ -174,20 +207,23 @@ class FlatSGD(FlatOptimizer):
     def _state_tensors(self):
         return {"momentum_buffer": self.buf}
 
-    def _step_torch(self, g):
-        p = self.params32
-        d = g + self.weight_decay * self.decay_mask() * p if self.weight_decay else g
+    def _step_torch(self, g, a=0, b=None):
+        """``g``: the gradient of local elements [a, b) (the whole local range by default)."""
+        b = self.state_numel if b is None else b
+        p = self.params32[a:b]
+        buf = self.buf[a:b]
+        d = g + self.weight_decay * self.decay_mask()[a:b] * p if self.weight_decay else g
         if self.momentum:
             if self.step_count == 1:
-                self.buf.copy_(d)
+                buf.copy_(d)
             else:
-                self.buf.mul_(self.momentum).add_(d)
-            d = d + self.momentum * self.buf if self.nesterov else self.buf
+                buf.mul_(self.momentum).add_(d)
+            d = d + self.momentum * buf if self.nesterov else buf
         p.add_(d, alpha=-self.lr)
 
-    def _step_native(self, grad, scale):
+    def _step_native(self, grad, scale, rng=None):
         from ..ops import _native_optim
-        _native_optim.sgd(self, grad, scale)
+        _native_optim.sgd(self, grad, scale, rng)
 
 
 class FlatAdamW(FlatOptimizer):
@@ -204,21 +240,22 @@ class FlatAdamW(FlatOptimizer):
     def _state_tensors(self):
         return {"exp_avg": self.m, "exp_avg_sq": self.v}
 
-    def _step_torch(self, g):
-        p = self.params32
+    def _step_torch(self, g, a=0, b=None):
+        b = self.state_numel if b is None else b
+        p, m, v = self.params32[a:b], self.m[a:b], self.v[a:b]
         t = self.step_count
         if self.weight_decay:
-            p.mul_(1.0 - self.lr * self.weight_decay * self.decay_mask())
-        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
-        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            p.mul_(1.0 - self.lr * self.weight_decay * self.decay_mask()[a:b])
+        m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
         bc1 = 1 - self.b1 ** t
         bc2 = 1 - self.b2 ** t
-        denom = (self.v / bc2).sqrt_().add_(self.eps)
-        p.addcdiv_(self.m, denom, value=-self.lr / bc1)
+        denom = (v / bc2).sqrt_().add_(self.eps)
+        p.addcdiv_(m, denom, value=-self.lr / bc1)
 
-    def _step_native(self, grad, scale):
+    def _step_native(self, grad, scale, rng=None):
         from ..ops import _native_optim
-        _native_optim.adamw(self, grad, scale)
+        _native_optim.adamw(self, grad, scale, rng)
 
 
 class FlatLAMB(FlatOptimizer):
@@ -237,21 +274,23 @@ class FlatLAMB(FlatOptimizer):
     def _state_tensors(self):
         return {"exp_avg": self.m, "exp_avg_sq": self.v}
 
-    def _step_torch(self, g):
-        p = self.params32
+    def _step_torch(self, g, ra=0, rb=None):
+        rb = self.state_numel if rb is None else rb
+        p, m, v = self.params32[ra:rb], self.m[ra:rb], self.v[ra:rb]
         t = self.step_count
-        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
-        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
         bc1 = 1 - self.b1 ** t if self.bias_correction else 1.0
         bc2 = 1 - self.b2 ** t if self.bias_correction else 1.0
-        u = (self.m / bc1) / ((self.v / bc2).sqrt() + self.eps)
+        u = (m / bc1) / ((v / bc2).sqrt() + self.eps)
         if self.weight_decay:
-            u = u + self.weight_decay * self.decay_mask() * p
-        # per-tensor ||p||^2, ||u||^2 over this rank's part of each tensor (summed over ranks when sharded)
+            u = u + self.weight_decay * self.decay_mask()[ra:rb] * p
+        # per-tensor ||p||^2, ||u||^2 over this rank's part of each tensor (summed over ranks when sharded),
+        # restricted to the tensors of local range [ra, rb); offsets relative to ra
         segs = []
         for e in self.arena.entries:
-            a, b = max(e.offset, self.lo), min(e.offset + e.numel, self.hi)
-            segs.append((a - self.lo, b - self.lo) if a < b else None)
+            a, b = max(e.offset, self.lo + ra), min(e.offset + e.numel, self.lo + rb)
+            segs.append((a - self.lo - ra, b - self.lo - ra) if a < b else None)
         sq = torch.zeros(2 * len(segs), dtype=torch.float32, device=p.device)
         for ti, sg in enumerate(segs):
             if sg is not None:
@@ -267,9 +306,9 @@ class FlatLAMB(FlatOptimizer):
             ratio = torch.where((pn > 0) & (un > 0), pn / un, torch.ones_like(pn))
             p[sg[0]:sg[1]].add_(u[sg[0]:sg[1]] * ratio, alpha=-self.lr)
 
-    def _step_native(self, grad, scale):
+    def _step_native(self, grad, scale, rng=None):
         from ..ops import _native_optim
-        _native_optim.lamb(self, grad, scale)
+        _native_optim.lamb(self, grad, scale, rng)
 
 
 def build_optimizer(name: str, arena: ParamArena, cfg, shard=None) -> FlatOptimizer:

@@ -34,6 +34,7 @@ _SIGS = {
     "ddl_comm_reduce_scatter": ([P, P, P, L, I, I, P], I),
     "ddl_comm_all_gather": ([P, P, P, L, I, P], I),
     "ddl_comm_wait": ([P, P], I),
+    "ddl_comm_wait_upto": ([P, L, P], I),
     "ddl_comm_synchronize": ([P], I),
     "ddl_comm_stats": ([P, I], L),
     "ddl_comm_destroy": ([P, I], None),
@@ -101,6 +102,7 @@ class NativeComm:
         dist.broadcast_object_list(obj, src=src, group=group)
         if isinstance(obj[0], str):
             raise CommError(obj[0])
+        self._seq = 0          # all-reduces issued (the engine's numbering for wait_upto)
         self._h = _fn("ddl_comm_create")(path, obj[0], self.world, self.rank, self.device.index)
         ok = torch.tensor([1 if self._h else 0], device=self.device)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
@@ -112,21 +114,33 @@ class NativeComm:
         if rc != 0:
             raise CommError(f"{what} failed ({rc}): {_err()}")
 
-    def all_reduce(self, t: torch.Tensor, average: bool = False) -> None:
-        """In-place all-reduce of a contiguous GPU tensor on the comm stream (async)."""
+    def all_reduce(self, t: torch.Tensor, average: bool = False) -> int:
+        """In-place all-reduce of a contiguous GPU tensor on the comm stream (async).
+        Returns its sequence number for :meth:`wait_upto` (0: nothing was issued)."""
         assert t.is_cuda and t.is_contiguous()
         self._check(_fn("ddl_comm_allreduce")(self._h, t.data_ptr(), t.numel(), _DTYPES[t.dtype], int(average),
                                               _stream()), "all_reduce")
+        if t.numel() > 0:
+            self._seq += 1
+        return self._seq if t.numel() > 0 else 0
 
-    def all_reduce_many(self, ts: Sequence[torch.Tensor], average: bool = False) -> None:
+    def all_reduce_many(self, ts: Sequence[torch.Tensor], average: bool = False) -> int:
         if not ts:
-            return
+            return 0
         dt = ts[0].dtype
         assert all(t.dtype == dt and t.is_contiguous() for t in ts)
         bufs = (P * len(ts))(*[t.data_ptr() for t in ts])
         counts = (L * len(ts))(*[t.numel() for t in ts])
         self._check(_fn("ddl_comm_allreduce_many")(self._h, bufs, counts, len(ts), _DTYPES[dt], int(average),
                                                    _stream()), "all_reduce_many")
+        self._seq += sum(1 for t in ts if t.numel() > 0)
+        return self._seq
+
+    def wait_upto(self, seq: int) -> None:
+        """Current (compute) stream waits for all-reduce number ``seq`` and every earlier
+        collective: the optimizer can start on a bucket while later ones are in flight."""
+        if seq > 0:
+            self._check(_fn("ddl_comm_wait_upto")(self._h, int(seq), _stream()), "wait_upto")
 
     def broadcast(self, t: torch.Tensor, root: int = 0) -> None:
         self._check(_fn("ddl_comm_broadcast")(self._h, t.data_ptr(), t.numel(), _DTYPES[t.dtype], root, _stream()),

@@ -31,7 +31,7 @@ from __future__ import annotations
 
 import contextlib
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -52,6 +52,7 @@ class Bucket:
     launched: bool = False
     payload: Optional[torch.Tensor] = None
     grads_seen: set = field(default_factory=set)
+    seq: int = 0                 # native engine: this bucket's all-reduce number (wait_upto)
 
 
 class DataParallel(nn.Module):
@@ -138,6 +139,8 @@ class DataParallel(nn.Module):
             b.launched = False
             b.payload = None
             b.grads_seen = set()
+            b.seq = 0
+        self._order: List[Bucket] = []       # buckets in all-reduce launch order
 
     def _make_hook(self, ei: int):
         def hook(_p):
@@ -166,12 +169,14 @@ class DataParallel(nn.Module):
         if b.launched:
             return
         b.launched = True
+        self._order.append(b)
         b.payload = self._payload(b)
         if self.native is not None or self.world > 1:
             if self.native is not None:
                 # payload is the arena slice / fp32 accumulator / a converted copy held
                 # in b.payload until finish() -- alive until the comm stream is drained
-                self.native.all_reduce(b.payload)
+                seq = self.native.all_reduce(b.payload)
+                b.seq = seq if isinstance(seq, int) else 0
             else:
                 b.handle = dist.all_reduce(b.payload, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
@@ -196,17 +201,36 @@ class DataParallel(nn.Module):
                 self.arena.grad.zero_()
                 self._acc_active = True
 
-    def finish(self) -> torch.Tensor:
+    def finish(self, on_ready: Optional[Callable[[torch.Tensor, int, int], None]] = None) -> torch.Tensor:
         """Wait for all buckets; return the flat reduced gradient (SUM over ranks).
 
         The caller scales by ``1/world`` (optimizers take ``grad_scale``).
+
+        ``on_ready(grad, lo, hi)``: called per bucket in all-reduce order once the compute
+        stream has been made to wait for THAT bucket only, with the arena index range it
+        covers -- a range-stepping optimizer updates the early buckets while the last
+        all-reduces (the embedding's, in BERT) are still on the wire.
         """
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
-        for b in self.buckets:
-            if b.handle is not None:
-                b.handle.wait()
+        streamed = on_ready is not None and self.reduce_dtype == self.arena.dtype
+        out_early = self._acc32 if self._acc_active else self.arena.grad
+        if streamed:
+            can_seq = self.native is not None and hasattr(self.native, "wait_upto") and \
+                all(b.seq > 0 for b in self._order if b.end > b.start)
+            if self.native is not None and not can_seq:
+                self.native.wait()          # engine without per-collective marks: one wait
+            for b in self._order:
+                if b.handle is not None:
+                    b.handle.wait()
+                elif self.native is not None and can_seq:
+                    self.native.wait_upto(b.seq)
+                on_ready(out_early, b.start, b.end)
+        else:
+            for b in self.buckets:
+                if b.handle is not None:
+                    b.handle.wait()
         if self.native is not None:
             self.native.wait()
         if self._acc_active:

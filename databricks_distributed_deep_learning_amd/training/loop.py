@@ -66,6 +66,8 @@ class Trainer:
         self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg,
                                    shard=(self.rank, self.world) if zero else None)
         self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
+        self.overlap_optimizer = (self.world > 1 and cfg.overlap_optimizer and self.opt.supports_ranges()
+                                  and self.ddp.reduce_dtype == self.arena.dtype)
         if cfg.batch_size <= 0:
             cfg.batch_size = self._auto_batch()
         self.loader = self._make_loader()
@@ -118,8 +120,17 @@ class Trainer:
                 loss = self.loss_fn(batch)
                 loss.backward()
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
-        grad = self.ddp.finish()
-        self.opt.step(grad, grad_scale=1.0 / (self.world * c.grad_accum), lr=self.sched(self.step))
+        scale = 1.0 / (self.world * c.grad_accum)
+        if self.overlap_optimizer:
+            # each bucket's optimizer update starts as soon as ITS all-reduce is done, so
+            # the last buckets' rings (BERT's 68 MB embedding bucket) run under the update
+            # of everything else instead of in front of it
+            self.opt.begin_step(lr=self.sched(self.step))
+            self.ddp.finish(on_ready=lambda g, lo, hi: self.opt.step_range(g, scale, lo, hi))
+            self.opt.end_step()
+        else:
+            grad = self.ddp.finish()
+            self.opt.step(grad, grad_scale=scale, lr=self.sched(self.step))
         self.step += 1
         return loss_sum / c.grad_accum
 

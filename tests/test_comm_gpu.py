@@ -106,3 +106,35 @@ def test_sync_batchnorm_native_world1(pg, fused_stats):
         outs.append((z.float(), xs.grad.float(), gs.grad.float(), bs.grad.float(), rm, rv))
     for a, c in zip(outs[0], outs[1]):
         torch.testing.assert_close(a, c, rtol=2e-2, atol=2e-2)
+
+
+def test_reducer_native_per_bucket_ready(pg):
+    """finish(on_ready=...) with the native engine: the compute stream waits for each
+    bucket's own all-reduce (wait_upto on the engine's completion ring), and a
+    range-stepped optimizer over those callbacks equals one fused step."""
+    from databricks_distributed_deep_learning_amd.models import resnet18
+    from databricks_distributed_deep_learning_amd.optim import FlatSGD
+    from databricks_distributed_deep_learning_amd.optim.arena import ParamArena
+    from databricks_distributed_deep_learning_amd.parallel.ddp import DataParallel
+    x = torch.randn(4, 64, 64, 3, device=pg)
+    finals = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        m = resnet18(num_classes=10).to(pg)
+        arena = ParamArena(list(m.named_parameters()))
+        ddp = DataParallel(m, arena, bucket_mb=4, first_bucket_mb=1, comm="native")
+        opt = FlatSGD(arena, lr=0.05, momentum=0.9)
+        for _ in range(2):
+            ddp.zero_grad()
+            m(x).float().square().mean().backward()
+            if overlap:
+                opt.begin_step()
+                seqs = []
+                ddp.finish(on_ready=lambda g, lo, hi: (seqs.append(lo), opt.step_range(g, 1.0, lo, hi)))
+                opt.end_step()
+                assert len(seqs) == len(ddp.buckets) > 2
+            else:
+                opt.step(ddp.finish())
+        torch.cuda.synchronize()
+        finals.append(arena.flat.float().clone())
+    torch.testing.assert_close(finals[0], finals[1])

@@ -142,6 +142,41 @@ def _train_zero_checkpoint(tmpdir):
             "loss2": s2["final_loss"]}
 
 
+def _overlap_equivalence(opt_name):
+    """Per-bucket optimizer updates as each all-reduce completes (finish(on_ready=...))
+    == one fused step after the last all-reduce."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.optim import ParamArena
+    from databricks_distributed_deep_learning_amd.optim.flat import FlatAdamW, FlatLAMB, FlatSGD
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    rank, world = dist.get_rank(), dist.get_world_size()
+    cls = {"sgd": FlatSGD, "adamw": FlatAdamW, "lamb": FlatLAMB}[opt_name]
+    kw = {"sgd": dict(lr=0.1, momentum=0.9, weight_decay=1e-3), "adamw": dict(lr=1e-2, weight_decay=0.01),
+          "lamb": dict(lr=1e-2, weight_decay=0.01, max_grad_norm=0.0)}[opt_name]
+    x, y = _data(16)
+    x, y = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+    finals, nb = [], 0
+    for overlap in (False, True):
+        model = _tiny_model()
+        arena = ParamArena(list(model.named_parameters()))
+        ddp = DataParallel(model, arena, bucket_mb=0.0005, first_bucket_mb=0.0002)
+        opt = cls(arena, **kw)
+        nb = len(ddp.buckets)
+        for _ in range(3):
+            ddp.zero_grad()
+            torch.nn.functional.cross_entropy(ddp(x), y).backward()
+            if overlap:
+                opt.begin_step()
+                seen = []
+                ddp.finish(on_ready=lambda g, lo, hi: (seen.append((lo, hi)), opt.step_range(g, 0.5, lo, hi)))
+                opt.end_step()
+                assert sorted(seen) == [(b.start, b.end) for b in ddp.buckets]
+            else:
+                opt.step(ddp.finish(), grad_scale=0.5)
+        finals.append(torch.cat([p.detach().flatten() for p in model.parameters()]))
+    return {"err": (finals[0] - finals[1]).abs().max().item(), "nbuckets": nb}
+
+
 def _broadcast_init_check():
     import torch.distributed as dist
     from databricks_distributed_deep_learning_amd.parallel import DataParallel
@@ -286,3 +321,9 @@ def test_zero1_checkpoint_save_and_resume_world2(tmp_path):
     assert out["err"] == 0.0, out
     assert out["resumed_step"] == 2, out
     assert out["loss2"] == out["loss2"], out
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adamw", "lamb"])
+def test_optimizer_overlapped_with_bucket_allreduce(opt_name):
+    out = Distributor(num_processes=2, use_gpu=False).run(_overlap_equivalence, opt_name)
+    assert out["nbuckets"] > 1 and out["err"] < 1e-6, out
