@@ -136,11 +136,12 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
     return 0.5f * (1.f + erf_v) + x * (0.3989422804014327f * e);
 }
 
-// Counter-based hash RNG: uniform 32-bit value from (seed, index) so dropout
-// masks are regenerated in backward, never stored.  Two rounds of the
-// "lowbias32" integer finaliser (xor-shift / 32-bit multiply): ~12 VALU ops per
-// element, cheap enough to recompute inside bandwidth-bound kernels (LayerNorm
-// backward) where a 64-bit-multiply hash was VALU-bound.
+// Counter-based dropout RNG: masks are regenerated in backward, never stored.  ONE
+// "lowbias32" integer-finaliser round (xor-shift / 32-bit multiply) per PAIR of
+// consecutive element indices (idx >> 1), each element thresholded on its 16-bit half
+// (the low half for even idx): P(keep) = 1 - thresh16 / 65536.  About 4 VALU ops per
+// element -- cheap enough inside bandwidth-bound LayerNorm / attention passes, where a
+// two-round hash per element was VALU-bound.
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -149,12 +150,26 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16;
     return x;
 }
-__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-    const uint32_t a = lowbias32((uint32_t)idx ^ (uint32_t)seed);
-    return lowbias32(a + (uint32_t)(idx >> 32) * 0x9E3779B9u + (uint32_t)(seed >> 32));
+__device__ __forceinline__ uint32_t pair_hash(uint64_t seed, uint64_t pidx) {
+    uint32_t x = (uint32_t)pidx ^ (uint32_t)seed;
+    x += (uint32_t)(pidx >> 32) * 0x9E3779B9u + (uint32_t)(seed >> 32);
+    return lowbias32(x);
 }
-__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
-    return hash_u32(seed, idx) >= thresh;   // P(keep) = 1 - thresh / 2^32
+__host__ __device__ __forceinline__ uint32_t drop_thresh16(float p) {
+    const float t = p * 65536.f;
+    return t >= 65536.f ? 65536u : (t <= 0.f ? 0u : (uint32_t)t);
+}
+__device__ __forceinline__ bool keep_half(uint32_t h, uint64_t idx, uint32_t thresh16) {
+    return ((h >> ((uint32_t)(idx & 1) * 16)) & 0xffffu) >= thresh16;
+}
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh16) {
+    return keep_half(pair_hash(seed, idx >> 1), idx, thresh16);
+}
+// keep bits of elements i0 .. i0+3, i0 even (bit j = element i0 + j): two hashes
+__device__ __forceinline__ uint32_t keep_bits4(uint64_t seed, uint64_t i0, uint32_t thresh16) {
+    const uint32_t h0 = pair_hash(seed, i0 >> 1), h1 = pair_hash(seed, (i0 >> 1) + 1);
+    return (uint32_t)((h0 & 0xffffu) >= thresh16) | ((uint32_t)((h0 >> 16) >= thresh16) << 1) |
+           ((uint32_t)((h1 & 0xffffu) >= thresh16) << 2) | ((uint32_t)((h1 >> 16) >= thresh16) << 3);
 }
 
 // BatchNorm-backward GEMM epilogue (ACT_BNB) side arguments: the BN's ReLU bit mask

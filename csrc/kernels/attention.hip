@@ -17,9 +17,11 @@
 // Backward: dKV kernel (one workgroup per 64 keys, loops over queries) and dQ
 // kernel (one workgroup per 64 queries, loops over keys): every sum stays on
 // chip, no atomics; P is recomputed from the saved log-sum-exp.
-// Dropout on the attention probabilities uses the counter hash of ddl_common.h
-// keyed by ((b*H+h)*S + q)*S + k, regenerated in backward.
+// Dropout on the attention probabilities: one lowbias32 hash per pair of score
+// indices ((b*H+h)*S + q)*S + k (attn_hash below), regenerated in backward.
 #include "ddl_common.h"
+
+#include <cstdlib>
 
 namespace {
 
@@ -99,9 +101,38 @@ struct Stager {
     }
 };
 
-__device__ __forceinline__ uint32_t drop_thresh(float p) {
-    const double t = (double)p * 4294967296.0;
-    return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+// Probability dropout: the pair hash of ddl_common.h over the score index
+// idx = ((b*H + h)*S + q)*S + k, the same decision in the forward and in both
+// backward kernels.
+__device__ __forceinline__ uint32_t attn_hash(uint64_t seed, uint64_t pidx) { return pair_hash(seed, pidx); }
+__device__ __forceinline__ bool attn_keep_half(uint32_t h, uint64_t idx, uint32_t thresh16) {
+    return keep_half(h, idx, thresh16);
+}
+// the 4 consecutive score indices i0 .. i0+3 (one lane's keys 4g..4g+3 of a 16-key block)
+__device__ __forceinline__ void attn_keep4(uint64_t seed, uint64_t i0, uint32_t thresh16, bool odd_rows,
+                                          bool (&keep)[4]) {
+    const uint64_t p0 = i0 >> 1;
+    const uint32_t h0 = attn_hash(seed, p0), h1 = attn_hash(seed, p0 + 1);
+    const uint32_t h2 = odd_rows ? attn_hash(seed, p0 + 2) : 0u;   // i0 odd only when S is odd
+    const int o = (int)(i0 & 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int e = o + r;
+        const uint32_t h = (e >> 1) == 0 ? h0 : ((e >> 1) == 1 ? h1 : h2);
+        keep[r] = ((h >> ((e & 1) * 16)) & 0xffffu) >= thresh16;
+    }
+}
+
+// additive key mask of keys k0 + {0..3} (k0 = a lane's first key of a 16-key block),
+// one 16-byte load when the whole group is in range and aligned
+__device__ __forceinline__ void mask4(const float* mrow, int k0, int S, float (&m)[4]) {
+    if (k0 + 3 < S && ((S | k0) & 3) == 0) {
+        const float4 v = *reinterpret_cast<const float4*>(mrow + k0);
+        m[0] = v.x; m[1] = v.y; m[2] = v.z; m[3] = v.w;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m[r] = k0 + r < S ? mrow[k0 + r] : 0.f;
+    }
 }
 
 __device__ __forceinline__ bf16x8 load_frag_global(const bf16_t* rowp, int kk) {
@@ -135,8 +166,10 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
     f32x4 o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const uint32_t thresh = drop_thresh(p_drop);
+    const uint32_t thresh = drop_thresh16(p_drop);
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;     // score index of (myq, key 0)
+    const float* mrow = mask ? mask + (long)b * S : nullptr;
 
     const int nt = (S + TK - 1) / TK;
     Stager sk, sv;
@@ -165,17 +198,21 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
         }
         // ---- scale, mask, online softmax (log2 domain)
         float tmax = -INFINITY;
+        const bool tail = (t + 1) * TK > S;          // uniform: keys past S in this tile
 #pragma unroll
-        for (int blk = 0; blk < 4; ++blk)
+        for (int blk = 0; blk < 4; ++blk) {
+            const int k0 = t * TK + 16 * blk + 4 * g;
+            float mk[4] = {0.f, 0.f, 0.f, 0.f};
+            if (mrow) mask4(mrow, k0, S, mk);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int key = t * TK + 16 * blk + 4 * g + r;
                 float v = s[blk][r] * c2;
-                if (mask) v += (key < S ? mask[(long)b * S + key] : 0.f) * LOG2E;
-                if (key >= S) v = -INFINITY;
+                if (mrow) v += mk[r] * LOG2E;
+                if (tail && k0 + r >= S) v = -INFINITY;
                 s[blk][r] = v;
                 tmax = fmaxf(tmax, v);
             }
+        }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float mnew = fmaxf(m, tmax);
@@ -184,18 +221,17 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
         m = mnew;
         float psum = 0.f;
 #pragma unroll
-        for (int blk = 0; blk < 4; ++blk)
+        for (int blk = 0; blk < 4; ++blk) {
+            bool keep[4] = {true, true, true, true};
+            if (p_drop > 0.f) attn_keep4(seed, rowidx + t * TK + 16 * blk + 4 * g, thresh, S & 1, keep);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float pv = exp2f(s[blk][r] - msub);
                 psum += pv;
-                if (p_drop > 0.f) {
-                    const int key = t * TK + 16 * blk + 4 * g + r;
-                    const uint64_t idx = ((uint64_t)bh * S + myq) * S + key;
-                    pv = keep_elem(seed, idx, thresh) ? pv * inv_keep : 0.f;
-                }
+                if (p_drop > 0.f) pv = keep[r] ? pv * inv_keep : 0.f;
                 s[blk][r] = pv;
             }
+        }
         lsum = lsum * alpha + psum;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] *= alpha;
@@ -282,7 +318,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
     }
     const float mbias = (mask && kok) ? mask[(long)b * S + myk] : 0.f;
     const float c2 = scale * LOG2E;
-    const uint32_t thresh = drop_thresh(p_drop);
+    const uint32_t thresh = drop_thresh16(p_drop);
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     f32x4 dv[4], dk[4];
 #pragma unroll
@@ -326,8 +362,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
                 float dpv = dp[qbk][r];
                 float pdrop = pv;
                 if (p_drop > 0.f) {
+                    // lane = key, elements along queries: consecutive elements are S indices
+                    // apart, so each needs its own pair hash
                     const uint64_t idx = ((uint64_t)bh * S + q) * S + myk;
-                    const bool keep = keep_elem(seed, idx, thresh);
+                    const bool keep = attn_keep_half(attn_hash(seed, idx >> 1), idx, thresh);
                     pdrop = keep ? pv * inv_keep : 0.f;
                     dpv = keep ? dpv * inv_keep : 0.f;
                 }
@@ -384,8 +422,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
     const float my_lse = qok ? lse[(long)bh * S + myq] : 0.f;
     const float my_delta = qok ? delta[(long)bh * S + myq] : 0.f;
     const float c2 = scale * LOG2E;
-    const uint32_t thresh = drop_thresh(p_drop);
+    const uint32_t thresh = drop_thresh16(p_drop);
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;
+    const float* mrow = mask ? mask + (long)b * S : nullptr;
     f32x4 dq[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
@@ -413,21 +453,23 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
             }
         }
         f32x4 ds[4];
+        const float lse2 = my_lse * LOG2E;
 #pragma unroll
-        for (int blk = 0; blk < 4; ++blk)
+        for (int blk = 0; blk < 4; ++blk) {
+            const int k0 = t * TK + 16 * blk + 4 * g;
+            float mk[4] = {0.f, 0.f, 0.f, 0.f};
+            if (mrow) mask4(mrow, k0, S, mk);
+            bool keep[4] = {true, true, true, true};
+            if (p_drop > 0.f) attn_keep4(seed, rowidx + k0, thresh, S & 1, keep);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int key = t * TK + 16 * blk + 4 * g + r;
-                const bool ok = qok && key < S;
-                const float mb = (mask && key < S) ? mask[(long)b * S + key] : 0.f;
-                const float pv = ok ? exp2f(sc[blk][r] * c2 + mb * LOG2E - my_lse * LOG2E) : 0.f;
+                const bool ok = qok && k0 + r < S;
+                const float pv = ok ? exp2f(sc[blk][r] * c2 + mk[r] * LOG2E - lse2) : 0.f;
                 float dpv = dp[blk][r];
-                if (p_drop > 0.f) {
-                    const uint64_t idx = ((uint64_t)bh * S + myq) * S + key;
-                    dpv = keep_elem(seed, idx, thresh) ? dpv * inv_keep : 0.f;
-                }
+                if (p_drop > 0.f) dpv = keep[r] ? dpv * inv_keep : 0.f;
                 ds[blk][r] = pv * (dpv - my_delta);
             }
+        }
         // dQ^T[d][q] += K^T[d][k] dS^T[k][q]
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -446,6 +488,213 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
     }
 }
 
+
+// ============================================================ fused backward, S <= 128
+// One workgroup (8 waves) per (b, h) holds the whole sequence: Q, K and dO are staged
+// into LDS once, delta = rowsum(dO * O) is computed in the prologue, and
+//   phase 1 (lane = key, wave w owns keys 16w..16w+15): S, dP over all 128 queries in
+//           chunks of 32, P (saved LSE), dropout, dS -> dV, dK complete in registers; the
+//           lane's dS column stays in registers (bf16) until every wave is done with Q and
+//           dO, then goes to LDS as two [128 keys][64 queries] dS^T row images over them
+//           (48 KB of LDS: two workgroups per CU);
+//   phase 2 (lane = query, wave w owns queries 16w..16w+15): dQ = dS K from the dS^T
+//           images and K, both read transposed.
+// Every input byte is read once and nothing is recomputed (the two-kernel path re-derives
+// P and dP in both its dK/dV and its dQ kernel and reads Q/K/V/dO once per tile pair).
+constexpr int FS = 128;
+__global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restrict__ qkv,
+                                                            const bf16_t* __restrict__ out,
+                                                            const bf16_t* __restrict__ dout,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
+                                                            int S, int H, float scale, float p_drop, uint64_t seed) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * FS * ROWB];   // Q, K, dO; then dS^T halves over Q, dO
+    __shared__ float s_lse[FS], s_delta[FS], s_mask[FS];
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const long rs = 3L * H * D;
+    const long ors = (long)H * D;
+    const bf16_t* qb = qkv + (long)b * S * rs + h * D;
+    const bf16_t* kb = qb + H * D;
+    const bf16_t* vb = qb + 2 * H * D;
+    const bf16_t* dob = dout + (long)b * S * ors + h * D;
+    const bf16_t* ob = out + (long)b * S * ors + h * D;
+    char* sQ = smem;
+    char* sK = sQ + FS * ROWB;
+    char* sO = sK + FS * ROWB;
+    char* sT0 = sQ;                 // dS^T[:, 0:64]   (after phase 1)
+    char* sT1 = sO;                 // dS^T[:, 64:128] (after phase 1)
+    uint2 dsk[8];                   // this lane's dS column, bf16, blocks of 4 queries (qc, j)
+
+    // ---- prologue: Q, K, dO row images (rows >= S are zeros), delta, scaled LSE, mask
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = (tid >> 3) + 64 * i, c = tid & 7;
+        const bool ok = r < S;
+        const int rr = ok ? r : 0;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 q4 = *reinterpret_cast<const uint4*>(qb + (long)rr * rs + c * 8);
+        const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
+        const uint4 o4 = *reinterpret_cast<const uint4*>(dob + (long)rr * ors + c * 8);
+        *reinterpret_cast<uint4*>(sQ + lds_off<false>(r, c)) = ok ? q4 : z;
+        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = ok ? k4 : z;
+        *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = ok ? o4 : z;
+    }
+    {
+        // delta[q] = sum_d dO[q][d] O[q][d]: 4 threads per query, 16 d each
+        const int q = tid >> 2, part = tid & 3;
+        float a = 0.f;
+        if (q < S) {
+            float x[8], y[8];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                load8(dob + (long)q * ors + part * 16 + hh * 8, x);
+                load8(ob + (long)q * ors + part * 16 + hh * 8, y);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a += x[j] * y[j];
+            }
+        }
+        a += __shfl_xor(a, 1);
+        a += __shfl_xor(a, 2);
+        if (part == 0) s_delta[q] = a;
+    }
+    if (tid < FS) {
+        s_lse[tid] = tid < S ? lse[(long)bh * S + tid] * LOG2E : 0.f;
+        s_mask[tid] = (mask && tid < S) ? mask[(long)b * S + tid] * LOG2E : 0.f;
+    }
+    __syncthreads();
+
+    const float c2 = scale * LOG2E;
+    const uint32_t thresh = drop_thresh16(p_drop);
+    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+
+    // ---- phase 1: lane = key
+    {
+        const int myk = 16 * w + (lane & 15);
+        const bool kok = myk < S;
+        bf16x8 kf[2], vf[2];
+        const bf16_t* vr = vb + (long)(kok ? myk : 0) * rs;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            kf[kk] = frag_rows<false>(sK, 16 * w, kk);   // B operand: my key's row, d = 32kk + 8g ..
+            vf[kk] = load_frag_global(vr, kk);
+        }
+        const float mb2 = s_mask[kok ? myk : 0];
+        f32x4 dv[4], dk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
+        const int nqc = (S + 31) / 32;
+        for (int qc = 0; qc < nqc; ++qc) {
+            f32x4 sc[2], dp[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                sc[j] = (f32x4){0, 0, 0, 0};
+                dp[j] = (f32x4){0, 0, 0, 0};
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+                    sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sQ, 32 * qc + 16 * j, kk), kf[kk],
+                                                                    sc[j], 0, 0, 0);
+                    dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sO, 32 * qc + 16 * j, kk), vf[kk],
+                                                                    dp[j], 0, 0, 0);
+                }
+            }
+            f32x4 pd[2], ds[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int ql = 32 * qc + 16 * j + 4 * g + r;
+                    const float pv = (ql < S && kok) ? exp2f(sc[j][r] * c2 + mb2 - s_lse[ql]) : 0.f;
+                    float dpv = dp[j][r];
+                    float pdrop = pv;
+                    if (p_drop > 0.f) {
+                        const uint64_t idx = ((uint64_t)bh * S + ql) * S + myk;
+                        const bool keep = attn_keep_half(attn_hash(seed, idx >> 1), idx, thresh);
+                        pdrop = keep ? pv * inv_keep : 0.f;
+                        dpv = keep ? dpv * inv_keep : 0.f;
+                    }
+                    pd[j][r] = pdrop;
+                    ds[j][r] = pv * (dpv - s_delta[ql]);
+                }
+                // dS^T row myk, query columns 32qc + 16j + 4g .. +3 (written after phase 1)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (c == qc) dsk[2 * c + j] = make_uint2(pack2bf(ds[j][0], ds[j][1]), pack2bf(ds[j][2], ds[j][3]));
+            }
+            // dV^T[d][k] += dO^T[d][q] Pd[q][k];  dK^T[d][k] += Q^T[d][q] dS[q][k]
+            const bf16x8 pf = pack_acc(pd[0], pd[1]);
+            const bf16x8 sf = pack_acc(ds[0], ds[1]);
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sO, 32 * qc, 16 * db), pf, dv[db], 0, 0, 0);
+                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sQ, 32 * qc, 16 * db), sf, dk[db], 0, 0, 0);
+            }
+        }
+        // query chunks past S: their dS^T columns read as zeros in phase 2
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (c >= nqc) dsk[2 * c] = dsk[2 * c + 1] = make_uint2(0u, 0u);
+        if (kok) {
+            bf16_t* dkr = dqkv + ((long)b * S + myk) * rs + H * D + h * D;
+            bf16_t* dvr = dkr + H * D;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                float a4[4] = {dk[db][0] * scale, dk[db][1] * scale, dk[db][2] * scale, dk[db][3] * scale};
+                float b4[4] = {dv[db][0], dv[db][1], dv[db][2], dv[db][3]};
+                store4(dkr + 16 * db + 4 * g, a4);
+                store4(dvr + 16 * db + 4 * g, b4);
+            }
+        }
+    }
+    __syncthreads();               // every wave is done with the Q and dO images
+    {
+        const int myk = 16 * w + (lane & 15);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int q0 = 16 * c + 4 * g;             // block c = (qc, j) = (c / 2, c % 2)
+            char* img = q0 < 64 ? sT0 : sT1;
+            const int qq = q0 & 63;
+            *reinterpret_cast<uint2*>(img + lds_off<false>(myk, qq >> 3) + (qq & 7) * 2) = dsk[c];
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 2: lane = query; dQ^T[d][q] = K^T[d][k] dS^T[k][q] over all keys
+    {
+        const int myq = 16 * w + (lane & 15);
+        const char* img = w < 4 ? sT0 : sT1;
+        const int cb = (16 * w) & 63;
+        f32x4 dq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
+        const int nkc = (S + 31) / 32;
+        for (int st = 0; st < nkc; ++st) {
+            const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
+        }
+        if (myq < S) {
+            bf16_t* dqr = dqkv + ((long)b * S + myq) * rs + h * D;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                float a4[4] = {dq[db][0] * scale, dq[db][1] * scale, dq[db][2] * scale, dq[db][3] * scale};
+                store4(dqr + 16 * db + 4 * g, a4);
+            }
+        }
+    }
+}
+}  // namespace
+
+namespace {
+// DDL_ATTN_FUSED_BWD=0: the two-kernel backward for every S (A/B timing, tests)
+bool fused_bwd_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_ATTN_FUSED_BWD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 }  // namespace
 
 // qkv [B, S, 3*H*64] bf16; mask: additive key bias [B, S] fp32 or null; out [B, S, H*64]; lse [B, H, S] fp32
@@ -460,6 +709,11 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
 DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, const float* mask,
                          float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop, uint64_t seed,
                          hipStream_t st) {
+    if (S <= FS && fused_bwd_enabled()) {   // the whole sequence fits one workgroup's LDS
+        attn_bwd_fused_k<<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, (const bf16_t*)dout, lse,
+                                                mask, (bf16_t*)dqkv, S, H, scale, p_drop, seed);
+        DDL_RETURN_LAUNCH();
+    }
     const long rows = (long)B * S * H;
     attn_delta_k<<<(int)((rows * 8 + 255) / 256), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
     dim3 grid((S + TK - 1) / TK, B * H);

@@ -35,15 +35,16 @@ __global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ dy, cons
 }
 
 // ------------------------------------------------------------------ dropout
-// keep iff hash(seed, idx) >= thresh; mask regenerated in backward.
+// keep bits from the pair hash of ddl_common.h (16-bit threshold); regenerated in backward.
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_k(const T* __restrict__ x, T* __restrict__ y, long n8, uint64_t seed,
                                                  uint32_t thresh, float scale) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
         float v[8];
         load8(x + i * 8, v);
+        const uint32_t kb = keep_bits4(seed, (uint64_t)i * 8, thresh) | (keep_bits4(seed, (uint64_t)i * 8 + 4, thresh) << 4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = keep_elem(seed, (uint64_t)(i * 8 + j), thresh) ? v[j] * scale : 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = ((kb >> j) & 1u) ? v[j] * scale : 0.f;
         store8(y + i * 8, v);
     }
 }
@@ -389,7 +390,7 @@ DDL_API int ddl_gelu_bwd(int dtype, const void* dy, const void* x, void* dx, lon
 DDL_API int ddl_dropout(int dtype, const void* x, void* y, long n, uint64_t seed, float p, hipStream_t st) {
     if (n % 8) return -1;
     const long n8 = n / 8;
-    const uint32_t thresh = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+    const uint32_t thresh = drop_thresh16(p);
     const float scale = 1.f / (1.f - p);
     DISPATCH_T(dtype,
                (dropout_k<bf16_t><<<grid_for(n8), 256, 0, st>>>((const bf16_t*)x, (bf16_t*)y, n8, seed, thresh, scale)),

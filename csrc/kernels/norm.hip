@@ -359,14 +359,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_k(const T* __restrict__
 // (and the column sums of the latter: the producing Linear's bias gradient).
 struct Drop {
     uint64_t seed;
-    uint32_t thresh;   // 0: no dropout
+    uint32_t thresh;   // 16-bit threshold (ddl_common.h keep_bits4); 0: no dropout
     float scale;       // 1 / (1 - p)
     void* dres;        // backward: residual gradient (unmasked), only with dropout
 };
-__device__ __forceinline__ void drop4(const Drop& d, long idx, float* v) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = keep_elem(d.seed, (uint64_t)(idx + j), d.thresh) ? v[j] * d.scale : 0.f;
+// idx % 4 == 0 (H % 4 == 0, 4 columns per lane): two pair hashes per 4 elements
+__device__ __forceinline__ uint32_t drop_bits4(const Drop& d, long idx) {
+    return keep_bits4(d.seed, (uint64_t)idx, d.thresh);
 }
+__device__ __forceinline__ void apply4(const Drop& d, uint32_t bits, float* v) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ((bits >> j) & 1u) ? v[j] * d.scale : 0.f;
+}
+__device__ __forceinline__ void drop4(const Drop& d, long idx, float* v) { apply4(d, drop_bits4(d, idx), v); }
 
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T* __restrict__ res, long res_rows,
@@ -432,29 +437,31 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
     }
     const long r0 = (long)blockIdx.x * rows_per_blk;
     const long r1 = min(rows, r0 + rows_per_blk);
-    // raw loads of one row: input (x, plus residual) and dy
-    auto load_row = [&](long row, float (&xv)[VPL][4], float (&d)[VPL][4]) {
+    // raw loads of one row: input (x, plus residual) and dy; with dropout, the row's keep
+    // bits (4 per lane and column group) are generated once and reused for dx
+    auto load_row = [&](long row, float (&xv)[VPL][4], float (&d)[VPL][4], uint32_t (&kb)[VPL]) {
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
             const int col = 256 * k + 4 * lane;
             load4(x + row * H + col, xv[k]);
             load4(dy + row * H + col, d[k]);
+            kb[k] = drop.thresh ? drop_bits4(drop, row * H + col) : 0xfu;
         }
         if (res) {
 #pragma unroll
             for (int k = 0; k < VPL; ++k) {
                 float r[4];
                 load4(res + (row % res_rows) * H + 256 * k + 4 * lane, r);
-                if (drop.thresh) drop4(drop, row * H + 256 * k + 4 * lane, xv[k]);
+                if (drop.thresh) apply4(drop, kb[k], xv[k]);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) xv[k][j] += r[j];
             }
         } else if (drop.thresh) {
 #pragma unroll
-            for (int k = 0; k < VPL; ++k) drop4(drop, row * H + 256 * k + 4 * lane, xv[k]);
+            for (int k = 0; k < VPL; ++k) apply4(drop, kb[k], xv[k]);
         }
     };
-    auto finish_row = [&](long row, const float (&xv)[VPL][4], const float (&d)[VPL][4]) {
+    auto finish_row = [&](long row, const float (&xv)[VPL][4], const float (&d)[VPL][4], const uint32_t (&kb)[VPL]) {
         const float mu = mean[row], rs = rstd[row];
         float xh[VPL][4], gy[VPL][4];
         float s1 = 0.f, s2 = 0.f;
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             for (int j = 0; j < 4; ++j) o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
             if (drop.thresh) {
                 store4((T*)drop.dres + idx, o);      // residual gradient: unmasked
-                drop4(drop, idx, o);                 // x gradient: through the dropout mask
+                apply4(drop, kb[k], o);              // x gradient: through the dropout mask
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) ds[k][j] += to_f(from_f<T>(o[j]));   // sum of the stored (rounded) dx
@@ -490,10 +497,11 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
     for (long row = r0 + w; row < r1; row += 8) {
         const bool two = row + 4 < r1;   // wave-uniform
         float xa[VPL][4], da[VPL][4], xb[VPL][4], dbv[VPL][4];
-        load_row(row, xa, da);
-        if (two) load_row(row + 4, xb, dbv);
-        finish_row(row, xa, da);
-        if (two) finish_row(row + 4, xb, dbv);
+        uint32_t ka[VPL], kbb[VPL];
+        load_row(row, xa, da, ka);
+        if (two) load_row(row + 4, xb, dbv, kbb);
+        finish_row(row, xa, da, ka);
+        if (two) finish_row(row + 4, xb, dbv, kbb);
     }
 #pragma unroll
     for (int k = 0; k < VPL; ++k)
@@ -759,7 +767,7 @@ static Drop make_drop(unsigned long long seed, float p, void* dres) {
     Drop d{};
     if (p > 0.f) {
         d.seed = seed;
-        d.thresh = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+        d.thresh = drop_thresh16(p);
         d.scale = 1.f / (1.f - p);
         d.dres = dres;
     }

@@ -26,6 +26,17 @@ def hash_u32(seed, idx):
     return _lowbias32((a + ((idx >> 32) * 0x9E3779B9 & M32) + (seed >> 32)) & M32)
 
 
+def attn_keep(seed, idx, p):
+    """attention.hip attn_hash / attn_keep_half: one lowbias32 round per pair of score
+    indices (idx >> 1), each element thresholded on its 16-bit half."""
+    pidx = idx >> 1
+    x = (pidx & M32) ^ (seed & M32)
+    x = (x + ((pidx >> 32) * 0x9E3779B9 & M32) + (seed >> 32)) & M32
+    h = _lowbias32(x)
+    half = (h >> ((idx & 1) * 16)) & 0xFFFF
+    return half >= min(int(p * 65536.0), 65536)
+
+
 def ref_attention(qkv, H, mask=None, keep=None, p=0.0):
     B, S, hd3 = qkv.shape
     D = hd3 // (3 * H)
@@ -62,22 +73,22 @@ def test_attention_fwd_bwd(B, S, H, masked):
     assert gerr < 3e-2 * q32.grad.abs().max().item() + 1e-2, gerr
 
 
-def test_attention_dropout_mask_parity():
+@pytest.mark.parametrize("S", [96, 97])          # odd S: pairs of score indices straddle rows
+def test_attention_dropout_mask_parity(S):
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd.ops import _native_attention as NA
     torch.manual_seed(1)
-    B, S, H, p = 2, 96, 3, 0.25
+    B, H, p = 2, 3, 0.25
     qkv = torch.randn(B, S, 3 * H * 64, device=dev).to(torch.bfloat16).requires_grad_(True)
     torch.manual_seed(123)
     out = NA.attention(qkv, H, None, p)
     torch.manual_seed(123)
     seed = NA.new_seed()
-    thresh = min(int(p * 2 ** 32), 2 ** 32 - 1)
     bh = torch.arange(B * H, device=dev).view(B, H, 1, 1)
     qi = torch.arange(S, device=dev).view(1, 1, S, 1)
     ki = torch.arange(S, device=dev).view(1, 1, 1, S)
     idx = (bh * S + qi) * S + ki
-    keep = (hash_u32(seed, idx) >= thresh).float()
+    keep = attn_keep(seed, idx, p).float()
     assert abs(keep.mean().item() - (1 - p)) < 0.02
     q32 = qkv.detach().float().requires_grad_(True)
     ref = ref_attention(q32, H, None, keep, p)

@@ -66,7 +66,8 @@ def test_batchnorm_train(dtype, relu, res, C, big):
 
 
 def _hash_keep(seed: int, n: int, p: float):
-    """Python replica of the kernels' counter hash (ddl_common.h hash_u32): keep mask."""
+    """Python replica of the kernels' dropout RNG (ddl_common.h pair_hash / keep_half):
+    one lowbias32 round per pair of element indices, 16 bits per element."""
     import numpy as np
 
     def lowbias32(x):
@@ -77,12 +78,14 @@ def _hash_keep(seed: int, n: int, p: float):
         return x ^ (x >> np.uint32(16))
     with np.errstate(over="ignore"):
         idx = np.arange(n, dtype=np.uint64)
-        lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-        hi = (idx >> np.uint64(32)).astype(np.uint32)
-        a = lowbias32(lo ^ np.uint32(seed & 0xFFFFFFFF))
-        h = lowbias32(a + hi * np.uint32(0x9E3779B9) + np.uint32(seed >> 32)).astype(np.float64)
-    thresh = min(4294967295.0, float(int(p * 4294967296.0)))
-    return torch.from_numpy(h >= thresh)
+        pidx = idx >> np.uint64(1)
+        lo = (pidx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (pidx >> np.uint64(32)).astype(np.uint32)
+        x = (lo ^ np.uint32(seed & 0xFFFFFFFF)) + hi * np.uint32(0x9E3779B9) + np.uint32(seed >> 32)
+        h = lowbias32(x)
+        half = (h >> ((idx & np.uint64(1)).astype(np.uint32) * np.uint32(16))) & np.uint32(0xFFFF)
+    thresh = min(65536, int(p * 65536.0))
+    return torch.from_numpy(half.astype(np.int64) >= thresh)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
