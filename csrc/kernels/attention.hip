@@ -29,9 +29,14 @@ constexpr int D = 64;          // head dim
 constexpr int TQ = 64;         // queries per workgroup
 constexpr int TK = 64;         // keys per tile
 constexpr int ROWB = 128;      // bytes per LDS row (64 bf16)
+constexpr int FS = 128;        // longest sequence of the one-workgroup-per-(b, h) kernels
 constexpr float LOG2E = 1.4426950408889634f;
 
 typedef __attribute__((address_space(3))) s16x4 lds_v4;
+
+// 2^x as the bare v_exp_f32: exp2f adds a denormal-range fix-up (ldexp, compare, select)
+// per call; softmax arguments are <= 0 and a result below 2^-126 may as well be 0
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // Row image swizzle (128-B rows; ds_read_b128 fragment reads conflict free).
 __device__ __forceinline__ int swz_row(int r, int c) { return c ^ ((r >> 1) & 7); }
@@ -216,7 +221,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float mnew = fmaxf(m, tmax);
-        const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mnew);
+        const float alpha = (m == -INFINITY) ? 0.f : fast_exp2(m - mnew);
         const float msub = mnew == -INFINITY ? 0.f : mnew;
         m = mnew;
         float psum = 0.f;
@@ -226,7 +231,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
             if (p_drop > 0.f) attn_keep4(seed, rowidx + t * TK + 16 * blk + 4 * g, thresh, S & 1, keep);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float pv = exp2f(s[blk][r] - msub);
+                float pv = fast_exp2(s[blk][r] - msub);
                 psum += pv;
                 if (p_drop > 0.f) pv = keep[r] ? pv * inv_keep : 0.f;
                 s[blk][r] = pv;
@@ -358,7 +363,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
             for (int r = 0; r < 4; ++r) {
                 const int ql = 16 * qbk + 4 * g + r;
                 const int q = t * TQ + ql;
-                float pv = (q < S && kok) ? exp2f(sc[qbk][r] * c2 + mbias * LOG2E - s_lse[ql] * LOG2E) : 0.f;
+                float pv = (q < S && kok) ? fast_exp2(sc[qbk][r] * c2 + mbias * LOG2E - s_lse[ql] * LOG2E) : 0.f;
                 float dpv = dp[qbk][r];
                 float pdrop = pv;
                 if (p_drop > 0.f) {
@@ -464,7 +469,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const bool ok = qok && k0 + r < S;
-                const float pv = ok ? exp2f(sc[blk][r] * c2 + mk[r] * LOG2E - lse2) : 0.f;
+                const float pv = ok ? fast_exp2(sc[blk][r] * c2 + mk[r] * LOG2E - lse2) : 0.f;
                 float dpv = dp[blk][r];
                 if (p_drop > 0.f) dpv = keep[r] ? dpv * inv_keep : 0.f;
                 ds[blk][r] = pv * (dpv - my_delta);
@@ -489,6 +494,114 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
 }
 
 
+// ============================================================ forward, S <= 128
+// One workgroup (8 waves) per (b, h): K and V of the whole sequence staged into LDS once
+// (the tiled forward stages them once per 64-query workgroup), wave w owns queries
+// 16w..16w+15 with every key's score in registers, so the softmax needs no online
+// rescaling: one max, one exponential per score, one sum.
+__global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restrict__ qkv,
+                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
+                                                            float* __restrict__ lse, int S, int H, float scale,
+                                                            float p_drop, uint64_t seed) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * FS * ROWB];   // K (row image), V (transposed-read image)
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const long rs = 3L * H * D;
+    const bf16_t* qb = qkv + (long)b * S * rs + h * D;
+    const bf16_t* kb = qb + H * D;
+    const bf16_t* vb = qb + 2 * H * D;
+    char* sK = smem;
+    char* sV = smem + FS * ROWB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = (tid >> 3) + 64 * i, c = tid & 7;
+        const bool ok = r < S;
+        const int rr = ok ? r : 0;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
+        const uint4 v4 = *reinterpret_cast<const uint4*>(vb + (long)rr * rs + c * 8);
+        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = ok ? k4 : z;
+        *reinterpret_cast<uint4*>(sV + lds_off<true>(r, c)) = ok ? v4 : z;
+    }
+    const int myq = 16 * w + (lane & 15);
+    const bool qok = myq < S;
+    bf16x8 qf[2];
+    {
+        const bf16_t* qr = qb + (long)(qok ? myq : 0) * rs;
+        qf[0] = load_frag_global(qr, 0);
+        qf[1] = load_frag_global(qr, 1);
+    }
+    const float c2 = scale * LOG2E;
+    const float* mrow = mask ? mask + (long)b * S : nullptr;
+    __syncthreads();
+    const int nblk = (S + 15) / 16;
+    // S^T blocks: lane holds s[blk][r] = score(q = myq, k = 16 blk + 4 g + r)
+    f32x4 s[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int blk = 0; blk < 8; ++blk) {
+        s[blk] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (blk < nblk) {
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                s[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sK, 16 * blk, kk), qf[kk], s[blk], 0, 0, 0);
+        }
+        const int k0 = 16 * blk + 4 * g;
+        float mk[4] = {0.f, 0.f, 0.f, 0.f};
+        if (mrow && blk < nblk) mask4(mrow, k0, S, mk);
+        const bool edge = 16 * blk + 16 > S;          // uniform: this block reaches past S
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = mrow ? s[blk][r] * c2 + mk[r] * LOG2E : s[blk][r] * c2;
+            if (edge && k0 + r >= S) v = -INFINITY;
+            s[blk][r] = v;
+            mx = fmaxf(mx, v);
+        }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float msub = mx == -INFINITY ? 0.f : mx;
+    const uint32_t thresh = drop_thresh16(p_drop);
+    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;
+    float lsum = 0.f;
+#pragma unroll
+    for (int blk = 0; blk < 8; ++blk) {
+        bool keep[4] = {true, true, true, true};
+        if (p_drop > 0.f && blk < nblk) attn_keep4(seed, rowidx + 16 * blk + 4 * g, thresh, S & 1, keep);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float pv = fast_exp2(s[blk][r] - msub);
+            lsum += pv;
+            if (p_drop > 0.f) pv = keep[r] ? pv * inv_keep : 0.f;
+            s[blk][r] = pv;
+        }
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    // O^T[d][q] = V^T[d][k] P^T[k][q]
+    f32x4 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+        if (2 * st >= nblk) break;
+        const bf16x8 pf = pack_acc(s[2 * st], s[2 * st + 1]);
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+            o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sV, 32 * st, 16 * db), pf, o[db], 0, 0, 0);
+    }
+    if (!qok) return;
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16_t* orow = out + ((long)b * S + myq) * H * D + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+        float v[4] = {o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv};
+        store4(orow + 16 * db + 4 * g, v);
+    }
+    if (g == 0) lse[(long)bh * S + myq] = (mx + log2f(lsum)) / LOG2E;
+}
+
 // ============================================================ fused backward, S <= 128
 // One workgroup (8 waves) per (b, h) holds the whole sequence: Q, K and dO are staged
 // into LDS once, delta = rowsum(dO * O) is computed in the prologue, and
@@ -501,7 +614,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
 //           images and K, both read transposed.
 // Every input byte is read once and nothing is recomputed (the two-kernel path re-derives
 // P and dP in both its dK/dV and its dQ kernel and reads Q/K/V/dO once per tile pair).
-constexpr int FS = 128;
 __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restrict__ qkv,
                                                             const bf16_t* __restrict__ out,
                                                             const bf16_t* __restrict__ dout,
@@ -509,7 +621,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                                                             const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
                                                             int S, int H, float scale, float p_drop, uint64_t seed) {
     __shared__ __attribute__((aligned(16))) char smem[3 * FS * ROWB];   // Q, K, dO; then dS^T halves over Q, dO
-    __shared__ float s_lse[FS], s_delta[FS], s_mask[FS];
+    __shared__ __attribute__((aligned(16))) float s_lse[FS];
+    __shared__ __attribute__((aligned(16))) float s_delta[FS];
+    __shared__ float s_mask[FS];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -580,6 +694,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
             vf[kk] = load_frag_global(vr, kk);
         }
         const float mb2 = s_mask[kok ? myk : 0];
+        const uint64_t rowk = (uint64_t)bh * S * S + myk;     // score index of (q = 0, myk)
         f32x4 dv[4], dk[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
@@ -601,20 +716,24 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
             f32x4 pd[2], ds[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
+                const int q0 = 32 * qc + 16 * j + 4 * g;
+                const f32x4 lse4 = *reinterpret_cast<const f32x4*>(s_lse + q0);     // one LDS read per 4 queries
+                const f32x4 del4 = *reinterpret_cast<const f32x4*>(s_delta + q0);
+                uint64_t idx = rowk + (uint64_t)q0 * S;                            // score index of (q0, myk)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int ql = 32 * qc + 16 * j + 4 * g + r;
-                    const float pv = (ql < S && kok) ? exp2f(sc[j][r] * c2 + mb2 - s_lse[ql]) : 0.f;
+                    const int ql = q0 + r;
+                    const float pv = (ql < S && kok) ? fast_exp2(sc[j][r] * c2 + (mb2 - lse4[r])) : 0.f;
                     float dpv = dp[j][r];
                     float pdrop = pv;
                     if (p_drop > 0.f) {
-                        const uint64_t idx = ((uint64_t)bh * S + ql) * S + myk;
                         const bool keep = attn_keep_half(attn_hash(seed, idx >> 1), idx, thresh);
                         pdrop = keep ? pv * inv_keep : 0.f;
                         dpv = keep ? dpv * inv_keep : 0.f;
                     }
+                    idx += S;
                     pd[j][r] = pdrop;
-                    ds[j][r] = pv * (dpv - s_delta[ql]);
+                    ds[j][r] = pv * (dpv - del4[r]);
                 }
                 // dS^T row myk, query columns 32qc + 16j + 4g .. +3 (written after phase 1)
 #pragma unroll
@@ -687,7 +806,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
 }  // namespace
 
 namespace {
-// DDL_ATTN_FUSED_BWD=0: the two-kernel backward for every S (A/B timing, tests)
+// DDL_ATTN_FUSED_BWD=0: the tiled forward and two-kernel backward for every S (A/B timing, tests)
 bool fused_bwd_enabled() {
     static const bool on = [] {
         const char* e = getenv("DDL_ATTN_FUSED_BWD");
@@ -700,6 +819,10 @@ bool fused_bwd_enabled() {
 // qkv [B, S, 3*H*64] bf16; mask: additive key bias [B, S] fp32 or null; out [B, S, H*64]; lse [B, H, S] fp32
 DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int S, int H, float scale,
                          float p_drop, uint64_t seed, hipStream_t st) {
+    if (S <= FS && fused_bwd_enabled()) {
+        attn_fwd_short_k<<<B * H, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed);
+        DDL_RETURN_LAUNCH();
+    }
     dim3 grid((S + TQ - 1) / TQ, B * H);
     attn_fwd_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed);
     DDL_RETURN_LAUNCH();

@@ -452,8 +452,9 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
 // Register epilogue of one 256x256 tile.  Lane layout: acc[qm][qn][i][j] holds
 // row m0 + qm*128 + wm*64 + i*16 + (lane & 15), columns n0 + qn*128 + wn*32 +
 // j*16 + 4*(lane >> 4) .. +3.
-//   EK_BF16: interior tile, bf16 out, optional bf16 bias / residual -- one 8-byte store a site
-//   EK_GELU: interior tile, bf16 out = GELU(acc + bf16 bias), pre-activation to aux
+//   EK_BF16: interior tile, bf16 out, optional bf16 bias / residual -- one 16-byte store per
+//            two sites (N, ldc % 8 == 0)
+//   EK_GELU: interior tile, bf16 out = GELU(acc + bf16 bias), pre-activation to aux (likewise)
 //   EK_DGELU: interior tile, bf16 out = acc * GELU'(aux) (+ column sums for the bias gradient)
 //   EK_F32 : interior tile, fp32 split-K partial or fp32 out (+accumulate) -- one 16-byte store
 //   EK_GEN : anything direct4 covers, with bounds checks (edge tiles)
@@ -554,6 +555,19 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         rb[qm][i] = *reinterpret_cast<const uint2*>(
                             pre + (long)(m0 + qm * 128 + wm * 64 + i * 16 + r16) * p.ldc + n);
             }
+            // EK_BF16 / EK_GELU store two sites (row blocks i, i + 1) per lane as ONE 16-byte
+            // store: v_permlane16_swap hands the odd lane rows (g = 1, 3) the even rows' quads
+            // of row block i + 1 in exchange for theirs of row block i, so each lane holds 8
+            // consecutive columns of one row (half the store instructions; 8-byte stores kept
+            // the epilogue store-issue bound).  Row-block i values wait in (plo, phi) / (zlo, zhi).
+            uint32_t plo = 0, phi = 0, zlo = 0, zhi = 0;
+            const int wcol = n0 + qn * 128 + wn * 32 + j * 16 + (lane >> 5) * 8;   // (g >> 1) * 8
+            auto store_pair = [&](void* base, uint32_t lo0, uint32_t hi0, uint32_t lo1, uint32_t hi1, int m1) {
+                const auto x = __builtin_amdgcn_permlane16_swap(lo0, lo1, false, false);
+                const auto y = __builtin_amdgcn_permlane16_swap(hi0, hi1, false, false);
+                const int mrow = (lane & 16) ? m1 : m1 - 16;      // g odd: row block i + 1
+                *reinterpret_cast<uint4*>((bf16_t*)base + (long)mrow * p.ldc + wcol) = make_uint4(x[0], y[0], x[1], y[1]);
+            };
 #pragma unroll
             for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -571,7 +585,8 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         }
                         const uint32_t lo = pack2bf(a[0] + bv[0] + rv[0], a[1] + bv[1] + rv[1]);
                         const uint32_t hi = pack2bf(a[2] + bv[2] + rv[2], a[3] + bv[3] + rv[3]);
-                        *reinterpret_cast<uint2*>((bf16_t*)p.C + (long)m * p.ldc + n) = make_uint2(lo, hi);
+                        if ((i & 1) == 0) { plo = lo; phi = hi; }
+                        else store_pair(p.C, plo, phi, lo, hi, m);
                         if (stats) {
                             const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                                 __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
@@ -584,11 +599,14 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                     } else if (EK == EK_GELU) {
                         // z = acc + bias kept for the backward (aux), y = GELU(z)
                         float z[4] = {a[0] + bv[0], a[1] + bv[1], a[2] + bv[2], a[3] + bv[3]};
-                        const long o = (long)m * p.ldc + n;
-                        if (p.aux)
-                            *reinterpret_cast<uint2*>(p.aux + o) = make_uint2(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]));
-                        *reinterpret_cast<uint2*>((bf16_t*)p.C + o) =
-                            make_uint2(pack2bf(gelu_erf(z[0]), gelu_erf(z[1])), pack2bf(gelu_erf(z[2]), gelu_erf(z[3])));
+                        const uint32_t zl = pack2bf(z[0], z[1]), zh = pack2bf(z[2], z[3]);
+                        const uint32_t yl = pack2bf(gelu_erf(z[0]), gelu_erf(z[1]));
+                        const uint32_t yh = pack2bf(gelu_erf(z[2]), gelu_erf(z[3]));
+                        if ((i & 1) == 0) { zlo = zl; zhi = zh; plo = yl; phi = yh; }
+                        else {
+                            if (p.aux) store_pair(p.aux, zlo, zhi, zl, zh, m);
+                            store_pair(p.C, plo, phi, yl, yh, m);
+                        }
                     } else if (EK == EK_DGELU) {
                         // dZ = dH * GELU'(z) (z = the Linear's saved pre-activation), and the
                         // column sums of the stored dZ: that Linear's bias gradient
@@ -759,7 +777,17 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
 
     // phases 1-4: the four quarter-products of the E buffer (tile kE); stO1
     // stages the last O half of tile kE+1, more stages tile kE+2 into E
-    auto phasesE = [&](int kE, bool stO1, bool more) {
+    // phase-4 wait that retires tile O: normally VM6 (the three stages issued after O's
+    // last half); right after a store-behind epilogue O was staged whole BEFORE the
+    // tile's epilogue stores, so it retires with those stores still in flight: `hold`
+    // = stores + 6 (a lower bound of the ops issued after O)
+    auto vm_retire_o = [&](int hold) {
+        if (hold == 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+        else if (hold == 30) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+        else if (hold == 38) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+        else VM6();
+    };
+    auto phasesE = [&](int kE, bool stO1, bool more, int hold = 0) {
         // phase 1: E (0,0)
         readA(0, 0);
         readB(0, 0, fb0);
@@ -780,7 +808,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         mma(1, 1, fb1);
         BARRIER();
         // phase 4: E (1,0); retire O(kE+1)
-        if (more) { sb.stage(p, smem, 0, 1, kE + 2); VM6(); } else { VM0(); }
+        if (more) { sb.stage(p, smem, 0, 1, kE + 2); vm_retire_o(hold); } else { VM0(); }
         BARRIER();
         mma(1, 0, fb0);
         BARRIER();
@@ -816,6 +844,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         prologueO();
     }
     publish();
+    int hold_o = 0;     // != 0: the coming tile's O was staged before the previous tile's stores
     for (;;) {
         if (nK > 0) {
             const int pairs = nK / 2;
@@ -823,7 +852,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 const int kE = kt0 + 2 * it, kO = kE + 1;
                 const bool more = kE + 2 < kt_end;
                 const bool moreO = kO + 2 < kt_end;
-                phasesE(kE, true, more);
+                // first pair after a store-behind epilogue: O is already staged whole
+                if constexpr (BNB) phasesE(kE, true, more);
+                else phasesE(kE, !(it == 0 && hold_o), more, it == 0 ? hold_o : 0);
                 // phase 5: O (0,0)
                 readA(1, 0);
                 readB(1, 0, fb0);
@@ -888,6 +919,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                     sa.stage(p, smem, 1, 0, kt0 + 1);
                     sb.stage(p, smem, 1, 0, kt0 + 1);
                     sb.stage(p, smem, 1, 1, kt0 + 1);
+                    sa.stage(p, smem, 1, 1, kt0 + 1);   // all of O ahead of the stores (see vm_retire_o)
                 }
             }
             // interior tiles take a lean variant (no bounds checks, one store per site);
@@ -909,20 +941,26 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 return;
             }
             zero_acc();
+            hold_o = 0;
             vt = vn;
             if (nK > 0) {
                 if (behind) {
                     // E landed once at most (O loads) + (epilogue stores) remain outstanding;
                     // GELU tiles store twice per site (output + pre-activation): the 6-bit
                     // counter's maximum is a stronger wait than needed, never a weaker one
+                    // per wave: EK_BF16 16 pair stores (+8 statistics stores), EK_GELU 32;
+                    // E retires with O (8 ops, nK > 1) and those stores younger than it
                     if (p.ek == EK_GELU) {
-                        asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-                    } else if (nK > 1) {
-                        if (p.colstats) asm volatile("s_waitcnt vmcnt(46)" ::: "memory");
-                        else asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
-                    } else {
-                        if (p.colstats) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+                        if (nK > 1) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
                         else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                        hold_o = nK > 1 ? 38 : 0;
+                    } else if (nK > 1) {
+                        if (p.colstats) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+                        hold_o = p.colstats ? 30 : 22;
+                    } else {
+                        if (p.colstats) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
                     }
                     BARRIER();
 #if DDL_STAGGER
@@ -1176,9 +1214,9 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     if (splits > 1 || (p.out_f32 && !p.bias && p.act == ACT_NONE))
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_F32 : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_NONE && (!p.bias || p.bias_bf16) && !p.row_remap)
-        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_BF16 : EK_GEN;
+        p.ek = (p.N % 8 == 0 && p.ldc % 8 == 0) ? EK_BF16 : EK_GEN;   // 16-byte pair stores
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_GELU && (!p.bias || p.bias_bf16) && !p.row_remap && !p.res)
-        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_GELU : EK_GEN;
+        p.ek = (p.N % 8 == 0 && p.ldc % 8 == 0) ? EK_GELU : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_DGELU && p.aux && !p.bias && !p.row_remap && !p.res)
         p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_DGELU : EK_GEN;
     else
