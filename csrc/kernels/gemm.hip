@@ -392,6 +392,18 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
 
     // ---- epilogue: lane holds C[m][n..n+3]
     const int g = lane >> 4;
+    // Interior tiles with 8-element-aligned rows store two row blocks (i, i + 1) of a
+    // column group per lane as ONE 16-byte store: v_permlane16_swap gives the odd lane
+    // rows (g = 1, 3) block i + 1's quads of the even rows in exchange for theirs of
+    // block i, so every lane holds 8 consecutive columns of one row (8-byte stores left
+    // these output-heavy tiles store-issue bound).  Needs every lane active.
+    const bool wide = m0 + BM <= p.M && n0 + BNT <= p.N && (p.N & 7) == 0 && (p.ldc & 7) == 0;
+    auto store_pair = [&](bf16_t* base, uint32_t lo0, uint32_t hi0, uint32_t lo1, uint32_t hi1, int mA, int nb) {
+        const auto x = __builtin_amdgcn_permlane16_swap(lo0, lo1, false, false);
+        const auto y = __builtin_amdgcn_permlane16_swap(hi0, hi1, false, false);
+        const int mrow = (lane & 16) ? mA + 16 : mA;       // g odd: row block i + 1
+        *reinterpret_cast<uint4*>(base + (long)mrow * p.ldc + nb + (lane >> 5) * 8) = make_uint4(x[0], y[0], x[1], y[1]);
+    };
     float st_s[NJ][4], st_q[NJ][4];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -422,6 +434,31 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
             float mu[4], is[4];
             load4(p.bn_mean + min(n, p.N - 4), mu);
             load4(p.bn_istd + min(n, p.N - 4), is);
+            if (wide) {
+                uint32_t plo = 0, phi = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float xv[4] = {__uint_as_float(xr[i][j].x << 16), __uint_as_float(xr[i][j].x & 0xffff0000u),
+                                         __uint_as_float(xr[i][j].y << 16), __uint_as_float(xr[i][j].y & 0xffff0000u)};
+                    const float rv[4] = {__uint_as_float(rr[i][j].x << 16), __uint_as_float(rr[i][j].x & 0xffff0000u),
+                                         __uint_as_float(rr[i][j].y << 16), __uint_as_float(rr[i][j].y & 0xffff0000u)};
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = ((mb[i][j] >> r) & 1u) ? acc[i][j][r] + rv[r] : 0.f;
+                    const uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+                    if ((i & 1) == 0) { plo = lo; phi = hi; }
+                    else store_pair((bf16_t*)p.C, plo, phi, lo, hi, m0 + wm * 64 + (i - 1) * 16 + (lane & 15),
+                                    n0 + wn * WN + j * 16);
+                    const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                        __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        st_s[j][r] += t[r];
+                        st_q[j][r] += t[r] * (xv[r] - mu[r]) * is[r];
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -443,9 +480,49 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
             }
         }
     }
+    const bool wide_plain = !BNB && wide && !(p.out_f32) && !p.trans_out && !p.row_remap && !p.bias &&
+                            p.act == ACT_NONE && !p.accumulate;
+    if (wide_plain) {
+        // bf16 (+ residual) (+ BatchNorm statistics of the stored values), pair stores
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int nb = n0 + wn * WN + j * 16;
+            uint2 rb[4];
+            if (p.res) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    rb[i] = *reinterpret_cast<const uint2*>(p.res + (long)(m0 + wm * 64 + i * 16 + (lane & 15)) * p.ldc +
+                                                            nb + 4 * g);
+            }
+            uint32_t plo = 0, phi = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                if (p.res) {
+                    v[0] += __uint_as_float(rb[i].x << 16);
+                    v[1] += __uint_as_float(rb[i].x & 0xffff0000u);
+                    v[2] += __uint_as_float(rb[i].y << 16);
+                    v[3] += __uint_as_float(rb[i].y & 0xffff0000u);
+                }
+                const uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+                if ((i & 1) == 0) { plo = lo; phi = hi; }
+                else store_pair((bf16_t*)p.C, plo, phi, lo, hi, m0 + wm * 64 + (i - 1) * 16 + (lane & 15), nb);
+                if (p.colstats) {
+                    const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                        __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        st_s[j][r] += t[r];
+                        st_q[j][r] += t[r] * t[r];
+                    }
+                }
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if constexpr (BNB) break;
+        if (wide_plain) break;
         const int m = m0 + wm * 64 + i * 16 + (lane & 15);
         if (m >= p.M) continue;
         const long orow = out_row(p, m);
