@@ -332,11 +332,13 @@ def test_split_k_reduce_thread_groups(splits, kernel, accumulate, with_bias, out
     assert _rel_err(out, want) < (2e-3 if out_f32 else 1e-2)
 
 
-def test_linear_dgrad_uses_current_weights_after_flat_optimizer_steps():
+@pytest.mark.parametrize("dgrad_nt", [False, True])
+def test_linear_dgrad_uses_current_weights_after_flat_optimizer_steps(dgrad_nt, monkeypatch):
     """The NT dgrad's cached W^T must follow the flat optimizer's in-place updates (they
-    write the arena behind the parameter views' version counters)."""
+    write the arena behind the parameter views' version counters); the NN dgrad reads W."""
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd.ops import _native_linear
+    monkeypatch.setattr(_native_linear, "_DGRAD_NT", dgrad_nt)
     from databricks_distributed_deep_learning_amd.optim import FlatSGD, ParamArena
     torch.manual_seed(4)
     lin = torch.nn.Linear(128, 256).to(dev).to(torch.bfloat16)
