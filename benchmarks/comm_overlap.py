@@ -33,6 +33,7 @@ SHAPES = [  # name, mode, M, N, K, act
     ("r50_1x1_64to256", 0, 802816, 256, 64, None),
     ("sq8192", 0, 8192, 8192, 8192, None),
     ("bert_nn_dgrad", 1, 16384, 768, 3072, None),       # dx = dy W (W reduction-outer)
+    ("bert_nn_dgelu", 1, 16384, 3072, 768, "dgelu"),    # FFN1 dgrad * GELU'(z) + bias-grad sums
     ("bert_tn_wgrad_3072x768", 2, 3072, 768, 16384, None),   # dW = dy^T x (split-K)
     ("bert_tn_wgrad_768x3072", 2, 768, 3072, 16384, None),
 ]
@@ -60,12 +61,17 @@ def main() -> int:
         lda = M if mode == 2 else K
         ldb = K if mode == 0 else N
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        bias = torch.randn(N, device=dev).to(torch.bfloat16) if act else None
+        bias = torch.randn(N, device=dev).to(torch.bfloat16) if act in ("gelu", "gelu_noaux") else None
         z = torch.empty_like(c) if act == "gelu" else None
+        stats = None
+        if act == "dgelu":
+            z = torch.randn_like(c)
+            stats = torch.empty((M + 127) // 128 * 2 * N, device=dev)
         act_k = "gelu" if act == "gelu_noaux" else act
 
         def run():
-            gemm(mode, a, lda, w, ldb, c, N, M, N, K, bias=bias, act=act_k, aux=z, kernel="big")
+            gemm(mode, a, lda, w, ldb, c, N, M, N, K, bias=bias, act=act_k, aux=z, kernel="big",
+                 colstats=stats)
         for _ in range(3):
             run()
         torch.cuda.synchronize()

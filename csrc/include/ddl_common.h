@@ -111,29 +111,66 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 
 // ---------------------------------------------------------------- math
-// erf for the GELU epilogues: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far
-// below bf16 resolution) -- one reciprocal, one exp and a degree-5 Horner chain,
-// branch-free, ~12 VALU ops instead of the ~30 (two-range, branching) of erff.  The
-// FFN GEMM applies it to 128 values per lane per output tile, where it was the
-// epilogue's main cost.
-__device__ __forceinline__ float erf_fast(float x) {
-    const float ax = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
-    const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
-                        0.254829592f) * t;
-    return copysignf(1.f - poly * __expf(-ax * ax), x);
+// GELU / GELU' for the epilogues: the Abramowitz & Stegun 7.1.26 erf (|error| <= 1.5e-7,
+// far below bf16 resolution) -- one reciprocal, one exponential and a degree-5 Horner
+// chain, branch-free.  With x = z / sqrt(2), t = 1 / (1 + p |x|) and
+// erf(x) = sign(x) (1 - t P(t) e^{-x^2}):
+//   GELU(z)  = max(z, 0) - w,            w = 0.5 |z| t P(t) e^{-z^2/2}
+//   GELU'(z) = 0.5 + copysign(0.5 - 0.5 t P(t) e^{-z^2/2}, z) + z phi(z)
+// (no copysign/1+ on the GELU path; the grad shares the one exponential with phi).
+// The *2 forms run two elements as packed f32 (v_pk_fma / v_pk_mul: half the issue
+// cycles of scalar f32 VALU): the FFN GEMM epilogues evaluate them for 128 values per
+// lane per output tile with no MFMA to hide behind, where they were the main cost.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+namespace gelu_c {
+constexpr float P1 = 0.3275911f * 0.70710678118654752f;   // p / sqrt(2)
+constexpr float A1 = 0.254829592f, A2 = -0.284496736f, A3 = 1.421413741f, A4 = -1.453152027f,
+                A5 = 1.061405429f;
+constexpr float NH_LOG2E = -0.5f * 1.4426950408889634f;    // e^{-z^2/2} = 2^{z * (z * NH_LOG2E)}
+constexpr float INV_SQRT_2PI = 0.3989422804014327f;
+}  // namespace gelu_c
+__device__ __forceinline__ f32x2_t gelu_erf2(f32x2_t z) {
+    using namespace gelu_c;
+    const f32x2_t a = {fabsf(z.x), fabsf(z.y)};
+    const f32x2_t d = a * P1 + 1.f;
+    const f32x2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    f32x2_t q = t * (0.5f * A5) + (0.5f * A4);
+    q = q * t + (0.5f * A3);
+    q = q * t + (0.5f * A2);
+    q = q * t + (0.5f * A1);
+    const f32x2_t s = (z * NH_LOG2E) * z;
+    const f32x2_t e = {__builtin_amdgcn_exp2f(s.x), __builtin_amdgcn_exp2f(s.y)};
+    const f32x2_t w = (a * t) * (q * e);
+    const f32x2_t r = {fmaxf(z.x, 0.f), fmaxf(z.y, 0.f)};
+    return r - w;
 }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
-// GELU'(x) = Phi(x) + x phi(x): the A&S erf of x/sqrt(2) and the normal density share
-// the one exponential exp(-x^2/2)
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float ax = fabsf(x) * 0.70710678118654752f;
-    const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
-    const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
-                        0.254829592f) * t;
-    const float e = __expf(-0.5f * x * x);
-    const float erf_v = copysignf(1.f - poly * e, x);
-    return 0.5f * (1.f + erf_v) + x * (0.3989422804014327f * e);
+__device__ __forceinline__ f32x2_t gelu_erf_grad2(f32x2_t z) {
+    using namespace gelu_c;
+    const f32x2_t a = {fabsf(z.x), fabsf(z.y)};
+    const f32x2_t d = a * P1 + 1.f;
+    const f32x2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    f32x2_t q = t * (-0.5f * A5) + (-0.5f * A4);
+    q = q * t + (-0.5f * A3);
+    q = q * t + (-0.5f * A2);
+    q = q * t + (-0.5f * A1);
+    const f32x2_t s = (z * NH_LOG2E) * z;
+    const f32x2_t e = {__builtin_amdgcn_exp2f(s.x), __builtin_amdgcn_exp2f(s.y)};
+    const f32x2_t h = (q * t) * e + 0.5f;   // 0.5 - 0.5 t P e, in [0, 0.5]
+    const f32x2_t c = {copysignf(h.x, z.x), copysignf(h.y, z.y)};
+    return (z * INV_SQRT_2PI) * e + c + 0.5f;
+}
+__device__ __forceinline__ float gelu_erf(float z) {
+    using namespace gelu_c;
+    const float a = fabsf(z), t = __builtin_amdgcn_rcpf(a * P1 + 1.f);
+    const float q = (((t * (0.5f * A5) + (0.5f * A4)) * t + (0.5f * A3)) * t + (0.5f * A2)) * t + (0.5f * A1);
+    return fmaxf(z, 0.f) - (a * t) * (q * __builtin_amdgcn_exp2f((z * NH_LOG2E) * z));
+}
+__device__ __forceinline__ float gelu_erf_grad(float z) {
+    using namespace gelu_c;
+    const float t = __builtin_amdgcn_rcpf(fabsf(z) * P1 + 1.f);
+    const float q = (((t * (-0.5f * A5) + (-0.5f * A4)) * t + (-0.5f * A3)) * t + (-0.5f * A2)) * t + (-0.5f * A1);
+    const float e = __builtin_amdgcn_exp2f((z * NH_LOG2E) * z);
+    return (z * INV_SQRT_2PI) * e + copysignf((q * t) * e + 0.5f, z) + 0.5f;
 }
 
 // Counter-based dropout RNG: masks are regenerated in backward, never stored.  ONE

@@ -600,8 +600,8 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         // z = acc + bias kept for the backward (aux), y = GELU(z)
                         float z[4] = {a[0] + bv[0], a[1] + bv[1], a[2] + bv[2], a[3] + bv[3]};
                         const uint32_t zl = pack2bf(z[0], z[1]), zh = pack2bf(z[2], z[3]);
-                        const uint32_t yl = pack2bf(gelu_erf(z[0]), gelu_erf(z[1]));
-                        const uint32_t yh = pack2bf(gelu_erf(z[2]), gelu_erf(z[3]));
+                        const f32x2_t y0 = gelu_erf2(f32x2_t{z[0], z[1]}), y1 = gelu_erf2(f32x2_t{z[2], z[3]});
+                        const uint32_t yl = pack2bf(y0.x, y0.y), yh = pack2bf(y1.x, y1.y);
                         if ((i & 1) == 0) { zlo = zl; zhi = zh; plo = yl; phi = yh; }
                         else {
                             if (p.aux) store_pair(p.aux, zlo, zhi, zl, zh, m);
@@ -614,8 +614,9 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         const uint2 z2 = rb[qm][i];
                         const float z[4] = {__uint_as_float(z2.x << 16), __uint_as_float(z2.x & 0xffff0000u),
                                             __uint_as_float(z2.y << 16), __uint_as_float(z2.y & 0xffff0000u)};
-                        const uint32_t lo = pack2bf(a[0] * gelu_erf_grad(z[0]), a[1] * gelu_erf_grad(z[1]));
-                        const uint32_t hi = pack2bf(a[2] * gelu_erf_grad(z[2]), a[3] * gelu_erf_grad(z[3]));
+                        const f32x2_t d0 = f32x2_t{a[0], a[1]} * gelu_erf_grad2(f32x2_t{z[0], z[1]});
+                        const f32x2_t d1 = f32x2_t{a[2], a[3]} * gelu_erf_grad2(f32x2_t{z[2], z[3]});
+                        const uint32_t lo = pack2bf(d0.x, d0.y), hi = pack2bf(d1.x, d1.y);
                         *reinterpret_cast<uint2*>((bf16_t*)p.C + o) = make_uint2(lo, hi);
                         if (stats) {
                             const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
