@@ -36,11 +36,61 @@ STATS_EPILOGUE = os.environ.get("DDL_BN_STATS_EPI", "1") != "0"   # 0: always a 
 _DGRAD_NT = os.environ.get("DDL_DGRAD_NT", "1") != "0"
 
 
+_CONV3X3 = os.environ.get("DDL_CONV3X3", "1") != "0"
+
+
+def _direct3x3_ok(x_shape, w_shape, stride, pad):
+    """Shapes the direct 3x3 kernel (csrc/kernels/conv3x3.hip) covers: stride 1, pad 1,
+    64 -> 64 channels, 49 <= W <= 64 with W % 8 == 0 (ResNet stage-1 conv2)."""
+    N, H, W_, C = x_shape
+    K, R, S, _ = w_shape
+    return (_CONV3X3 and R == 3 and S == 3 and stride == 1 and pad == 1 and C == 64 and K == 64
+            and W_ % 8 == 0 and 49 <= W_ <= 64 and N * H * W_ * 64 * 2 < 2 ** 31)
+
+
+def _direct3x3(x, w, y, part=None, res=None, bnb=None, grid=0):
+    """y = conv3x3(x, w) by the direct kernel; with ``bnb`` (ops.bridge.BNBackward) the
+    BatchNorm-backward epilogue.  Returns the number of statistics rows written."""
+    N, H, W_, C = x.shape
+    full = (N, H, W_, 64)
+    if (tuple(w.shape) != (64, 3, 3, 64) or tuple(y.shape) != full or C != 64 or not x.is_contiguous()
+            or not w.is_contiguous() or not y.is_contiguous() or x.dtype != torch.bfloat16
+            or w.dtype != torch.bfloat16 or y.dtype != torch.bfloat16):
+        raise ValueError("direct 3x3: operand shapes / layouts not covered")
+    for t in ((res,) + ((bnb.x,) if bnb is not None else ())):
+        if t is not None and (tuple(t.shape) != full or not t.is_contiguous() or t.dtype != torch.bfloat16):
+            raise ValueError("direct 3x3: residual / BN input must match the output")
+    if bnb is not None and bnb.mask is not None and bnb.mask.numel() * 8 < y.numel():
+        raise ValueError("direct 3x3: ReLU mask too short")
+    if part is not None and part.numel() < _direct3x3_rows(N * H * W_) * 128:
+        raise ValueError("direct 3x3: statistics buffer too short")
+    args = (_lib.p(bnb.x), _lib.p(bnb.mask), _lib.p(bnb.mean), _lib.p(bnb.istd)) if bnb is not None else (0, 0, 0, 0)
+    rc = _lib.fn("ddl_conv3x3")(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W_, C, w.shape[0], _lib.p(part),
+                                _lib.p(res), *args, int(grid), _lib.stream())
+    if rc < 0:
+        raise RuntimeError(f"ddl_conv3x3 failed: {rc}")
+    return rc
+
+
+def _direct3x3_rows(M):
+    return max(stats_rows_max(M), 256)
+
+
 def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
     """Implicit-GEMM conv forward; ``stats`` (ops.bridge.BNStats) also collects the
     BatchNorm statistics partials of the output in the GEMM epilogue."""
     N, H, W_, C = x.shape
     K, R, S, _ = w.shape
+    if (bias is None and act is None and residual is None and x.is_cuda
+            and _direct3x3_ok(x.shape, w.shape, stride, pad)):
+        y = torch.empty(N, H, W_, K, dtype=x.dtype, device=x.device)
+        use_stats = STATS_EPILOGUE and stats is not None
+        part = torch.empty(_direct3x3_rows(N * H * W_) * 2 * K, dtype=torch.float32, device=x.device) \
+            if use_stats else None
+        r = _direct3x3(x, w, y, part)
+        if part is not None:
+            stats.set(y, part, r)
+        return y
     P = (H + 2 * pad - R) // stride + 1
     Q = (W_ + 2 * pad - S) // stride + 1
     y = torch.empty(N, P, Q, K, dtype=x.dtype, device=x.device)
@@ -124,6 +174,14 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
     if stride == 1:
         wt = _w_dgrad(w, list(range(R - 1, -1, -1)), list(range(S - 1, -1, -1)))   # flipped [C, R, S, K]
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
+        if dy.is_cuda and _direct3x3_ok(dy.shape, wt.shape, 1, pad) and (bnb is not None or residual is None):
+            # the direct kernel (a stride-1 3x3 dgrad is the same convolution of dy)
+            if bnb is not None:
+                part = torch.empty(_direct3x3_rows(N * H * W_) * 2 * C, dtype=torch.float32, device=dx.device)
+                bnb.set(dx, part, _direct3x3(dy, wt, dx, part, res=residual, bnb=bnb))
+            else:
+                _direct3x3(dy, wt, dx)
+            return dx
         desc = _desc(N, P, Q, K, H, W_, 1, -(R - 1 - pad), -(S - 1 - pad), 1, 1, R, S, H, W_)
         if bnb is None or not _bnb_dgrad(MODE_CONV, dy, 0, wt, R * S * K, dx, N * H * W_, C, R * S * K, desc,
                                          residual, bnb):
