@@ -40,17 +40,20 @@ def main():
     mask = torch.randint(0, 255, (x.numel() // 8,), device="cuda", dtype=torch.uint8)
     hint = SimpleNamespace(x=aux, mask=mask, mean=torch.zeros(64, device="cuda"), istd=torch.ones(64, device="cuda"),
                            set=lambda *args: None)
+    dw = torch.empty(64, 3, 3, 64, device="cuda", dtype=torch.bfloat16)
     out = {}
     for g in a.grid:
         out[f"direct_fwd_stats_g{g}"] = timeit(lambda: nc._direct3x3(x, w, y, part, grid=g))
         out[f"direct_dgrad_bnb_g{g}"] = timeit(lambda: nc._direct3x3(x, w, y, part, bnb=hint, grid=g))
         out[f"direct_fwd_plain_g{g}"] = timeit(lambda: nc._direct3x3(x, w, y, None, grid=g))
+        out[f"direct_wgrad_g{g}"] = timeit(lambda: nc._direct3x3_wgrad(aux, x, dw, False, grid=g))
     nc._CONV3X3 = False
     st = BNStats()
     out["gemm_fwd_stats"] = timeit(lambda: nc._fwd(x, w, 1, 1, stats=st))
     out["gemm_fwd_plain"] = timeit(lambda: nc._fwd(x, w, 1, 1))
     out["gemm_dgrad_bnb"] = timeit(lambda: nc._dgrad(x, w, x.shape, 1, 1, bnb=hint))
     out["gemm_dgrad_plain"] = timeit(lambda: nc._dgrad(x, w, x.shape, 1, 1))
+    out["gemm_wgrad"] = timeit(lambda: nc._wgrad(aux, x, w.shape, 1, 1))
     nc._CONV3X3 = True
     for k, v in out.items():
         print(json.dumps({"case": k, "us": round(v, 1)}))

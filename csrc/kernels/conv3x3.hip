@@ -331,6 +331,225 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_k(C3Params p) {
     }
 }
 
+
+// ======================================================================= weight gradient
+// dW[k][r][s][c] = sum over output pixels p of dy[p][k] * x[p + (r - 1, s - 1)][c], as
+// dW^T (rows (tap, c), columns k) on MFMA with the pixels as the reduction: the same
+// persistent row-pair walk as the forward, x rows in the LDS ring, the tile's two dy
+// rows in a double-buffered LDS image, both fed one tile ahead by LDS-DMA.  Fragments
+// are k-major reads (ds_read_b64_tr_b16) of those images -- the 9 taps are 9 pixel
+// shifts of the same x rows.  Wave w owns channels 16w..16w+15 of every tap and all 64
+// k: 9 x 4 accumulator tiles (144 AGPRs) summed over all the workgroup's tiles, then one
+// fp32 partial [576][64] per workgroup, reduced (and transposed) by conv3x3_wgrad_reduce_k.
+// (The implicit GEMM ran this as a 64 x 576 x 802816 split-K CONVW GEMM at ~290 TF.)
+constexpr int DYB = 2 * 64 * 128;                 // one dy tile image: 2 rows x 64 pixel slots
+constexpr int WG_LDS = NSLOT * ROWB + 2 * DYB;    // x ring + zero row, two dy images
+
+struct C3WParams {
+    const bf16_t* x;       // [N, H, W, 64] conv input
+    const bf16_t* dy;      // [N, H, W, 64] output gradient
+    float* part;           // [gridDim.x][576][64]
+    int N, H, W, HP, tiles, chunk;
+    int dbg;
+};
+
+// transposing LDS read (ds_read_b64_tr_b16) the compiler does not track: the caller waits
+// (lgkmcnt) by hand -- tracked reads drew lgkmcnt(0) waits in the middle of the MFMA stream
+__device__ __forceinline__ s16x4 ds_read_tr(uint32_t addr) {
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+// k-major fragment (rows = the image's columns) from the two tr reads at LDS addresses a, b
+__device__ __forceinline__ bf16x8 tr_frag(uint32_t a, uint32_t b) {
+    const s16x4 lo = ds_read_tr(a), hi = ds_read_tr(b);
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// dy rows h0, h0 + 1 of image n into dy image `buf` (pixel slot swizzle: slot & 7)
+__device__ __forceinline__ void issue_dy(const C3WParams& p, char* smem, int n, int h0, int buf, int wv, int lane) {
+    char* base = smem + NSLOT * ROWB + buf * DYB;
+    const int nq = p.W >> 3;
+    for (int rr = 0; rr < 2; ++rr) {
+        if (h0 + rr >= p.H) continue;      // stays zero (cleared when the buffer is recycled)
+        const bf16_t* src = p.dy + ((long)n * p.H + h0 + rr) * p.W * CH;
+        for (int q = wv; q < nq; q += 4) {
+            const int px = q * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ (px & 7);
+            glds(src + px * CH + c * 8, base + rr * 8192 + q * 1024);
+        }
+    }
+}
+
+__device__ __forceinline__ void issue_xrow(const C3WParams& p, char* smem, int n, int h, int slot, int wv, int lane) {
+    char* base = smem + slot * ROWB + 128;
+    const bf16_t* src = p.x + ((long)n * p.H + h) * p.W * CH;
+    const int nq = p.W >> 3;
+    for (int q = wv; q < nq; q += 4) {
+        const int px = q * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ swz(px + 1);
+        glds(src + px * CH + c * 8, base + q * 1024);
+    }
+}
+
+__global__ __launch_bounds__(NT, 1) void conv3x3_wgrad_k(C3WParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[WG_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, pq = lane & 3;
+    for (int i = tid; i < WG_LDS / 16; i += NT) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+
+    // per-lane tr-read byte offsets (kernel constants; the step / row parts are scalar).
+    // x (A, rows = channels 16 wv + .., k = pixels): image row (pixel slot)
+    //   hw * 32 + s + 8 g + q4 (+ 4), column chunk 2 wv + (pq >> 1); the swizzle (slot & 7)
+    //   depends on s but not on hw (32 | hw * 32).
+    // dy (B, rows = k, k = pixels): slot (ks >> 1) * 64 + (ks & 1) * 32 + 8 g + q4 (+ 4).
+    uint32_t xo[3][2], dyo[4][2];
+#pragma unroll
+    for (int sh = 0; sh < 3; ++sh)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int ra = sh + 8 * g + q4 + 4 * e;
+            xo[sh][e] = ra * 128 + (((2 * wv + (pq >> 1)) ^ swz(ra)) << 4) + (pq & 1) * 8;
+        }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int slot = 8 * g + q4 + 4 * e;
+            dyo[j][e] = slot * 128 + (((2 * j + (pq >> 1)) ^ (slot & 7)) << 4) + (pq & 1) * 8;
+        }
+
+    f32x4 acc[9][4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int t0 = blockIdx.x * p.chunk, t1 = min(p.tiles, t0 + p.chunk);
+    int sl[4] = {ZSLOT, ZSLOT, ZSLOT, ZSLOT};
+    int ptr = 0;
+    bool pref = false;
+    for (int T = t0; T < t1; ++T) {
+        const int n = T / p.HP, h0 = (T - n * p.HP) * 2;
+        const int buf = (T - t0) & 1;
+        if (!pref) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int h = h0 - 1 + r;
+                if (h < 0 || h >= p.H) { sl[r] = ZSLOT; continue; }
+                sl[r] = ptr;
+                ptr = ptr == NRING - 1 ? 0 : ptr + 1;
+                issue_xrow(p, smem, n, h, sl[r], wv, lane);
+            }
+            issue_dy(p, smem, n, h0, buf, wv, lane);
+            if (h0 + 1 >= p.H)      // odd H: the missing second dy row must read as zeros
+                for (int i = tid; i < 8192 / 16; i += NT)
+                    reinterpret_cast<uint4*>(smem + NSLOT * ROWB + buf * DYB + 8192)[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // prefetch the next tile: its two new x rows and its dy rows (other dy image; a
+        // missing second row -- odd H -- is cleared instead)
+        int nsl[4] = {sl[2], sl[3], ZSLOT, ZSLOT};
+        const bool npref = T + 1 < t1 && h0 + 2 < p.H;
+        if (npref) {
+#pragma unroll
+            for (int r = 2; r < 4; ++r) {
+                const int h = h0 + 1 + r;
+                if (h >= p.H) continue;
+                nsl[r] = ptr;
+                ptr = ptr == NRING - 1 ? 0 : ptr + 1;
+                if (!(p.dbg & 2)) issue_xrow(p, smem, n, h, nsl[r], wv, lane);
+            }
+            if (h0 + 3 >= p.H)
+                for (int i = tid; i < 8192 / 16; i += NT)
+                    reinterpret_cast<uint4*>(smem + NSLOT * ROWB + (buf ^ 1) * DYB + 8192)[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (!(p.dbg & 2)) issue_dy(p, smem, n, h0 + 2, buf ^ 1, wv, lane);
+        }
+
+        // 4 pixel k-steps of 32 (row ks >> 1, columns (ks & 1) * 32 ..): 9 taps x 4 k-blocks;
+        // step ks + 1's fragments are read under step ks's MFMAs
+        const uint32_t lds_base = (uint32_t)(uintptr_t)smem;
+        const uint32_t dyb = lds_base + NSLOT * ROWB + buf * DYB;
+        const uint32_t xb[4] = {lds_base + sl[0] * ROWB, lds_base + sl[1] * ROWB, lds_base + sl[2] * ROWB,
+                                lds_base + sl[3] * ROWB};
+        bf16x8 fx[2][9], fd[2][4];
+        auto read_ks = [&](int ks, bf16x8 (&ax)[9], bf16x8 (&ad)[4]) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int r = t / 3, sh = t - r * 3;
+                const uint32_t rb = xb[(ks >> 1) + r] + (ks & 1) * 32 * 128;
+                ax[t] = tr_frag(rb + xo[sh][0], rb + xo[sh][1]);
+            }
+            const uint32_t db = dyb + ks * 32 * 128;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ad[j] = tr_frag(db + dyo[j][0], db + dyo[j][1]);
+        };
+        read_ks(0, fx[0], fd[0]);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            if (p.dbg & 4) break;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // step ks's reads
+            __builtin_amdgcn_sched_barrier(0);
+            const int c = ks & 1;
+            if (ks + 1 < 4) read_ks(ks + 1, fx[c ^ 1], fd[c ^ 1]);
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[c][j], fx[c][t], acc[t][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        sl[0] = nsl[0]; sl[1] = nsl[1]; sl[2] = nsl[2]; sl[3] = nsl[3];
+        pref = npref;
+    }
+    // partial dW^T of this workgroup: rows (tap, c = 16 wv + r16), 4 consecutive k per lane
+    const int c = 16 * wv + (lane & 15);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            *reinterpret_cast<f32x4*>(p.part + (((long)blockIdx.x * 9 + t) * 64 + c) * 64 + j * 16 + 4 * g) = acc[t][j];
+}
+
+// out[k][m] (+)= sum_b part[b][m][k], m = tap * 64 + c (576 rows), k < 64.  Block: 2 rows
+// of m x 16 k-quads x 8 slab groups, combined through LDS.
+__global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_k(const float* __restrict__ part, int nparts, void* out,
+                                                               int out_f32, int accumulate) {
+    __shared__ f32x4 red[8][32];
+    const int t = threadIdx.x, quad = t & 15, mr = (t >> 4) & 1, grp = t >> 5;
+    const int m = blockIdx.x * 2 + mr;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+    int b = grp;
+    for (; b + 8 < nparts; b += 16) {
+        s0 += *reinterpret_cast<const f32x4*>(part + ((long)b * 576 + m) * 64 + 4 * quad);
+        s1 += *reinterpret_cast<const f32x4*>(part + ((long)(b + 8) * 576 + m) * 64 + 4 * quad);
+    }
+    if (b < nparts) s0 += *reinterpret_cast<const f32x4*>(part + ((long)b * 576 + m) * 64 + 4 * quad);
+    red[grp][t & 31] = s0 + s1;
+    __syncthreads();
+    if (grp == 0) {
+        f32x4 v = red[0][t];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) v += red[i][t];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const long o = (long)(4 * quad + e) * 576 + m;
+            if (out_f32) {
+                float* d = (float*)out + o;
+                *d = accumulate ? *d + v[e] : v[e];
+            } else {
+                bf16_t* d = (bf16_t*)out + o;
+                *d = f2bf(accumulate ? bf2f(*d) + v[e] : v[e]);
+            }
+        }
+    }
+}
 }  // namespace
 
 // Direct 3x3 stride-1 pad-1 conv, 64 -> 64 channels, W in [49, 64] with W % 8 == 0.
@@ -370,4 +589,30 @@ DDL_API int ddl_conv3x3(const void* x, const void* w, void* y, int N, int H, int
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -2 - (int)e;
     return colstats ? g : 0;
+}
+
+// Weight gradient of the direct 3x3 conv (same shape coverage as ddl_conv3x3): dw [64][3][3][64]
+// (bf16 or fp32, accumulate: +=).  ws: >= grid * 576 * 64 floats (grid <= 0: 256).
+// Returns 0, -1 when the shape is not covered (nothing launched), or -2 - hipError.
+DDL_API int ddl_conv3x3_wgrad(const void* x, const void* dy, void* dw, int N, int H, int W, int C, int K, float* ws,
+                              long ws_elems, int accumulate, int out_f32, int grid, hipStream_t stream) {
+    if (C != CH || K != CH || W % 8 != 0 || W < 49 || W > 64 || H < 1 || N < 1) return -1;
+    C3WParams p{};
+    p.x = (const bf16_t*)x;
+    p.dy = (const bf16_t*)dy;
+    p.N = N; p.H = H; p.W = W; p.HP = (H + 1) / 2;
+    p.tiles = N * p.HP;
+    int g = grid > 0 ? grid : 256;
+    g = std::min(g, p.tiles);
+    p.chunk = (p.tiles + g - 1) / g;
+    g = (p.tiles + p.chunk - 1) / p.chunk;
+    if (ws_elems < (long)g * 576 * 64) return -1;
+    p.part = ws;
+    static const int dbg = getenv("DDL_CONV3X3_DBG") ? atoi(getenv("DDL_CONV3X3_DBG")) : 0;
+    p.dbg = dbg;
+    hipLaunchKernelGGL(conv3x3_wgrad_k, dim3(g), dim3(NT), 0, stream, p);
+    hipLaunchKernelGGL(conv3x3_wgrad_reduce_k, dim3(288), dim3(256), 0, stream, (const float*)ws, g, dw, out_f32,
+                       accumulate);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -2 - (int)e;
 }

@@ -273,12 +273,31 @@ def _pick_dgrad_path(key, serial, multi, dx):
     return best
 
 
+def _direct3x3_wgrad(dy, x, dw, accumulate, grid=0):
+    """dW of the direct 3x3 conv: per-workgroup fp32 partials + one reduce (conv3x3.hip)."""
+    N, H, W_, C = x.shape
+    if (tuple(dy.shape) != (N, H, W_, 64) or tuple(dw.shape) != (64, 3, 3, 64) or not dy.is_contiguous()
+            or not x.is_contiguous() or not dw.is_contiguous() or dy.dtype != torch.bfloat16
+            or x.dtype != torch.bfloat16 or dw.dtype not in (torch.bfloat16, torch.float32)):
+        raise ValueError("direct 3x3 wgrad: operand shapes / layouts not covered")
+    g = grid if grid > 0 else 256
+    ws = torch.empty(g * 576 * 64, dtype=torch.float32, device=x.device)
+    rc = _lib.fn("ddl_conv3x3_wgrad")(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), N, H, W_, C, 64, ws.data_ptr(),
+                                      ws.numel(), int(accumulate), int(dw.dtype == torch.float32), int(grid),
+                                      _lib.stream())
+    if rc != 0:
+        raise RuntimeError(f"ddl_conv3x3_wgrad failed: {rc}")
+    return dw
+
+
 def _wgrad(dy, x, w_shape, stride, pad, out=None):
     N, H, W_, C = x.shape
     K, R, S, _ = w_shape
     _, P, Q, _ = dy.shape
     acc = out is not None
     dw = out if acc else torch.empty(K, R, S, C, dtype=dy.dtype, device=dy.device)
+    if x.is_cuda and _direct3x3_ok(x.shape, w_shape, stride, pad) and dw.is_contiguous():
+        return _direct3x3_wgrad(dy, x, dw, acc)
     M = N * P * Q
     if R == 1 and S == 1 and stride == 1 and pad == 0:
         gemm(MODE_TN, dy, K, x, C, dw, C, K, C, M, accumulate=acc)

@@ -87,3 +87,25 @@ def test_direct3x3_conv_autograd_matches_reference():
     torch.testing.assert_close(y.float(), yr.permute(0, 2, 3, 1), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(w.grad.float(), wr.grad.permute(0, 2, 3, 1), atol=0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("shape,grid,acc,f32", [((2, 56, 56), 0, False, False), ((3, 7, 56), 2, True, False),
+                                                 ((2, 9, 64), 3, False, True), ((1, 1, 56), 0, True, True)])
+def test_direct3x3_wgrad(shape, grid, acc, f32):
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as nc
+    N, H, W = shape
+    torch.manual_seed(3)
+    x = torch.randn(N, H, W, 64, device="cuda").bfloat16()
+    dy = torch.randn(N, H, W, 64, device="cuda").bfloat16()
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = torch.zeros(64, 64, 3, 3, device="cuda", requires_grad=True)
+    F.conv2d(xr, wr, padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    ref = wr.grad.permute(0, 2, 3, 1)                       # [K, 3, 3, C]
+    base = torch.randn(64, 3, 3, 64, device="cuda")
+    dw = (base if f32 else base.bfloat16()).clone() if acc else \
+        torch.empty(64, 3, 3, 64, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
+    nc._direct3x3_wgrad(dy, x, dw, acc, grid=grid)
+    torch.cuda.synchronize()
+    want = ref + (base if f32 else base.bfloat16().float()) if acc else ref
+    tol = dict(atol=0.05, rtol=1e-2) if f32 else dict(atol=0.25, rtol=1e-2)
+    torch.testing.assert_close(dw.float(), want, **tol)
