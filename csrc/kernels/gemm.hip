@@ -334,6 +334,7 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = w & 1, wn = w >> 1;
+    const int g = lane >> 4;
 
     f32x4 acc[4][NJ];
 #pragma unroll
@@ -341,6 +342,70 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+    // wide plain-bf16 tiles with a residual: the residual tile is loaded up front, in flight
+    // under the operand loads and MFMAs (short-K GEMMs are epilogue-bound: loading it in the
+    // epilogue serialised a second memory latency behind the operand loads every tile)
+    const bool wide_early = m0 + BM <= p.M && n0 + BNT <= p.N && (p.N & 7) == 0 && (p.ldc & 7) == 0;
+    const bool wide_plain = !BNB && wide_early && !(p.out_f32) && !p.trans_out && !p.row_remap && !p.bias &&
+                            p.act == ACT_NONE && !p.accumulate;
+    uint2 rb_pre[NJ][4];
+    // BNB: the epilogue's BN input / residual / ReLU-mask sites, likewise loaded up front
+    // (unconditional loads from clamped addresses; absent operands read aux and are
+    // replaced afterwards -- a load under a branch gets waited at the join)
+    // (not for the implicit-GEMM conv variants: their loaders leave no registers for it)
+    constexpr bool EARLY_BNB = BNB && LA == KC;
+    uint2 xr[4][NJ], rr[4][NJ];
+    uint32_t mb[4][NJ];
+    // Interior tiles with 64-aligned rows (bnb_vec) load 16 bytes per lane -- 8 columns of
+    // row block i (g even) or i + 1 (g odd), the pair-store layout -- and un-pair them with
+    // v_permlane16_swap in the epilogue; the ReLU mask as one 32 / 64-bit word per row.
+    // (per-site 8-byte and 1-byte loads left the epilogue issue-stalled on the VMEM queue)
+    const bool bnb_vec = wide_early && (p.ldc & 63) == 0;
+    auto bnb_load = [&]() {
+        const bf16_t* auxp = (const bf16_t*)p.aux;
+        const bf16_t* resp = p.res ? p.res : auxp;
+        const uint8_t* mp = p.bn_mask ? p.bn_mask : (const uint8_t*)auxp;
+        if (bnb_vec) {
+#pragma unroll
+            for (int ip = 0; ip < 2; ++ip) {
+                const long mrow = m0 + wm * 64 + (2 * ip + (g & 1)) * 16 + (lane & 15);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const long o = mrow * p.ldc + n0 + wn * WN + j * 16 + (g >> 1) * 8;
+                    const uint4 vx = *reinterpret_cast<const uint4*>(auxp + o);
+                    const uint4 vr = *reinterpret_cast<const uint4*>(resp + o);
+                    xr[2 * ip][j] = make_uint2(vx.x, vx.y);
+                    xr[2 * ip + 1][j] = make_uint2(vx.z, vx.w);
+                    rr[2 * ip][j] = make_uint2(vr.x, vr.y);
+                    rr[2 * ip + 1][j] = make_uint2(vr.z, vr.w);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const long mw = ((long)(m0 + wm * 64 + i * 16 + (lane & 15)) * p.ldc + n0 + wn * WN) >> 3;
+                if constexpr (NJ == 4) {
+                    const uint2 w2 = *reinterpret_cast<const uint2*>(mp + mw);
+                    mb[i][0] = w2.x;
+                    mb[i][1] = w2.y;
+                } else {
+                    mb[i][0] = *reinterpret_cast<const uint32_t*>(mp + mw);
+                }
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long mc = min(m0 + wm * 64 + i * 16 + (lane & 15), p.M - 1);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int nc = min(n0 + wn * WN + j * 16 + 4 * g, p.N - 4);
+                const long o = mc * p.ldc + nc;
+                xr[i][j] = *reinterpret_cast<const uint2*>(auxp + o);
+                rr[i][j] = *reinterpret_cast<const uint2*>(resp + o);
+                mb[i][j] = (uint32_t)mp[o >> 3] >> (nc & 4);
+            }
+        }
+    };
     if (kt0 < kt1) {
         // two K-steps of global loads in flight (register sets 0 / 1 alternate): the
         // 128-row tiles do little MFMA work per K-step, so one step of prefetch left
@@ -351,6 +416,18 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
         if (kt0 + 1 < kt1) {
             la.load(p, (kt0 + 1) * BK, ra1);
             lb.load(p, (kt0 + 1) * BK, rb1);
+        }
+        // (issued after the first operand loads: vmcnt retires in order, so the operand
+        // wait does not also wait for the residual)
+        if constexpr (EARLY_BNB) bnb_load();
+        if (wide_plain && p.res) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    rb_pre[j][i] = *reinterpret_cast<const uint2*>(
+                        p.res + (long)(m0 + (threadIdx.x >> 6 & 1) * 64 + i * 16 + (threadIdx.x & 15)) * p.ldc + n0 +
+                        (threadIdx.x >> 7) * WN + j * 16 + 4 * ((threadIdx.x & 63) >> 4));
         }
         la.store(smem, ra0);
         lb.store(smem + TILE_BYTES, rb0);
@@ -391,7 +468,6 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
     }
 
     // ---- epilogue: lane holds C[m][n..n+3]
-    const int g = lane >> 4;
     // Interior tiles with 8-element-aligned rows store two row blocks (i, i + 1) of a
     // column group per lane as ONE 16-byte store: v_permlane16_swap gives the odd lane
     // rows (g = 1, 3) block i + 1's quads of the even rows in exchange for theirs of
@@ -414,20 +490,39 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
         // relu_mask stored, column sums of dz and dz * xhat.  Pass 1 puts every site's
         // loads in flight at once (clamped addresses; out-of-range sites are dropped in
         // pass 2) -- one site at a time the epilogue is load-latency bound.
-        uint2 xr[4][NJ], rr[4][NJ];
-        uint32_t mb[4][NJ];
+        // (the loads were issued with the first operand loads where that fits: bnb_load)
+        if constexpr (!EARLY_BNB) bnb_load();
+        if (bnb_vec) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const long mc = min(m0 + wm * 64 + i * 16 + (lane & 15), p.M - 1);
+            for (int ip = 0; ip < 2; ++ip)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int nc = min(n0 + wn * WN + j * 16 + 4 * g, p.N - 4);
-                const long o = mc * p.ldc + nc;
-                xr[i][j] = *reinterpret_cast<const uint2*>((const bf16_t*)p.aux + o);
-                rr[i][j] = p.res ? *reinterpret_cast<const uint2*>(p.res + o) : make_uint2(0u, 0u);
-                mb[i][j] = p.bn_mask ? (uint32_t)p.bn_mask[o >> 3] >> (nc & 4) : 0xfu;
+                for (int j = 0; j < NJ; ++j) {
+                    const auto a = __builtin_amdgcn_permlane16_swap(xr[2 * ip][j].x, xr[2 * ip + 1][j].x, false, false);
+                    const auto b = __builtin_amdgcn_permlane16_swap(xr[2 * ip][j].y, xr[2 * ip + 1][j].y, false, false);
+                    xr[2 * ip][j] = make_uint2(a[0], b[0]);
+                    xr[2 * ip + 1][j] = make_uint2(a[1], b[1]);
+                    const auto c = __builtin_amdgcn_permlane16_swap(rr[2 * ip][j].x, rr[2 * ip + 1][j].x, false, false);
+                    const auto d = __builtin_amdgcn_permlane16_swap(rr[2 * ip][j].y, rr[2 * ip + 1][j].y, false, false);
+                    rr[2 * ip][j] = make_uint2(c[0], d[0]);
+                    rr[2 * ip + 1][j] = make_uint2(c[1], d[1]);
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t bits[NJ];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    bits[j] = NJ == 4 ? mb[i][j >> 1] >> ((j & 1) * 16 + 4 * g) : mb[i][0] >> (j * 16 + 4 * g);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) mb[i][j] = bits[j];
             }
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                if (!p.res) rr[i][j] = make_uint2(0u, 0u);
+                mb[i][j] = p.bn_mask ? mb[i][j] & 0xfu : 0xfu;
+            }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int n = n0 + wn * WN + j * 16 + 4 * g;
@@ -480,20 +575,12 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
             }
         }
     }
-    const bool wide_plain = !BNB && wide && !(p.out_f32) && !p.trans_out && !p.row_remap && !p.bias &&
-                            p.act == ACT_NONE && !p.accumulate;
     if (wide_plain) {
-        // bf16 (+ residual) (+ BatchNorm statistics of the stored values), pair stores
+        // bf16 (+ residual, loaded up front) (+ BatchNorm statistics of the stored values), pair stores
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int nb = n0 + wn * WN + j * 16;
-            uint2 rb[4];
-            if (p.res) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    rb[i] = *reinterpret_cast<const uint2*>(p.res + (long)(m0 + wm * 64 + i * 16 + (lane & 15)) * p.ldc +
-                                                            nb + 4 * g);
-            }
+            const uint2* rb = rb_pre[j];
             uint32_t plo = 0, phi = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {

@@ -1,0 +1,9 @@
+#!/bin/bash
+# ResNet-50 steady-state kernel table (rocprofv3 kernel trace) -> gpurun_out/kernels_r50.md
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r50 -o run -- python3 bench.py --model resnet50 --steps 5 --warmup 3 > gpurun_out/prof_r50.log 2>&1 || exit $?
+python3 scripts/prof_summary.py gpurun_out/prof_r50/run_results.db --steps 5 --after sgd_k:3 --names "ResNet-50 bs256 (SGD), 1x MI355X, steady state" --top 45 > gpurun_out/kernels_r50.md
+rm -rf gpurun_out/prof_r50
+timeout -k 10 300 python scripts/debug/gemm_trace.py resnet50 --top 40 > gpurun_out/gemm_trace_r50.md 2> gpurun_out/gemm_trace_r50.err || { tail -20 gpurun_out/gemm_trace_r50.err; exit 1; }
