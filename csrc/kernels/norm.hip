@@ -789,13 +789,13 @@ DDL_API int ddl_ln_fwd(int dtype, const void* x, const void* res, long res_rows,
     DDL_RETURN_LAUNCH();
 }
 
-// rows per block (DDL_LN_BWD_ROWS, default 16) and block cap (DDL_LN_BWD_MAXBLK, default 1024)
+// rows per block (DDL_LN_BWD_ROWS, default 32: +0.6% BERT-base over 16, 64 -2%) and block cap (DDL_LN_BWD_MAXBLK, default 1024)
 static int ln_env(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && atoi(v) > 0 ? atoi(v) : dflt;
 }
 DDL_API int ddl_ln_bwd_nblk(long rows) {
-    static const int rpb = ln_env("DDL_LN_BWD_ROWS", 16), cap = ln_env("DDL_LN_BWD_MAXBLK", 1024);
+    static const int rpb = ln_env("DDL_LN_BWD_ROWS", 32), cap = ln_env("DDL_LN_BWD_MAXBLK", 1024);
     return (int)std::max<long>(1, std::min<long>(cap, (rows + rpb - 1) / rpb));
 }
 
