@@ -72,6 +72,39 @@ def _direct3x3(x, w, y, part=None, res=None, bnb=None, grid=0):
     return rc
 
 
+_SKINNY = os.environ.get("DDL_SKINNY", "1") != "0"
+
+
+def _skinny(a, b, c, part=None, res=None, bnb=None):
+    """c[M, N] = a[M, K] b[N, K]^T by the streaming kernel (csrc/kernels/skinny_gemm.hip) when
+    it covers the shape -- (N, K) = (256, 64) or (64, 256), bf16, contiguous, residual only
+    for N = 256, BN-backward epilogue only for N = 64.  Returns the statistics rows written,
+    or None when not covered (nothing launched)."""
+    if not (_SKINNY and a.is_cuda):
+        return None
+    M, K = a.shape
+    N = b.shape[0]
+    if (N, K) not in ((256, 64), (64, 256)) or tuple(c.shape) != (M, N) or b.shape[1] != K:
+        return None
+    ts = [a, b, c] + ([res] if res is not None else []) + ([bnb.x] if bnb is not None else [])
+    if any(t.dtype != torch.bfloat16 or not t.is_contiguous() for t in ts):
+        return None
+    if (res is not None and (N != 256 or bnb is not None)) or (bnb is not None and N != 64):
+        return None
+    if res is not None and tuple(res.shape) != (M, N) or bnb is not None and bnb.x.numel() != M * N:
+        return None
+    if part is not None and part.numel() < 1024 * 2 * N:
+        return None
+    args = (_lib.p(bnb.x), _lib.p(bnb.mask), _lib.p(bnb.mean), _lib.p(bnb.istd)) if bnb is not None else (0, 0, 0, 0)
+    rc = _lib.fn("ddl_skinny_gemm")(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, _lib.p(part), _lib.p(res),
+                                    *args, 0, _lib.stream())
+    if rc == -1:
+        return None
+    if rc < 0:
+        raise RuntimeError(f"ddl_skinny_gemm failed: {rc}")
+    return rc
+
+
 def _direct3x3_rows(M):
     return max(stats_rows_max(M), 256)
 
@@ -114,6 +147,14 @@ def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
         if use:
             part = torch.empty(stats_rows_max(M) * 2 * K, dtype=torch.float32, device=x.device)
             kernel = None if R * S * C >= STATS_MIN_K else "big"
+    if plain11 and bias is None and act is None and residual is None and x.is_cuda:
+        sk_part = torch.empty(max(stats_rows_max(M), 1024) * 2 * K, dtype=torch.float32, device=x.device) \
+            if part is not None else None
+        rows = _skinny(x.view(M, C), w.view(K, C), y.view(M, K), part=sk_part)
+        if rows is not None:
+            if part is not None:
+                stats.set(y, sk_part, rows)
+            return y
     if plain11:
         r = gemm(MODE_NT, x, C, w, C, y, K, M, K, C, bias=bias, act=act, residual=residual, colstats=part,
                  kernel=kernel)
@@ -166,6 +207,18 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
         if _DGRAD_NT:   # NT against W^T (k-contiguous operands; the weight copy is tiny)
             wt = _w_dgrad(w, [0], [0]).view(C, K)
+            M = N * H * W_
+            # the streaming kernel first (ResNet stage-1 shapes), then the general GEMMs
+            res2 = residual.view(M, C) if residual is not None else None
+            if bnb is not None:
+                part = torch.empty(max(stats_rows_max(M), 1024) * 2 * C + 64 * C, dtype=torch.float32,
+                                   device=dx.device)
+                rows = _skinny(dy.view(M, K), wt, dx.view(M, C), part=part, res=res2, bnb=bnb)
+                if rows is not None:
+                    bnb.set(dx, part, rows)
+                    return dx
+            elif _skinny(dy.view(M, K), wt, dx.view(M, C), res=res2) is not None:
+                return dx
             if bnb is None or not _bnb_dgrad(MODE_NT, dy, K, wt, K, dx, N * H * W_, C, K, None, residual, bnb):
                 gemm(MODE_NT, dy, K, wt, K, dx, C, N * H * W_, C, K, residual=residual)
         else:
