@@ -26,6 +26,8 @@
 // mod 8) walk neighbouring tiles (bijective remap, §5.5 T1).
 #include "ddl_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
@@ -80,6 +82,7 @@ struct Params {
     const float* bn_istd;
     ConvDesc cd;
     int tiles_m, tiles_n;
+    int stage_out;      // wide plain-bf16 tiles leave through LDS as whole rows (DDL_GEMM_STAGE_OUT)
 };
 
 // Loads are unconditional from a clamped (always valid) address and the VALUE is
@@ -576,7 +579,11 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
         }
     }
     if (wide_plain) {
-        // bf16 (+ residual, loaded up front) (+ BatchNorm statistics of the stored values), pair stores
+        // bf16 (+ residual, loaded up front) (+ BatchNorm statistics of the stored values).
+        // stage_out: the tile goes through LDS (the operand stages are free after the last
+        // K-step's barrier) and out as whole rows -- a pair store writes 32 rows x 32 B per
+        // instruction, a row store 1 KB of 4 (or 8) contiguous rows
+        constexpr int RB = BNT * 2, CH16 = RB / 16;            // staging row bytes, 16-B chunks per row
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int nb = n0 + wn * WN + j * 16;
@@ -592,8 +599,16 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
                     v[3] += __uint_as_float(rb[i].y & 0xffff0000u);
                 }
                 const uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
-                if ((i & 1) == 0) { plo = lo; phi = hi; }
-                else store_pair((bf16_t*)p.C, plo, phi, lo, hi, m0 + wm * 64 + (i - 1) * 16 + (lane & 15), nb);
+                if (p.stage_out) {
+                    const int row = wm * 64 + i * 16 + (lane & 15), c = (wn * WN + j * 16) / 8 + (g >> 1);
+                    *reinterpret_cast<uint2*>(smem + row * RB + ((c ^ (row & (CH16 - 1))) << 4) + (g & 1) * 8) =
+                        make_uint2(lo, hi);
+                } else if ((i & 1) == 0) {
+                    plo = lo;
+                    phi = hi;
+                } else {
+                    store_pair((bf16_t*)p.C, plo, phi, lo, hi, m0 + wm * 64 + (i - 1) * 16 + (lane & 15), nb);
+                }
                 if (p.colstats) {
                     const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                         __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
@@ -603,6 +618,16 @@ __device__ __forceinline__ void gemm_body(const Params& p, char* smem) {
                         st_q[j][r] += t[r] * t[r];
                     }
                 }
+            }
+        }
+        if (p.stage_out) {
+            __syncthreads();
+            constexpr int RPI = 1024 / RB;                     // rows per store instruction
+#pragma unroll
+            for (int q = 0; q < BM * RB / 1024 / 4; ++q) {
+                const int row = (q * 4 + w) * RPI + lane / CH16, c = lane % CH16;
+                const uint4 d = *reinterpret_cast<const uint4*>(smem + row * RB + ((c ^ (row & (CH16 - 1))) << 4));
+                *reinterpret_cast<uint4*>((bf16_t*)p.C + (long)(m0 + row) * p.ldc + n0 + c * 8) = d;
             }
         }
     }
@@ -1054,6 +1079,8 @@ static int gemm_entry(int narrow, int mode, const void* A, long lda, const void*
     mode &= 15;
     if (p.trans_out && (bias || act || res || row_remap)) return -5;
     p.colstats = colstats;
+    static const int stage_out = getenv("DDL_GEMM_STAGE_OUT") ? atoi(getenv("DDL_GEMM_STAGE_OUT")) : 1;
+    p.stage_out = stage_out;
     if (act == ACT_BNB) {
         const BnbArgs bn = ddl_take_bnb();
         // whole-K tiles writing a dense bf16 [M, C] gradient: the mask is indexed by element
