@@ -499,11 +499,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
 // (the tiled forward stages them once per 64-query workgroup), wave w owns queries
 // 16w..16w+15 with every key's score in registers, so the softmax needs no online
 // rescaling: one max, one exponential per score, one sum.
+// FULL: S == 128 (every score block valid: no per-block branches, so the compiler can
+// interleave one block's fragment reads with the previous block's MFMAs); MASK / DROP:
+// key-padding mask / probability dropout present (uniform per launch)
+template <bool FULL, bool MASK, bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restrict__ qkv,
                                                             const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse, int S, int H, float scale,
                                                             float p_drop, uint64_t seed) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * FS * ROWB];   // K (row image), V (transposed-read image)
+    // K (row image), V (transposed-read image), the key-padding mask row (additive, fp32)
+    __shared__ __attribute__((aligned(16))) char smem[2 * FS * ROWB + FS * 4];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -532,12 +537,18 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
         qf[1] = load_frag_global(qr, 1);
     }
     const float c2 = scale * LOG2E;
-    const float* mrow = mask ? mask + (long)b * S : nullptr;
+    const float* mrow = MASK ? mask + (long)b * S : nullptr;
+    // the mask row goes through LDS with K and V: read per score block from global, its
+    // loads sat between the QK MFMAs and the softmax, each waited for on its own
+    float* sM = reinterpret_cast<float*>(smem + 2 * FS * ROWB);
+    if (MASK && tid < FS) sM[tid] = tid < S ? mrow[tid] : 0.f;
     __syncthreads();
-    const int nblk = (S + 15) / 16;
+    const int nblk = FULL ? 8 : (S + 15) / 16;
     // S^T blocks: lane holds s[blk][r] = score(q = myq, k = 16 blk + 4 g + r)
     f32x4 s[8];
     float mx = -INFINITY;
+    // all QK^T MFMAs first (fragment reads only), then the scale / mask / max pass: the
+    // softmax math no longer waits on each block's MFMA result in turn
 #pragma unroll
     for (int blk = 0; blk < 8; ++blk) {
         s[blk] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -546,13 +557,17 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
             for (int kk = 0; kk < 2; ++kk)
                 s[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sK, 16 * blk, kk), qf[kk], s[blk], 0, 0, 0);
         }
+    }
+#pragma unroll
+    for (int blk = 0; blk < 8; ++blk) {
         const int k0 = 16 * blk + 4 * g;
-        float mk[4] = {0.f, 0.f, 0.f, 0.f};
-        if (mrow && blk < nblk) mask4(mrow, k0, S, mk);
-        const bool edge = 16 * blk + 16 > S;          // uniform: this block reaches past S
+        float4 mk = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MASK) mk = *reinterpret_cast<const float4*>(sM + k0);
+        const float mka[4] = {mk.x, mk.y, mk.z, mk.w};
+        const bool edge = !FULL && 16 * blk + 16 > S;   // uniform: this block reaches past S
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float v = mrow ? s[blk][r] * c2 + mk[r] * LOG2E : s[blk][r] * c2;
+            float v = MASK ? s[blk][r] * c2 + mka[r] * LOG2E : s[blk][r] * c2;
             if (edge && k0 + r >= S) v = -INFINITY;
             s[blk][r] = v;
             mx = fmaxf(mx, v);
@@ -568,12 +583,12 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
 #pragma unroll
     for (int blk = 0; blk < 8; ++blk) {
         bool keep[4] = {true, true, true, true};
-        if (p_drop > 0.f && blk < nblk) attn_keep4(seed, rowidx + 16 * blk + 4 * g, thresh, S & 1, keep);
+        if (DROP && blk < nblk) attn_keep4(seed, rowidx + 16 * blk + 4 * g, thresh, !FULL && (S & 1), keep);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float pv = fast_exp2(s[blk][r] - msub);
             lsum += pv;
-            if (p_drop > 0.f) pv = keep[r] ? pv * inv_keep : 0.f;
+            if (DROP) pv = keep[r] ? pv * inv_keep : 0.f;
             s[blk][r] = pv;
         }
     }
@@ -614,6 +629,8 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
 //           images and K, both read transposed.
 // Every input byte is read once and nothing is recomputed (the two-kernel path re-derives
 // P and dP in both its dK/dV and its dQ kernel and reads Q/K/V/dO once per tile pair).
+// FULL: S == 128 (the query / key chunk loops unroll, no bounds checks); DROP: dropout on
+template <bool FULL, bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restrict__ qkv,
                                                             const bf16_t* __restrict__ out,
                                                             const bf16_t* __restrict__ dout,
@@ -698,8 +715,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
         f32x4 dv[4], dk[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
-        const int nqc = (S + 31) / 32;
-        for (int qc = 0; qc < nqc; ++qc) {
+        const int nqc = FULL ? 4 : (S + 31) / 32;
+#pragma unroll
+        for (int qc = 0; qc < 4; ++qc) {
+            if (!FULL && qc >= nqc) break;
             f32x4 sc[2], dp[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -723,10 +742,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int ql = q0 + r;
-                    const float pv = (ql < S && kok) ? fast_exp2(sc[j][r] * c2 + (mb2 - lse4[r])) : 0.f;
+                    const float pv = (FULL || (ql < S && kok)) ? fast_exp2(sc[j][r] * c2 + (mb2 - lse4[r])) : 0.f;
                     float dpv = dp[j][r];
                     float pdrop = pv;
-                    if (p_drop > 0.f) {
+                    if (DROP) {
                         const bool keep = attn_keep_half(attn_hash(seed, idx >> 1), idx, thresh);
                         pdrop = keep ? pv * inv_keep : 0.f;
                         dpv = keep ? dpv * inv_keep : 0.f;
@@ -736,9 +755,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                     ds[j][r] = pv * (dpv - del4[r]);
                 }
                 // dS^T row myk, query columns 32qc + 16j + 4g .. +3 (written after phase 1)
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (c == qc) dsk[2 * c + j] = make_uint2(pack2bf(ds[j][0], ds[j][1]), pack2bf(ds[j][2], ds[j][3]));
+                dsk[2 * qc + j] = make_uint2(pack2bf(ds[j][0], ds[j][1]), pack2bf(ds[j][2], ds[j][3]));
             }
             // dV^T[d][k] += dO^T[d][q] Pd[q][k];  dK^T[d][k] += Q^T[d][q] dS[q][k]
             const bf16x8 pf = pack_acc(pd[0], pd[1]);
@@ -786,8 +803,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
         f32x4 dq[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
-        const int nkc = (S + 31) / 32;
-        for (int st = 0; st < nkc; ++st) {
+        const int nkc = FULL ? 4 : (S + 31) / 32;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            if (!FULL && st >= nkc) break;
             const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
 #pragma unroll
             for (int db = 0; db < 4; ++db)
@@ -820,7 +839,16 @@ bool fused_bwd_enabled() {
 DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int S, int H, float scale,
                          float p_drop, uint64_t seed, hipStream_t st) {
     if (S <= FS && fused_bwd_enabled()) {
-        attn_fwd_short_k<<<B * H, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed);
+        const bool full = S == FS, msk = mask != nullptr, drp = p_drop > 0.f;
+#define FWD_SHORT(F, M, D) attn_fwd_short_k<F, M, D><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed)
+        if (full) {
+            if (msk) { if (drp) FWD_SHORT(true, true, true); else FWD_SHORT(true, true, false); }
+            else { if (drp) FWD_SHORT(true, false, true); else FWD_SHORT(true, false, false); }
+        } else {
+            if (msk) { if (drp) FWD_SHORT(false, true, true); else FWD_SHORT(false, true, false); }
+            else { if (drp) FWD_SHORT(false, false, true); else FWD_SHORT(false, false, false); }
+        }
+#undef FWD_SHORT
         DDL_RETURN_LAUNCH();
     }
     dim3 grid((S + TQ - 1) / TQ, B * H);
@@ -833,8 +861,11 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
                          float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop, uint64_t seed,
                          hipStream_t st) {
     if (S <= FS && fused_bwd_enabled()) {   // the whole sequence fits one workgroup's LDS
-        attn_bwd_fused_k<<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, (const bf16_t*)dout, lse,
-                                                mask, (bf16_t*)dqkv, S, H, scale, p_drop, seed);
+#define BWD_FUSED(F, DR) attn_bwd_fused_k<F, DR><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, \
+        (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, seed)
+        if (S == FS) { if (p_drop > 0.f) BWD_FUSED(true, true); else BWD_FUSED(true, false); }
+        else { if (p_drop > 0.f) BWD_FUSED(false, true); else BWD_FUSED(false, false); }
+#undef BWD_FUSED
         DDL_RETURN_LAUNCH();
     }
     const long rows = (long)B * S * H;
