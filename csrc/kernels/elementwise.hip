@@ -545,6 +545,62 @@ DDL_API int ddl_conv_w_dgrad(const void* w, void* out, int K, int R, int S, int 
     DDL_RETURN_LAUNCH();
 }
 
+// Every conv's dgrad weight layout of one optimizer step in ONE launch (ResNet-50: 61
+// re-layouts of 2-600 KB each were 61 launch-latency-bound kernels, ~0.3 ms per step).
+// Job table in device memory, WJ_FIELDS int64 per job:
+//   [w, out, K, R, S, C, Rp, Sp, gk, gc, block0, r[8], s[8]]
+// gk / gc: 32-wide k / c tiles; block0: first flat block of the job (ascending).
+constexpr int WJ_FIELDS = 27;
+__global__ __launch_bounds__(256) void conv_w_dgrad_batch_k(const int64_t* __restrict__ tab, int njobs) {
+    __shared__ bf16_t tile[32][33];
+    const long b = blockIdx.x;
+    int lo = 0, hi = njobs - 1;          // last job with block0 <= b
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[mid * WJ_FIELDS + 10] <= b) lo = mid; else hi = mid - 1;
+    }
+    const int64_t* j = tab + lo * WJ_FIELDS;
+    const bf16_t* w = (const bf16_t*)j[0];
+    bf16_t* out = (bf16_t*)j[1];
+    const int K = (int)j[2], R = (int)j[3], S = (int)j[4], C = (int)j[5], Sp = (int)j[7];
+    const int Rp = (int)j[6], gk = (int)j[8], gc = (int)j[9];
+    const int loc = (int)(b - j[10]);
+    const int tap = loc / (gk * gc), rem = loc - tap * gk * gc;
+    const int k0 = (rem % gk) * 32, c0 = (rem / gk) * 32;
+    const int rp = tap / Sp, sp = tap - rp * Sp;
+    const int r = (int)j[11 + rp], s_ = (int)j[19 + sp];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = k0 + ty + 8 * i, c = c0 + tx;
+        if (k < K && c < C) tile[ty + 8 * i][tx] = w[((k * R + r) * S + s_) * C + c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = c0 + ty + 8 * i, k = k0 + tx;
+        if (k < K && c < C) out[((c * Rp + rp) * Sp + sp) * K + k] = tile[tx][ty + 8 * i];
+    }
+}
+
+// tab: device copy of the job table; host_tab: the same table on the host (validated here)
+DDL_API int ddl_conv_w_dgrad_batch(const int64_t* tab, const int64_t* host_tab, int njobs, hipStream_t st) {
+    if (njobs <= 0) return 0;
+    long total = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const int64_t* j = host_tab + (long)i * WJ_FIELDS;
+        const long K = j[2], R = j[3], S = j[4], C = j[5], Rp = j[6], Sp = j[7];
+        if (Rp > 8 || Sp > 8 || Rp < 1 || Sp < 1 || K * R * S * C >= (1L << 31)) return -1;
+        if (j[8] != (K + 31) / 32 || j[9] != (C + 31) / 32 || j[10] != total) return -2;
+        for (int t = 0; t < Rp; ++t) if (j[11 + t] < 0 || j[11 + t] >= R) return -3;
+        for (int t = 0; t < Sp; ++t) if (j[19 + t] < 0 || j[19 + t] >= S) return -3;
+        total += j[8] * j[9] * Rp * Sp;
+    }
+    if (total >= (1L << 31)) return -4;
+    conv_w_dgrad_batch_k<<<(unsigned)total, 256, 0, st>>>(tab, njobs);
+    DDL_RETURN_LAUNCH();
+}
+
 DDL_API int ddl_acc_f32(int dtype, void* dst, const float* src, long n, hipStream_t st) {
     const int g = (int)std::min<long>(1024, (n + 255) / 256);
     DISPATCH_T(dtype, (acc_f32_k<bf16_t><<<g, 256, 0, st>>>((bf16_t*)dst, src, n)),

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
 template <typename TP>
 __global__ __launch_bounds__(1024) void colsum_partials_k(const float* __restrict__ part, int nblk, int H,
                                                           TP* __restrict__ dg, TP* __restrict__ db, int acc,
-                                                          float* __restrict__ dxsum) {
+                                                          float* __restrict__ dxsum, TP* __restrict__ dxsink) {
     __shared__ float red[1024];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     const long stride = (dxsum ? 3L : 2L) * H;
@@ -534,6 +534,8 @@ __global__ __launch_bounds__(1024) void colsum_partials_k(const float* __restric
     dg[c] = from_f<TP>(a + (acc ? to_f(dg[c]) : 0.f));
     db[c] = from_f<TP>(b + (acc ? to_f(db[c]) : 0.f));
     if (dxsum) dxsum[c] = d;
+    // the producing Linear's bias gradient, accumulated straight into its arena slot
+    if (dxsink) dxsink[c] = from_f<TP>(d + (acc ? to_f(dxsink[c]) : 0.f));
 }
 
 inline int grid_for(long n, int nt = 256, int cap = 4096) {
@@ -802,7 +804,7 @@ DDL_API int ddl_ln_bwd_nblk(long rows) {
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
                            const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, int acc,
-                           float* dxsum, Drop drop, hipStream_t st) {
+                           float* dxsum, T* dxsink, Drop drop, hipStream_t st) {
     const int nblk = ddl_ln_bwd_nblk(rows);
     const int rpb = (int)((rows + nblk - 1) / nblk);
     switch (H / 256) {
@@ -817,7 +819,7 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
     }
     int nrows = nblk;
     const float* fin = collapse_partials(part, nrows, (dxsum ? 3 : 2) * H, st);
-    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(fin, nrows, H, dg, db, acc, dxsum);
+    colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(fin, nrows, H, dg, db, acc, dxsum, dxsink);
     return 0;
 }
 
@@ -825,21 +827,25 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
 // collapse); dxsum (nullable, fp32 [H]) receives the
 // column sums of dx -- the bias gradient of the Linear feeding this LayerNorm
 // drop_p > 0: dx = gradient of x through the dropout mask, dres (required) = the
-// unmasked gradient of (dropout(x) + res); dxsum then sums the masked dx
+// unmasked gradient of (dropout(x) + res); dxsum then sums the masked dx.
+// dxsink (nullable, dtype of dg): the same column sums also added to (acc_params) or
+// stored in that Linear's bias gradient -- needs dxsum
 DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res, long res_rows, const void* g,
                        const float* mean, const float* rstd, void* dx, float* part, void* dg, void* db, long rows, int H,
                        int acc_params, float* dxsum, unsigned long long drop_seed, float drop_p, void* dres,
-                       hipStream_t st) {
+                       void* dxsink, hipStream_t st) {
     if (!ddl_ln_supported(H)) return -1;
     if (res_rows <= 0) res_rows = rows;
     if (drop_p > 0.f && (!dres || res_rows != rows)) return -2;
+    if (dxsink && !dxsum) return -3;
     const Drop drop = make_drop(drop_seed, drop_p, dres);
     int rc = dtype == 1
                  ? ln_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
                                    mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, dxsum,
-                                   drop, st)
+                                   (bf16_t*)dxsink, drop, st)
                  : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
-                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum, drop, st);
+                                   rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum,
+                                   (float*)dxsink, drop, st);
     if (rc) return rc;
     DDL_RETURN_LAUNCH();
 }
@@ -856,7 +862,27 @@ __global__ __launch_bounds__(1024) void rows_sum_k(const float* __restrict__ par
     const float s = colsum64(part, nrows, width, c, c < width, red);
     if (threadIdx.x < 64 && c < width) out[c] = s;
 }
+// sink[c] (+)= sum_r part[r][c] for c < n (row stride `width`): a column sum straight into a
+// parameter's gradient slot (bf16 / fp32), no fp32 row + accumulate launch
+template <typename TP>
+__global__ __launch_bounds__(1024) void rows_sum_sink_k(const float* __restrict__ part, int nrows, int width, int n,
+                                                        TP* __restrict__ sink, int acc) {
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const float s = colsum64(part, nrows, width, c, c < n, red);
+    if (threadIdx.x < 64 && c < n) sink[c] = from_f<TP>(s + (acc ? to_f(sink[c]) : 0.f));
+}
 }  // namespace
+
+DDL_API int ddl_rows_sum_sink(int dtype, const float* part, int nblk, int width, int n, void* sink, int acc,
+                              float* ws, hipStream_t st) {
+    if (n > width) return -1;
+    int nrows = nblk;
+    const float* src = collapse_partials(part, nrows, width, st, ws);
+    if (dtype == 1) rows_sum_sink_k<bf16_t><<<(n + 63) / 64, 1024, 0, st>>>(src, nrows, width, n, (bf16_t*)sink, acc);
+    else rows_sum_sink_k<float><<<(n + 63) / 64, 1024, 0, st>>>(src, nrows, width, n, (float*)sink, acc);
+    DDL_RETURN_LAUNCH();
+}
 
 // out[c] = sum_r part[r][c]; ws (ceil(nblk/32) * width floats) may be null when part
 // itself holds (nblk + ceil(nblk/32)) * width floats

@@ -110,6 +110,7 @@ _SIGS = {
     "ddl_bn_stats_nblk": [L, I],
     "ddl_bn_bwd_nblk": [L, I],
     "ddl_bn_rows_sum": [P, I, I, P, P, P],
+    "ddl_rows_sum_sink": [I, P, I, I, I, P, I, P, P],
     "ddl_bn_stats_partials": [I, P, L, I, P, P],
     "ddl_bn_bwd_partials": [I, P, P, P, P, P, L, I, I, P, P],
     "ddl_bn_bwd_finish": [I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P, P, P, I, P],
@@ -120,6 +121,7 @@ _SIGS = {
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P, P],
     "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P, L],
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
+    "ddl_conv_w_dgrad_batch": [P, P, I, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
     "ddl_acc_f32": [I, P, P, L, P],
     "ddl_softmax_topk": [I, P, L, I, I, P, P, P, P],
@@ -131,7 +133,7 @@ _SIGS = {
     "ddl_ln_supported": [I],
     "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, U64, F, P],
     "ddl_ln_bwd_nblk": [L],
-    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P, U64, F, P, P],
+    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P, U64, F, P, P, P],
     # elementwise.hip
     "ddl_gelu_fwd": [I, P, P, L, P],
     "ddl_gelu_bwd": [I, P, P, P, L, P],

@@ -166,10 +166,81 @@ def _fwd(x, w, stride, pad, bias=None, act=None, residual=None, stats=None):
     return y
 
 
-def _w_dgrad(w, rs, ss):
+class _WDgradCache:
+    """Every conv's dgrad weight layout of an optimizer step in one launch.
+
+    The layouts depend only on the weights, which change once per optimizer step (the
+    arena's ``generation``).  The first dgrad after a step re-lays-out every weight this
+    cache has seen (``ddl_conv_w_dgrad_batch``: one launch instead of one per conv and
+    parity class -- 61 per ResNet-50 step); the others find their layout ready.  A job is
+    valid for the (generation, weight version) it was filled at, so in-place torch updates
+    of a weight (which bump ``_version``, not the generation) still re-lay it out."""
+
+    def __init__(self):
+        self.jobs = {}          # key -> [w, rs, ss, out, filled_at]
+        self.gen = None
+        self.table = None       # (device int64 table, host copy, njobs)
+
+    def _build(self):
+        rows, blk = [], 0
+        for w, rs, ss, out, _ in self.jobs.values():
+            K, R, S, C = w.shape
+            gk, gc = (K + 31) // 32, (C + 31) // 32
+            r8 = list(rs) + [0] * (8 - len(rs))
+            s8 = list(ss) + [0] * (8 - len(ss))
+            rows.append([w.data_ptr(), out.data_ptr(), K, R, S, C, len(rs), len(ss), gk, gc, blk] + r8 + s8)
+            blk += gk * gc * len(rs) * len(ss)
+        host = torch.tensor(rows, dtype=torch.int64)
+        self.table = (host.to(next(iter(self.jobs.values()))[0].device), host, len(rows))
+
+    def get(self, w, rs, ss, generation):
+        key = (w.data_ptr(), tuple(w.shape), tuple(rs), tuple(ss))
+        if generation != self.gen:
+            self.gen = generation
+            if self.jobs:
+                if self.table is None:
+                    self._build()
+                dev, host, n = self.table
+                rc = _lib.fn("ddl_conv_w_dgrad_batch")(dev.data_ptr(), host.data_ptr(), n, _lib.stream())
+                if rc != 0:
+                    raise RuntimeError(f"ddl_conv_w_dgrad_batch failed: {rc}")
+                for job in self.jobs.values():
+                    job[4] = (generation, job[0]._version)
+        job = self.jobs.get(key)
+        stamp = (generation, w._version)
+        if job is not None and job[4] == stamp:
+            return job[3]
+        if job is None:
+            job = [w, tuple(rs), tuple(ss), None, None]
+            self.jobs[key] = job
+            self.table = None
+        job[3] = _w_dgrad_once(w, rs, ss, job[3])
+        job[4] = stamp
+        return job[3]
+
+
+_WDG_BATCH = os.environ.get("DDL_WDG_BATCH", "1") != "0"
+
+
+def _w_dgrad(w, rs, ss, param=None):
+    """[C, len(rs), len(ss), K] = w[:, rs][:, :, ss] transposed.  With ``param`` (the
+    arena parameter ``w`` is) the layout comes from the arena's per-step batch."""
+    ref = getattr(param, "_ddl_arena", None) if param is not None else None
+    arena = ref() if ref is not None else None
+    if _WDG_BATCH and arena is not None and param.data_ptr() == w.data_ptr() and w.is_cuda \
+            and not torch.cuda.is_current_stream_capturing():
+        cache = getattr(arena, "_ddl_wdg", None)
+        if cache is None:
+            cache = arena._ddl_wdg = _WDgradCache()
+        return cache.get(w, rs, ss, arena.generation)
+    return _w_dgrad_once(w, rs, ss)
+
+
+def _w_dgrad_once(w, rs, ss, out=None):
     """[C, len(rs), len(ss), K] = w[:, rs][:, :, ss] transposed, in one native launch."""
     K, R, S, C = w.shape
-    out = torch.empty(C, len(rs), len(ss), K, dtype=w.dtype, device=w.device)
+    if out is None:
+        out = torch.empty(C, len(rs), len(ss), K, dtype=w.dtype, device=w.device)
     ra = (ctypes.c_int * len(rs))(*rs)
     sa = (ctypes.c_int * len(ss))(*ss)
     rc = _lib.fn("ddl_conv_w_dgrad")(w.data_ptr(), out.data_ptr(), K, R, S, C, len(rs), len(ss), ra, sa,
@@ -195,7 +266,7 @@ def _bnb_dgrad(mode, dy, lda, wt, ldb, dx, M, C, K, conv, residual, hint):
     return True
 
 
-def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
+def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None, param=None):
     """dx (+ ``residual``, added in the GEMM epilogue; strided convs add it in place,
     so there ``residual`` must be a tensor the caller owns)."""
     N, H, W_, C = x_shape
@@ -206,7 +277,7 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
     if R == 1 and S == 1 and stride == 1 and pad == 0:
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
         if _DGRAD_NT:   # NT against W^T (k-contiguous operands; the weight copy is tiny)
-            wt = _w_dgrad(w, [0], [0]).view(C, K)
+            wt = _w_dgrad(w, [0], [0], param).view(C, K)
             M = N * H * W_
             # the streaming kernel first (ResNet stage-1 shapes), then the general GEMMs
             res2 = residual.view(M, C) if residual is not None else None
@@ -217,6 +288,10 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
                 if rows is not None:
                     bnb.set(dx, part, rows)
                     return dx
+                # residual-adding stage-1 dgrads (N = 256): the streaming kernel without the
+                # BN-backward epilogue beats the general GEMM with it
+                if res2 is not None and _skinny(dy.view(M, K), wt, dx.view(M, C), res=res2) is not None:
+                    return dx
             elif _skinny(dy.view(M, K), wt, dx.view(M, C), res=res2) is not None:
                 return dx
             if bnb is None or not _bnb_dgrad(MODE_NT, dy, K, wt, K, dx, N * H * W_, C, K, None, residual, bnb):
@@ -225,7 +300,7 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
             gemm(MODE_NN, dy, K, w, C, dx, C, N * H * W_, C, K, residual=residual)
         return dx
     if stride == 1:
-        wt = _w_dgrad(w, list(range(R - 1, -1, -1)), list(range(S - 1, -1, -1)))   # flipped [C, R, S, K]
+        wt = _w_dgrad(w, list(range(R - 1, -1, -1)), list(range(S - 1, -1, -1)), param)   # flipped [C, R, S, K]
         dx = torch.empty(N, H, W_, C, dtype=dy.dtype, device=dy.device)
         if dy.is_cuda and _direct3x3_ok(dy.shape, wt.shape, 1, pad) and (bnb is not None or residual is None):
             # the direct kernel (a stride-1 3x3 dgrad is the same convolution of dy)
@@ -262,7 +337,7 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None):
         dx = (torch.zeros if empty else torch.empty)(N, H, W_, C, dtype=dy.dtype, device=dy.device)
     probs = []
     for a, b, rs, ss, Ho, Wo in classes:
-        wc = _w_dgrad(w, rs, ss)                                     # [C, R', S', K]
+        wc = _w_dgrad(w, rs, ss, param)                                   # [C, R', S', K]
         h_off = (a + pad - rs[0]) // stride
         w_off = (b + pad - ss[0]) // stride
         Rp, Sp = len(rs), len(ss)
@@ -384,7 +459,7 @@ class _Conv(torch.autograd.Function):
             res = ctx.bridge.take() if ctx.bridge is not None else None
             if res is not None:
                 res = res.contiguous().view(x.shape)
-            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad, residual=res, bnb=ctx.bnb)
+            dx = _dgrad(dy, w, x.shape, ctx.stride, ctx.pad, residual=res, bnb=ctx.bnb, param=ctx.w_param)
             ctx.bnb = None
             if ctx.grad_to is not None and ctx.grad_to.offer(dx):
                 dx = None       # the sibling conv's dgrad epilogue adds it

@@ -82,6 +82,10 @@ class _Linear(torch.autograd.Function):
         if z is not None:
             ctx.gelu_token = object()
             out._ddl_gelu_pre = (z, ctx.gelu_token)
+        elif b is not None and act is None:
+            # a LayerNorm consuming ``out`` may add the column sums of its input gradient
+            # (this bias's gradient) straight into the bias's arena slot
+            out._ddl_bias_param = b
         return out
 
     @staticmethod
@@ -169,8 +173,21 @@ class _Linear(torch.autograd.Function):
             else:
                 dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
                 gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
+        sunk = getattr(ctx.b_param, "_ddl_sunk", None) if ctx.has_bias else None
+        if sunk is not None:
+            ctx.b_param._ddl_sunk = None
         if bias_done:
             db = db_ret
+        elif sunk is not None and ctx.needs_input_grad[2]:
+            # a LayerNorm backward already added its input gradient's column sums to the bias
+            # gradient; if dy is not exactly that gradient (autograd summed another branch in),
+            # add the full column sums and take the LayerNorm's share back out
+            pre = getattr(dy, "_ddl_colsum", None)
+            if ctx.act is not None or pre is None or pre[0] is not sunk or pre[1] != dy._version:
+                sink = grad_sink(ctx.b_param)
+                E.colsum(dz, sink, accumulate=True)
+                sink.copy_(sink.float() - sunk)
+            grad_ready(ctx.b_param)
         elif ctx.has_bias and ctx.needs_input_grad[2]:
             sink = grad_sink(ctx.b_param)
             # a LayerNorm backward that produced dy already summed its columns
@@ -209,14 +226,15 @@ class _DgeluHandoff:
         self.token, self.part, self.nrows, self.width, self.version = token, part, nrows, width, -1
 
     def bias_grad(self, b_param, N: int):
-        row = torch.empty(2 * self.width, dtype=torch.float32, device=self.part.device)
         ws = torch.empty(-(-self.nrows // 32) * 2 * self.width, dtype=torch.float32, device=self.part.device)
-        call("ddl_bn_rows_sum", p(self.part), self.nrows, 2 * self.width, p(row), p(ws))
         sink = grad_sink(b_param)
         if sink is not None:
-            call("ddl_acc_f32", dcode(sink), p(sink), p(row), N)
+            # column sums accumulated straight into the bias's gradient slot
+            call("ddl_rows_sum_sink", dcode(sink), p(self.part), self.nrows, 2 * self.width, N, p(sink), 1, p(ws))
             grad_ready(b_param)
             return None
+        row = torch.empty(2 * self.width, dtype=torch.float32, device=self.part.device)
+        call("ddl_bn_rows_sum", p(self.part), self.nrows, 2 * self.width, p(row), p(ws))
         return row[:N].to(b_param.dtype)
 
 

@@ -12,11 +12,17 @@ from ._lib import call, dcode, grad_ready, grad_sink, p
 
 # BatchNorm backward reduction in the dgrad epilogue of the conv that consumes the BN
 # output (ops/bridge.py BNBackward); DDL_BN_BWD_EPI=0 keeps the separate partial pass
-_BN_BWD_EPI = os.environ.get("DDL_BN_BWD_EPI", "nores") != "0"
-# ... also when the dgrad adds a bridged residual gradient ("1"): three extra operand
-# streams per output site made those K=64..256 GEMMs slower than GEMM + partial pass
-# (profiles/bn_bwd_epilogue_ab.log, kernels_r50.md), so the default ("nores") skips them
-_BN_BWD_EPI_RES = os.environ.get("DDL_BN_BWD_EPI", "nores") not in ("0", "nores")
+_BN_BWD_EPI = os.environ.get("DDL_BN_BWD_EPI", "1") != "0"
+# ... also when the dgrad adds a bridged residual gradient ("1", default; "nores" skips
+# them): on its own the fused epilogue was neutral there (three extra operand streams per
+# output site, profiles/bn_bwd_epilogue_ab.log), but its output dz IS the residual gradient
+# the BN hands on, so the BN backward no longer writes a copy (+0.3-0.8 % ResNet-50)
+_BN_BWD_EPI_RES = os.environ.get("DDL_BN_BWD_EPI", "1") not in ("0", "nores")
+
+
+# LayerNorm backward adds its input gradient's column sums (the producing Linear's bias
+# gradient) straight into that bias's arena slot (DDL_LN_BIAS_SINK=0: the Linear adds them)
+_LN_BIAS_SINK = os.environ.get("DDL_LN_BIAS_SINK", "1") != "0"
 
 
 def _bn_supported(C: int) -> bool:
@@ -103,7 +109,6 @@ class _BatchNormTrain(torch.autograd.Function):
         part = torch.empty((nblk + -(-nblk // 32)) * 2 * C, **f32)
         coef = torch.empty(3 * C, **f32)
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
         sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
         direct = sg is not None and sb is not None
         if direct:
@@ -113,6 +118,7 @@ class _BatchNormTrain(torch.autograd.Function):
             dbeta = torch.empty_like(weight) if weight is not None else None
         given = ctx.bnb.take_for(dy) if ctx.bnb is not None else None
         ctx.bnb = None
+        dres = torch.empty_like(x) if ctx.has_res and (given is None or ctx.group is not None) else None
         if given is not None:
             # dy is dz (ReLU mask applied) and [sum dz | sum dz*xhat] came from the dgrad epilogue
             gpart, nrows = given
@@ -125,9 +131,13 @@ class _BatchNormTrain(torch.autograd.Function):
                      ctx.m_total, C, 0, p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
             else:
                 ws = gpart[nrows * 2 * C:]
+                # the residual gradient IS dz (mask applied, no affine): hand on the dgrad's
+                # output itself instead of copying it (one write pass per residual block)
                 call("ddl_bn_bwd_from_partials", dcode(x), p(gpart), nrows, p(ws), ws.numel(), p(dy), p(x),
-                     p(stats[0]), p(stats[1]), p(weight), M, C, p(dgamma), p(dbeta), p(coef), p(dx), p(dres),
+                     p(stats[0]), p(stats[1]), p(weight), M, C, p(dgamma), p(dbeta), p(coef), p(dx), None,
                      int(direct))
+                if ctx.has_res:
+                    dres = dy
         elif ctx.group is not None:
             # SyncBatchNorm: [sum dz | sum dz*xhat] summed over the group before the finalize
             call("ddl_bn_bwd_partials", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), M, C,
@@ -195,6 +205,8 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, e
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps, residual, drop_p, bridge=None):
+        # the bias of the Linear that produced x
+        ctx.bias_param = getattr(x, "_ddl_bias_param", None) if _LN_BIAS_SINK else None
         x = x.contiguous()
         H = x.shape[-1]
         rows = x.numel() // H
@@ -228,8 +240,16 @@ class _LayerNorm(torch.autograd.Function):
         dg, db = (sg, sb) if direct else (torch.empty_like(weight), torch.empty_like(weight))
         # with fused dropout the residual gets the unmasked gradient, x the masked one
         dres_buf = torch.empty_like(x) if ctx.drop_p > 0.0 else None
+        # the producing Linear's bias gradient (column sums of dx) straight into its arena slot
+        bsink = grad_sink(ctx.bias_param) if (direct and ctx.bias_param is not None) else None
+        if bsink is not None and (bsink.numel() != H or bsink.dtype != dg.dtype
+                                  or getattr(ctx.bias_param, "_ddl_sunk", None) is not None):
+            bsink = None
         call("ddl_ln_bwd", dcode(x), p(dy), p(x), p(res), ctx.res_rows, p(weight), p(stats[0]), p(stats[1]), p(dx),
-             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum), ctx.seed, ctx.drop_p, p(dres_buf))
+             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum), ctx.seed, ctx.drop_p, p(dres_buf), p(bsink))
+        if bsink is not None:
+            ctx.bias_param._ddl_sunk = dxsum     # the Linear's backward only marks it ready
+        ctx.bias_param = None
         # the column sums of dx ride along on the gradient tensor: the Linear whose output
         # fed this LayerNorm takes them as its bias gradient instead of re-reading dx
         # (the version guards against autograd accumulating another gradient into dx in place)

@@ -352,3 +352,84 @@ def test_linear_dgrad_uses_current_weights_after_flat_optimizer_steps(dgrad_nt, 
         want = dy.float() @ lin.weight.detach().float()
         assert _rel_err(x.grad, want) < 2e-2
         opt.step()
+
+
+def test_conv_dgrad_weight_batch_follows_flat_optimizer_steps():
+    """Conv dgrads read their weight layouts from the arena's per-step batch
+    (ddl_conv_w_dgrad_batch, one launch per optimizer step): after every flat optimizer step
+    (and after an in-place torch update, which bumps only the weight's version) the input
+    gradients must use the current weights -- 1x1, stride-1 3x3 and stride-2 (parity classes)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.ops.conv import conv2d_reference
+    from databricks_distributed_deep_learning_amd.optim import FlatSGD, ParamArena
+    torch.manual_seed(6)
+    shapes = {"w1": (64, 1, 1, 32), "w3": (32, 3, 3, 64), "w3s": (48, 3, 3, 32), "w1s": (40, 1, 1, 48)}
+    mod = torch.nn.Module()
+    for n, s in shapes.items():
+        mod.register_parameter(n, torch.nn.Parameter((torch.randn(*s, device=dev) * 0.1).bfloat16()))
+    arena = ParamArena(list(mod.named_parameters()))
+    opt = FlatSGD(arena, lr=0.5, momentum=0.9)
+    plan = [("w1", 1, 0), ("w3", 1, 1), ("w3s", 2, 1), ("w1s", 2, 0)]
+
+    def run(x, ref):
+        h = x
+        for n, st, pad in plan:
+            w = getattr(mod, n)
+            h = conv2d_reference(h, w.detach().float(), st, pad) if ref else ops.conv2d(h, w, st, pad)
+        return h
+
+    for step in range(4):
+        x = torch.randn(4, 16, 16, 32, device=dev).bfloat16().requires_grad_(True)
+        y = run(x, False)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        xr = x.detach().float().requires_grad_(True)
+        run(xr, True).backward(dy.float())
+        assert _rel_err(x.grad, xr.grad) < 3e-2, step
+        if step == 2:
+            with torch.no_grad():
+                mod.w3.mul_(-1.0)          # torch in-place update: version bump only
+        else:
+            opt.step()
+    cache = getattr(arena, "_ddl_wdg", None)
+    assert cache is not None and len(cache.jobs) >= 4 and cache.table is not None
+
+
+@pytest.mark.parametrize("second_consumer", [False, True])
+def test_layernorm_sinks_linear_bias_gradient(second_consumer):
+    """LayerNorm backward adds the column sums of its input gradient straight into the
+    producing Linear's bias-gradient slot (DataParallel sink); the Linear only marks it ready.
+    With a second consumer of the Linear output (autograd sums another gradient into dy) the
+    Linear adds the full column sums and takes the LayerNorm's share back out."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    torch.manual_seed(7)
+    H = 768
+    mod = torch.nn.Module()
+    mod.lin = torch.nn.Linear(512, H).to(dev).to(torch.bfloat16)
+    mod.ln_w = torch.nn.Parameter(torch.ones(H, device=dev, dtype=torch.bfloat16))
+    mod.ln_b = torch.nn.Parameter(torch.zeros(H, device=dev, dtype=torch.bfloat16))
+    dp = DataParallel(mod, broadcast_init=False, comm="torch")
+    W, b = mod.lin.weight.detach().float(), mod.lin.bias.detach().float()
+    scale = torch.linspace(-1, 1, H, device=dev)
+    want = torch.zeros(H, device=dev)
+    for _ in range(2):                      # second round: accumulation into the slot
+        x = torch.randn(2048, 512, device=dev).bfloat16()
+        res = torch.randn(2048, H, device=dev).bfloat16()
+        y = ops.linear(x, mod.lin.weight, mod.lin.bias, None)
+        out = ops.layer_norm(y, mod.ln_w, mod.ln_b, 1e-12, res, 0.0)
+        loss = (out.float() * scale).sum()
+        if second_consumer:
+            loss = loss + (y.float() ** 2).sum() * 1e-3
+        loss.backward()
+        yr = (x.float() @ W.t() + b).requires_grad_(True)
+        lr = (F.layer_norm(yr + res.float(), (H,), eps=1e-12) * scale).sum()
+        if second_consumer:
+            lr = lr + (yr ** 2).sum() * 1e-3
+        lr.backward()
+        want += yr.grad.sum(0)
+    dp.finish()
+    assert getattr(mod.lin.bias, "_ddl_sunk", None) is None
+    assert _rel_err(mod.lin.bias.grad, want) < 2e-2
