@@ -28,7 +28,14 @@
 namespace {
 
 constexpr int TM = 64, NT = 256;
-enum Epi { EPI_PLAIN = 0, EPI_RES = 1, EPI_BNB = 2 };
+// EPI_RESBNB (N = 256): residual added, then the BatchNorm backward as EPI_BNB -- the
+// BN input is register-prefetched a tile ahead (its LDS image would not fit beside the
+// residual's), the mask comes by LDS-DMA
+enum Epi { EPI_PLAIN = 0, EPI_RES = 1, EPI_BNB = 2, EPI_RESBNB = 3 };
+template <int EPI>
+constexpr bool is_bnb() { return EPI == EPI_BNB || EPI == EPI_RESBNB; }
+template <int N>
+constexpr int mask_stride() { return TM * N / 8 > 1024 ? TM * N / 8 : 1024; }   // bytes per mask image
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -106,14 +113,15 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
     constexpr int OFF_A = BBYTES, OFF_C = OFF_A + 2 * ABYTES;
     constexpr int NCIMG = EPI == EPI_PLAIN ? 1 : 2;
     constexpr int OFF_M = OFF_C + NCIMG * CBYTES;
-    constexpr int LDS = OFF_M + (EPI == EPI_BNB ? 2048 : 0);
+    constexpr int MS = mask_stride<N>();
+    constexpr int LDS = OFF_M + (is_bnb<EPI>() ? 2 * MS : 0);
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
     const int cb = wv * 16 * NCF;                 // this wave's first column
     const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
     const __amdgpu_buffer_rsrc_t crs = rsrc(p.C, p.c_bytes);
-    const bf16_t* eop = EPI == EPI_RES ? p.res : p.aux;
+    const bf16_t* eop = (EPI == EPI_RES || EPI == EPI_RESBNB) ? p.res : p.aux;
 
     const int t0 = blockIdx.x * p.chunk, t1 = min(p.tiles, t0 + p.chunk);
     // everything a tile reads comes in by LDS-DMA, one tile ahead: A, the epilogue operand,
@@ -123,22 +131,41 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
     auto prefetch = [&](int t, int buf) {
         dma_rows<K, TM>(p.A, (long)t * TM, p.M, smem + OFF_A + buf * ABYTES, wv, lane);
         if constexpr (EPI != EPI_PLAIN) dma_rows<N, TM>(eop, (long)t * TM, p.M, smem + OFF_C + buf * CBYTES, wv, lane);
-        if constexpr (EPI == EPI_BNB) {
-            // 64 rows x 8 mask bytes = 512 B as two 4-byte-per-lane DMA instructions (the
+        if constexpr (is_bnb<EPI>()) {
+            // 64 rows x N/8 mask bytes (512 B / 2 KB) as 4-byte-per-lane DMA instructions (the
             // mask ends on a dword: clamping never misplaces a valid row's bytes); every
-            // wave issues the same two (identical data)
+            // wave issues the same ones (identical data)
             const long byte0 = (long)t * TM * (N / 8), last = p.M * (N / 8) - 4;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < TM * N / 8 / 256; ++k) {
                 const long b = min(byte0 + (long)(k * 64 + lane) * 4, last);
                 const uint8_t* src = p.mask ? p.mask + b : (const uint8_t*)p.A;
-                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(smem + OFF_M + buf * 1024 + k * 256), 4, 0,
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(smem + OFF_M + buf * MS + k * 256), 4, 0,
                                                  0);
             }
         }
     };
+    // EPI_RESBNB: this lane's BN-input values (rows 16 i + r16, columns cb + 16 j + 4 g ..+3)
+    // of tile t, loaded one tile ahead into registers (issued with the DMAs, so the counted
+    // wait at the top of the tile that uses them covers them too)
+    // Two register sets, alternating per tile (the tile loop is unrolled by two for this
+    // epilogue): no copies, and the compiler's wait before a set's first use only covers the
+    // loads issued before it, not the stores behind them.
+    uint2 xa[4][NCF], xb[4][NCF];
+    auto prefetch_x = [&](int t, uint2 (&dst)[4][NCF]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long row = min((long)t * TM + 16 * i + r16, p.M - 1);
+#pragma unroll
+            for (int j = 0; j < NCF; ++j)
+                dst[i][j] = *reinterpret_cast<const uint2*>(p.aux + row * N + cb + 16 * j + 4 * g);
+        }
+    };
     dma_rows<K, N>(p.B, 0, N, smem, wv, lane);
-    if (t0 < t1) prefetch(t0, 0);
+    if (t0 < t1) {
+        prefetch(t0, 0);
+        if constexpr (EPI == EPI_RESBNB) prefetch_x(t0, xa);
+    }
 
     // per-lane fragment byte offsets (kernel constants)
     uint32_t aoff[4][KK], boff[NCF][KK];
@@ -167,7 +194,7 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) st_s[j][e] = st_q[j][e] = 0.f;
     float bmu[NCF][4] = {}, bis[NCF][4] = {};
-    if constexpr (EPI == EPI_BNB) {
+    if constexpr (is_bnb<EPI>()) {
 #pragma unroll
         for (int j = 0; j < NCF; ++j) {
             load4(p.mean + cb + 16 * j + 4 * g, bmu[j]);
@@ -175,14 +202,25 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
         }
     }
 
-    for (int t = t0; t < t1; ++t) {
+    auto tile = [&](const int t, uint2 (&xc)[4][NCF], uint2 (&xn)[4][NCF]) __attribute__((always_inline)) {
         const int buf = (t - t0) & 1;
-        if (t == t0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NCF) : "memory");   // the previous tile's stores
+        if constexpr (EPI == EPI_RESBNB) {
+            // the builtin (not asm) form: the compiler sees that the register-prefetched BN
+            // input (older than the previous tile's stores) has landed and adds no vmcnt(0)
+            // of its own before its first use (gfx9 encoding: vmcnt[3:0], expcnt 7, lgkmcnt 15)
+            // (unconditional: the first tile's vmcnt(0) is issued before the loop)
+            __builtin_amdgcn_s_waitcnt(0xF70 | (2 * NCF));
+        } else {
+            if (t == t0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NCF) : "memory");   // the previous tile's stores
+        }
         __builtin_amdgcn_s_barrier();
         // the next tile's loads (none after the last tile: LDS-DMA still landing when the
         // workgroup exits would write into the LDS of the next workgroup on this CU)
         if (t + 1 < t1) prefetch(t + 1, buf ^ 1);
+        // unconditional (a clamped row past the last tile): the same number of loads on every
+        // path lets the compiler's wait before the first use of xc leave these in flight
+        if constexpr (EPI == EPI_RESBNB) prefetch_x(t + 1, xn);
 
         const uint32_t abase = lds0 + OFF_A + buf * ABYTES;
         f32x4 acc[4][NCF];
@@ -212,12 +250,21 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
         // as whole rows
         const long m0 = (long)t * TM;
         const uint32_t cimg = lds0 + OFF_C + (EPI == EPI_PLAIN ? 0 : buf * CBYTES);
-        uint32_t mwords[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-        if constexpr (EPI == EPI_BNB) {
+        // mask words of this lane's row: bits of columns (cb & ~31) + 32 w + 0..31
+        uint32_t mwords[4][2] = {{~0u, ~0u}, {~0u, ~0u}, {~0u, ~0u}, {~0u, ~0u}};
+        if constexpr (is_bnb<EPI>()) {
             if (p.mask) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    mwords[i] = ds_read32(lds0 + OFF_M + buf * 1024 + (16 * i + r16) * (N / 8) + (cb & ~31) / 8);
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t a = lds0 + OFF_M + buf * MS + (16 * i + r16) * (N / 8) + (cb & ~31) / 8;
+                    if constexpr (NCF > 2) {
+                        const uint2 w2 = ds_read8(a);
+                        mwords[i][0] = w2.x;
+                        mwords[i][1] = w2.y;
+                    } else {
+                        mwords[i][0] = ds_read32(a);
+                    }
+                }
             }
         }
         uint2 ev[4][NCF];
@@ -244,12 +291,18 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
                     xv[2] = __uint_as_float(ev[i][j].y << 16);
                     xv[3] = __uint_as_float(ev[i][j].y & 0xffff0000u);
                 }
-                if constexpr (EPI == EPI_RES) {
+                if constexpr (EPI == EPI_RES || EPI == EPI_RESBNB) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] += xv[e];
                 }
-                if constexpr (EPI == EPI_BNB) {
-                    const uint32_t bits = mwords[i] >> (((cb + 16 * j) & 16) + 4 * g);
+                if constexpr (EPI == EPI_RESBNB) {   // the BN input for the statistics
+                    xv[0] = __uint_as_float(xc[i][j].x << 16);
+                    xv[1] = __uint_as_float(xc[i][j].x & 0xffff0000u);
+                    xv[2] = __uint_as_float(xc[i][j].y << 16);
+                    xv[3] = __uint_as_float(xc[i][j].y & 0xffff0000u);
+                }
+                if constexpr (is_bnb<EPI>()) {
+                    const uint32_t bits = mwords[i][(((cb & 31) + 16 * j) >> 5)] >> (((cb + 16 * j) & 16) + 4 * g);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = ((bits >> e) & 1u) ? v[e] : 0.f;
                 }
@@ -261,7 +314,7 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         st_s[j][e] += tq[e];
-                        st_q[j][e] += EPI == EPI_BNB ? tq[e] * xv[e] : tq[e] * tq[e];
+                        st_q[j][e] += is_bnb<EPI>() ? tq[e] * xv[e] : tq[e] * tq[e];
                     }
                 }
             }
@@ -281,6 +334,15 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
             const uint32_t off = grow < p.M ? (uint32_t)((grow * N + c * 8) * 2) : 0x80000000u;
             __builtin_amdgcn_raw_buffer_store_b128(d, crs, (int)off, 0, 0);
         }
+    };
+    if constexpr (EPI == EPI_RESBNB) {
+        __builtin_amdgcn_s_waitcnt(0xF70);      // B, the first tile's operands and BN input
+        for (int t = t0; t < t1; t += 2) {
+            tile(t, xa, xb);
+            if (t + 1 < t1) tile(t + 1, xb, xa);
+        }
+    } else {
+        for (int t = t0; t < t1; ++t) tile(t, xa, xb);
     }
 
     if (EPI != EPI_RES && p.colstats) {
@@ -294,7 +356,7 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float a = row16_sum(st_s[j][e]), b = row16_sum(st_q[j][e]);
-                if constexpr (EPI == EPI_BNB) b = (b - bmu[j][e] * a) * bis[j][e];   // sum dz * xhat
+                if constexpr (is_bnb<EPI>()) b = (b - bmu[j][e] * a) * bis[j][e];   // sum dz * xhat
                 if (r16 == 0) {
                     const int col = cb + 16 * j + 4 * g + e;
                     atomicAdd(&red[col], a);
@@ -309,7 +371,8 @@ __global__ __launch_bounds__(NT) void skinny_gemm_k(SkParams p) {
 template <int N, int K, int EPI>
 int launch(const SkParams& p0, int grid, hipStream_t st) {
     SkParams p = p0;
-    constexpr int lds = N * K * 2 + 2 * TM * K * 2 + (EPI == EPI_PLAIN ? 1 : 2) * TM * N * 2 + (EPI == EPI_BNB ? 2048 : 0);
+    constexpr int lds = N * K * 2 + 2 * TM * K * 2 + (EPI == EPI_PLAIN ? 1 : 2) * TM * N * 2 +
+                        (is_bnb<EPI>() ? 2 * mask_stride<N>() : 0);
     const int per_cu = std::max(1, std::min(4, (160 * 1024) / lds));
     int g = grid > 0 ? grid : 256 * per_cu;
     g = std::min(g, p.tiles);
@@ -322,8 +385,9 @@ int launch(const SkParams& p0, int grid, hipStream_t st) {
 }  // namespace
 
 // C[M, N] = A[M, K] B[N, K]^T for (N, K) = (256, 64) or (64, 256), bf16, all row-major
-// contiguous.  Epilogue: res (N = 256 only): C += res; aux (N = 64 only): the BatchNorm
-// backward -- C = acc * relu_mask, colstats rows [sum C | sum C * (aux - mean) * istd];
+// contiguous.  Epilogue: res (N = 256 only): C += res; aux (N = 64, or N = 256 with res):
+// the BatchNorm backward -- C = (acc [+ res]) * relu_mask, colstats rows
+// [sum C | sum C * (aux - mean) * istd];
 // otherwise colstats (nullable) rows [sum C | sum C^2].  Returns the number of statistics
 // rows written (0 without colstats), -1 when not covered (nothing launched), -2 - hipError.
 DDL_API int ddl_skinny_gemm(const void* A, const void* B, void* C, long M, int N, int K, float* colstats,
@@ -332,8 +396,8 @@ DDL_API int ddl_skinny_gemm(const void* A, const void* B, void* C, long M, int N
     if (M < 1 || M * (long)N * 2 >= (1l << 31)) return -1;
     const bool n256 = N == 256 && K == 64, n64 = N == 64 && K == 256;
     if (!n256 && !n64) return -1;
-    if (res && (!n256 || aux)) return -1;
-    if (aux && (!n64 || !mean || !istd)) return -1;
+    if (res && !n256) return -1;
+    if (aux && (!mean || !istd || (n256 && !res))) return -1;
     SkParams p{};
     p.A = (const bf16_t*)A;
     p.B = (const bf16_t*)B;
@@ -348,9 +412,10 @@ DDL_API int ddl_skinny_gemm(const void* A, const void* B, void* C, long M, int N
     p.istd = istd;
     p.c_bytes = (uint32_t)(M * N * 2);
     int g;
-    if (n256) g = res ? launch<256, 64, EPI_RES>(p, grid, stream) : launch<256, 64, EPI_PLAIN>(p, grid, stream);
+    if (n256) g = res ? (aux ? launch<256, 64, EPI_RESBNB>(p, grid, stream) : launch<256, 64, EPI_RES>(p, grid, stream))
+                      : launch<256, 64, EPI_PLAIN>(p, grid, stream);
     else g = aux ? launch<64, 256, EPI_BNB>(p, grid, stream) : launch<64, 256, EPI_PLAIN>(p, grid, stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -2 - (int)e;
-    return (colstats && !res) ? g : 0;
+    return (colstats && (!res || aux)) ? g : 0;
 }

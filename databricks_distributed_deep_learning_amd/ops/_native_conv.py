@@ -73,13 +73,14 @@ def _direct3x3(x, w, y, part=None, res=None, bnb=None, grid=0):
 
 
 _SKINNY = os.environ.get("DDL_SKINNY", "1") != "0"
+_SKINNY_RESBNB = os.environ.get("DDL_SKINNY_RESBNB", "1") != "0"
 
 
 def _skinny(a, b, c, part=None, res=None, bnb=None):
     """c[M, N] = a[M, K] b[N, K]^T by the streaming kernel (csrc/kernels/skinny_gemm.hip) when
     it covers the shape -- (N, K) = (256, 64) or (64, 256), bf16, contiguous, residual only
-    for N = 256, BN-backward epilogue only for N = 64.  Returns the statistics rows written,
-    or None when not covered (nothing launched)."""
+    for N = 256, BN-backward epilogue for N = 64, or for N = 256 together with the residual.
+    Returns the statistics rows written, or None when not covered (nothing launched)."""
     if not (_SKINNY and a.is_cuda):
         return None
     M, K = a.shape
@@ -89,7 +90,7 @@ def _skinny(a, b, c, part=None, res=None, bnb=None):
     ts = [a, b, c] + ([res] if res is not None else []) + ([bnb.x] if bnb is not None else [])
     if any(t.dtype != torch.bfloat16 or not t.is_contiguous() for t in ts):
         return None
-    if (res is not None and (N != 256 or bnb is not None)) or (bnb is not None and N != 64):
+    if (res is not None and N != 256) or (bnb is not None and N != 64 and (res is None or not _SKINNY_RESBNB)):
         return None
     if res is not None and tuple(res.shape) != (M, N) or bnb is not None and bnb.x.numel() != M * N:
         return None

@@ -70,3 +70,32 @@ def test_skinny_bn_backward_epilogue(M, grid, with_mask):
     xhat = (x.float() - mean) * istd
     torch.testing.assert_close(st[0], d.sum(0), atol=0.1, rtol=1e-3)
     torch.testing.assert_close(st[1], (d * xhat).sum(0), atol=0.1, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,grid,with_mask", [(4096, 0, True), (64 * 37 + 5, 8, True), (64 * 9, 3, True),
+                                              (1000, 5, False)])
+def test_skinny_residual_bn_backward_epilogue(M, grid, with_mask):
+    """N = 256 with residual AND the BatchNorm-backward epilogue (stage-1 residual dgrads):
+    dz = (a w^T + res) * relu_mask, rows [sum dz | sum dz * xhat]; odd tile counts per
+    workgroup exercise the two-tile unrolled loop's tail."""
+    torch.manual_seed(3)
+    N, K = 256, 64
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.1).bfloat16()
+    res = torch.randn(M, N, device="cuda").bfloat16()
+    x = torch.randn(M, N, device="cuda").bfloat16()
+    mean = torch.randn(N, device="cuda") * 0.1
+    istd = torch.rand(N, device="cuda") + 0.5
+    bits = torch.rand(M * N, device="cuda") > 0.3 if with_mask else torch.ones(M * N, device="cuda", dtype=torch.bool)
+    mask = (bits.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    part = torch.full((4096 * 2 * N,), float("nan"), device="cuda")
+    rows = _run(a, w, c, part=part, res=res, aux=x, mask=mask if with_mask else None, mean=mean, istd=istd, grid=grid)
+    assert rows > 0
+    v = (a.float() @ w.float().t() + res.float()) * bits.view(M, N).float()
+    torch.testing.assert_close(c.float(), v, atol=3e-2, rtol=2e-2)
+    st = part[:rows * 2 * N].view(rows, 2, N).sum(0)
+    d = c.float()
+    xhat = (x.float() - mean) * istd
+    torch.testing.assert_close(st[0], d.sum(0), atol=0.1, rtol=1e-3)
+    torch.testing.assert_close(st[1], (d * xhat).sum(0), atol=0.2, rtol=1e-3)
