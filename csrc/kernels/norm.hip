@@ -357,6 +357,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_k(const T* __restrict__
 // mask is the counter hash of (seed, flat element index), regenerated in the
 // backward, which writes the residual gradient g and the x gradient g*mask/(1-p)
 // (and the column sums of the latter: the producing Linear's bias gradient).
+// raw 4-element loads (bf16: 8 bytes, fp32: 16 bytes) converted later, so a load can stay in
+// flight across unrelated work
+template <typename T> struct Raw4;
+template <> struct Raw4<bf16_t> { typedef uint2 type; };
+template <> struct Raw4<float> { typedef float4 type; };
+__device__ __forceinline__ uint2 ld_raw4(const bf16_t* p) { return *reinterpret_cast<const uint2*>(p); }
+__device__ __forceinline__ float4 ld_raw4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void cvt_raw4(const uint2& u, float* v) {
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void cvt_raw4(const float4& a, float* v) { v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; }
+
 struct Drop {
     uint64_t seed;
     uint32_t thresh;   // 16-bit threshold (ddl_common.h keep_bits4); 0: no dropout
@@ -437,28 +450,36 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
     }
     const long r0 = (long)blockIdx.x * rows_per_blk;
     const long r1 = min(rows, r0 + rows_per_blk);
-    // raw loads of one row: input (x, plus residual) and dy; with dropout, the row's keep
-    // bits (4 per lane and column group) are generated once and reused for dx
-    auto load_row = [&](long row, float (&xv)[VPL][4], float (&d)[VPL][4], uint32_t (&kb)[VPL]) {
+    // raw (unconverted) loads of one row -- input x, dy and the residual -- so the next row
+    // pair's loads stay in flight while the current pair's reductions run; with dropout the
+    // row's keep bits (4 per lane and column group) are generated once and reused for dx
+    struct RowRaw {
+        typename Raw4<T>::type x[VPL], d[VPL], r[VPL];
+        uint32_t kb[VPL];
+    };
+    auto load_row = [&](long row, RowRaw& R) {
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
             const int col = 256 * k + 4 * lane;
-            load4(x + row * H + col, xv[k]);
-            load4(dy + row * H + col, d[k]);
-            kb[k] = drop.thresh ? drop_bits4(drop, row * H + col) : 0xfu;
+            R.x[k] = ld_raw4(x + row * H + col);
+            R.d[k] = ld_raw4(dy + row * H + col);
+            if (res) R.r[k] = ld_raw4(res + (row % res_rows) * H + col);
+            R.kb[k] = drop.thresh ? drop_bits4(drop, row * H + col) : 0xfu;
         }
-        if (res) {
+    };
+    // converted input (dropout(x) + residual) and dy of a loaded row
+    auto prep_row = [&](const RowRaw& R, float (&xv)[VPL][4], float (&d)[VPL][4]) {
 #pragma unroll
-            for (int k = 0; k < VPL; ++k) {
+        for (int k = 0; k < VPL; ++k) {
+            cvt_raw4(R.x[k], xv[k]);
+            cvt_raw4(R.d[k], d[k]);
+            if (drop.thresh) apply4(drop, R.kb[k], xv[k]);
+            if (res) {
                 float r[4];
-                load4(res + (row % res_rows) * H + 256 * k + 4 * lane, r);
-                if (drop.thresh) apply4(drop, kb[k], xv[k]);
+                cvt_raw4(R.r[k], r);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) xv[k][j] += r[j];
             }
-        } else if (drop.thresh) {
-#pragma unroll
-            for (int k = 0; k < VPL; ++k) apply4(drop, kb[k], xv[k]);
         }
     };
     auto finish_row = [&](long row, const float (&xv)[VPL][4], const float (&d)[VPL][4], const uint32_t (&kb)[VPL]) {
@@ -492,16 +513,37 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             store4(dx + idx, o);
         }
     };
-    // two rows per wave per iteration: the second row's loads are in flight while
-    // the first row's reductions run
-    for (long row = r0 + w; row < r1; row += 8) {
+    // two rows per wave per iteration, software-pipelined: the next pair's loads are issued
+    // before the current pair's reductions (the kernel was load-latency bound at ~3 TB/s)
+    // (H > 768: two pairs in registers would drop occupancy to one wave per SIMD, so one pair)
+    constexpr bool PIPE = VPL <= 3;
+    RowRaw ra{}, rb{}, rc{}, rd{};
+    long row = r0 + w;
+    if (PIPE && row < r1) load_row(row, ra);
+    if (PIPE && row + 4 < r1) load_row(row + 4, rb);
+    for (; row < r1; row += 8) {
         const bool two = row + 4 < r1;   // wave-uniform
-        float xa[VPL][4], da[VPL][4], xb[VPL][4], dbv[VPL][4];
-        uint32_t ka[VPL], kbb[VPL];
-        load_row(row, xa, da, ka);
-        if (two) load_row(row + 4, xb, dbv, kbb);
-        finish_row(row, xa, da, ka);
-        if (two) finish_row(row + 4, xb, dbv, kbb);
+        if constexpr (PIPE) {
+            if (row + 8 < r1) load_row(row + 8, rc);
+            if (row + 12 < r1) load_row(row + 12, rd);
+        } else {
+            load_row(row, ra);
+            if (two) load_row(row + 4, rb);
+        }
+        {
+            float xv[VPL][4], d[VPL][4];
+            prep_row(ra, xv, d);
+            finish_row(row, xv, d, ra.kb);
+        }
+        if (two) {
+            float xv[VPL][4], d[VPL][4];
+            prep_row(rb, xv, d);
+            finish_row(row + 4, xv, d, rb.kb);
+        }
+        if constexpr (PIPE) {
+            ra = rc;
+            rb = rd;
+        }
     }
 #pragma unroll
     for (int k = 0; k < VPL; ++k)
