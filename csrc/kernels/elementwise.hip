@@ -250,6 +250,60 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const T* __restrict__ x, T*
         *reinterpret_cast<uint2*>(idx + i * 8) = packed;
     }
 }
+// ResNet stem: training BatchNorm apply + ReLU + max-pool 3x3/2 (pad 1) in one pass over the
+// conv output (the full-resolution activation is never written).  Needs H == 2P, W == 2Q:
+// output pixel (p, q) owns input pixels (2p..2p+1, 2q..2q+1) and writes their ReLU-mask
+// bits (bn_apply's layout: bit j of byte e/8 for flat NHWC element e).  Pools the
+// bf16-rounded activations with maxpool_fwd_k's tie / NaN rules, so y and idx equal the
+// unfused BN apply -> max-pool.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_relu_maxpool_k(const T* __restrict__ x, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, T* __restrict__ y,
+                                                         uint8_t* __restrict__ idx, uint8_t* __restrict__ mask, int N,
+                                                         int H, int W, int C, int P, int Q) {
+    const int c8 = C / 8;
+    const long total = (long)N * P * Q * c8;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int cg = (int)(i % c8);
+        long t = i / c8;
+        const int q = (int)(t % Q); t /= Q;
+        const int p = (int)(t % P);
+        const int n = (int)(t / P);
+        float sc[8], sh[8], best[8];
+        uint8_t arg[8];
+        load8(scale + cg * 8, sc);
+        load8(shift + cg * 8, sh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int h = 2 * p - 1 + r;
+            if (h < 0) continue;
+#pragma unroll
+            for (int s_ = 0; s_ < 3; ++s_) {
+                const int w = 2 * q - 1 + s_;
+                if (w < 0) continue;
+                const long e = (((long)n * H + h) * W + w) * C + cg * 8;
+                float v[8];
+                load8(x + e, v);
+                uint32_t bits = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float a = to_f(from_f<T>(fmaxf(v[j] * sc[j] + sh[j], 0.f)));
+                    bits |= (a > 0.f ? 1u : 0u) << j;
+                    if (a > best[j] || (a != a)) { best[j] = a; arg[j] = (uint8_t)(r * 3 + s_); }
+                }
+                if (r >= 1 && s_ >= 1) mask[e >> 3] = (uint8_t)bits;   // an owned pixel
+            }
+        }
+        store8(y + i * 8, best);
+        uint2 packed;
+        packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+        packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
+        *reinterpret_cast<uint2*>(idx + i * 8) = packed;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                      T* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int K,
@@ -457,6 +511,17 @@ DDL_API int ddl_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int
                                                                       Q, K, S, pad)),
                (maxpool_fwd_k<float><<<grid_for(tot), 256, 0, st>>>((const float*)x, (float*)y, idx, N, H, W, C, P, Q,
                                                                      K, S, pad)));
+    DDL_RETURN_LAUNCH();
+}
+DDL_API int ddl_bn_relu_maxpool(int dtype, const void* x, const float* scale, const float* shift, void* y,
+                                uint8_t* idx, uint8_t* mask, int N, int H, int W, int C, int P, int Q, hipStream_t st) {
+    if (C % 8 || H != 2 * P || W != 2 * Q) return -1;
+    const long tot = (long)N * P * Q * (C / 8);
+    DISPATCH_T(dtype,
+               (bn_relu_maxpool_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)x, scale, shift, (bf16_t*)y,
+                                                                          idx, mask, N, H, W, C, P, Q)),
+               (bn_relu_maxpool_k<float><<<grid_for(tot), 256, 0, st>>>((const float*)x, scale, shift, (float*)y, idx,
+                                                                         mask, N, H, W, C, P, Q)));
     DDL_RETURN_LAUNCH();
 }
 DDL_API int ddl_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int P,

@@ -188,6 +188,62 @@ __global__ __launch_bounds__(256) void bn_apply_rows_k(const T* __restrict__ x, 
     }
 }
 
+// Two BatchNorms meeting at a residual add (a ResNet downsample block's output):
+// y = relu(x * scale + shift + x2 * scale2 + shift2) in one pass -- the downsample BN's
+// output is never written and re-read.
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply2_rows_k(const T* __restrict__ x, const T* __restrict__ x2,
+                                                        const float* __restrict__ scale, const float* __restrict__ shift,
+                                                        const float* __restrict__ scale2,
+                                                        const float* __restrict__ shift2, T* __restrict__ y,
+                                                        uint8_t* __restrict__ mask, long M, int C) {
+    const int tpr = C / 8, rpb = 256 / tpr;
+    const int cg = threadIdx.x % tpr, rr = threadIdx.x / tpr;
+    float sc[8], sh[8], sc2[8];
+    load8(scale + cg * 8, sc);
+    load8(shift + cg * 8, sh);
+    load8(scale2 + cg * 8, sc2);
+    {
+        float sh2[8];
+        load8(shift2 + cg * 8, sh2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sh[j] += sh2[j];
+    }
+    const long rs = (long)gridDim.x * rpb;
+    auto one = [&](const float* v, const float* r, long row) {
+        float o[8];
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float t = v[j] * sc[j] + r[j] * sc2[j] + sh[j];
+            if (RELU) {
+                t = fmaxf(t, 0.f);
+                bits |= (to_f(from_f<T>(t)) > 0.f ? 1u : 0u) << j;
+            }
+            o[j] = t;
+        }
+        store8(y + row * C + cg * 8, o);
+        if (RELU && mask) mask[row * tpr + cg] = (uint8_t)bits;
+    };
+    long r = (long)blockIdx.x * rpb + rr;
+    for (; r + 3 * rs < M; r += 4 * rs) {
+        float v[4][8], rv[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            load8(x + (r + u * rs) * C + cg * 8, v[u]);
+            load8(x2 + (r + u * rs) * C + cg * 8, rv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) one(v[u], rv[u], r + u * rs);
+    }
+    for (; r < M; r += rs) {
+        float v[8], rv[8];
+        load8(x + r * C + cg * 8, v);
+        load8(x2 + r * C + cg * 8, rv);
+        one(v, rv, r);
+    }
+}
+
 // blocks for the row-major passes: ~8 blocks of 256 threads per CU, each thread
 // looping over rows
 static int rows_grid(long M, int C) {
@@ -722,6 +778,23 @@ static void bn_apply_dispatch(const T* x, const T* res, const float* sc, const f
         if (relu) bn_apply_k<T, false, true><<<g, 256, 0, st>>>(x, res, sc, sh, y, mask, n8, C);
         else bn_apply_k<T, false, false><<<g, 256, 0, st>>>(x, res, sc, sh, y, mask, n8, C);
     }
+}
+
+// y = relu?(x * scale + shift + x2 * scale2 + shift2), bit mask as ddl_bn_apply (row-major
+// channel counts only: -1 otherwise)
+DDL_API int ddl_bn_apply2(int dtype, const void* x, const void* x2, const float* scale, const float* shift,
+                          const float* scale2, const float* shift2, void* y, long n, int C, int relu, void* mask,
+                          hipStream_t st) {
+    if (n % 8 || !rows_ok(C) || n % C) return -1;
+    const long M = n / C;
+    const int gr = rows_grid(M, C);
+    uint8_t* mk = (uint8_t*)mask;
+#define BA2(T) do { if (relu) bn_apply2_rows_k<T, true><<<gr, 256, 0, st>>>((const T*)x, (const T*)x2, scale, shift, scale2, shift2, (T*)y, mk, M, C); \
+                    else bn_apply2_rows_k<T, false><<<gr, 256, 0, st>>>((const T*)x, (const T*)x2, scale, shift, scale2, shift2, (T*)y, mk, M, C); } while (0)
+    if (dtype == 1) BA2(bf16_t);
+    else BA2(float);
+#undef BA2
+    DDL_RETURN_LAUNCH();
 }
 
 DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float* scale, const float* shift, void* y,

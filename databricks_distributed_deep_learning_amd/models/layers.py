@@ -119,6 +119,45 @@ def conv_bn(conv: "Conv2d", bn: "BatchNorm2d", x, residual=None, grad_residual=N
     return bn(y, residual=residual, residual_grad_to=residual_grad_to, stats=st)
 
 
+def conv_stats(conv: "Conv2d", bn: "BatchNorm2d", x, grad_residual=None):
+    """conv(x) with the BatchNorm statistics partials of ``bn`` from its GEMM epilogue, the
+    BatchNorm itself deferred (``conv_bn_add_bn``) -> (y, stats)."""
+    st = BNStats() if bn.training else None
+    return conv(x, grad_residual=grad_residual, bn_stats=st), st
+
+
+def conv_bn_add_bn(conv: "Conv2d", bn: "BatchNorm2d", x, bn2: "BatchNorm2d", y2, st2=None):
+    """relu(BN(conv(x)) + BN2(y2)), y2 / st2 from ``conv_stats``: a ResNet downsample block's
+    output.  In training on the native kernels both BatchNorms are applied in one pass (the
+    identity branch's BN output is never written); otherwise BN2's output is BN's residual."""
+    st = BNStats() if bn.training else None
+    y = conv(x, bn_stats=st)
+    if bn.training and bn2.training and bn.sync_group is None and bn2.sync_group is None and bn.relu \
+            and not bn2.relu:
+        out = ops.batch_norm_add_bn(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                                    y2, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var, bn2.momentum,
+                                    bn2.eps, st, st2)
+        if out is not None:
+            bn._nbt_pending += 1
+            bn2._nbt_pending += 1
+            return out
+    return bn(y, residual=bn2(y2, stats=st2), stats=st)
+
+
+def conv_bn_maxpool(conv: "Conv2d", bn: "BatchNorm2d", x):
+    """max_pool2d(relu(BN(conv(x))), 3, 2, 1): the ResNet stem.  In training on the native
+    kernels the BatchNorm, ReLU and max-pool run as one pass over the conv output."""
+    if bn.training and bn.sync_group is None and bn.relu:
+        st = BNStats()
+        y = conv(x, bn_stats=st)
+        out = ops.bn_relu_maxpool(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps, st)
+        if out is not None:
+            bn._nbt_pending += 1
+            return out
+        return ops.max_pool2d(bn(y, stats=st), 3, 2, 1)
+    return ops.max_pool2d(conv_bn(conv, bn, x), 3, 2, 1)
+
+
 class LayerNorm(nn.Module):
     def __init__(self, d: int, eps: float = 1e-12):
         super().__init__()

@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..ops.bridge import GradBridge
-from .layers import BatchNorm2d, Conv2d, Linear, conv_bn
+from .layers import BatchNorm2d, Conv2d, Linear, conv_bn, conv_bn_add_bn, conv_bn_maxpool, conv_stats
 
 
 _BRIDGE = os.environ.get("DDL_GRAD_BRIDGE", "1") != "0"
@@ -49,9 +49,9 @@ class BasicBlock(nn.Module):
             out = conv_bn(self.conv1, self.bn1, x, grad_residual=br)
             return conv_bn(self.conv2, self.bn2, out, residual=x, residual_grad_to=br)
         br = _bridge(x, self.training)
-        identity = self.downsample(x, grad_residual=br)
+        y_id, st_id = self.downsample.conv_stats(x, grad_residual=br)
         out = conv_bn(self.conv1, self.bn1, x, grad_to=br)
-        return conv_bn(self.conv2, self.bn2, out, residual=identity)
+        return conv_bn_add_bn(self.conv2, self.bn2, out, self.downsample.bn, y_id, st_id)
 
 
 class Bottleneck(nn.Module):
@@ -78,11 +78,12 @@ class Bottleneck(nn.Module):
             return conv_bn(self.conv3, self.bn3, out, residual=x, residual_grad_to=br)
         # downsample block: conv1 offers its input gradient to the downsample conv,
         # whose dgrad epilogue adds it (autograd runs the longer conv1 branch first)
+        # (its BatchNorm is applied together with bn3's: conv_bn_add_bn)
         br = _bridge(x, self.training)
-        identity = self.downsample(x, grad_residual=br)
+        y_id, st_id = self.downsample.conv_stats(x, grad_residual=br)
         out = conv_bn(self.conv1, self.bn1, x, grad_to=br)
         out = conv_bn(self.conv2, self.bn2, out)
-        return conv_bn(self.conv3, self.bn3, out, residual=identity)
+        return conv_bn_add_bn(self.conv3, self.bn3, out, self.downsample.bn, y_id, st_id)
 
 
 class Downsample(nn.Module):
@@ -92,6 +93,15 @@ class Downsample(nn.Module):
         super().__init__()
         self.add_module("0", Conv2d(cin, cout, 1, stride, 0))
         self.add_module("1", BatchNorm2d(cout, relu=False))
+
+    @property
+    def bn(self):
+        return self._modules["1"]
+
+    def conv_stats(self, x, grad_residual=None):
+        """The strided conv with its BatchNorm's statistics partials; the BN is applied by the
+        block together with the main branch's last BN (``conv_bn_add_bn``)."""
+        return conv_stats(self._modules["0"], self._modules["1"], x, grad_residual=grad_residual)
 
     def forward(self, x, grad_residual=None):
         return conv_bn(self._modules["0"], self._modules["1"], x, grad_residual=grad_residual)
@@ -124,8 +134,7 @@ class ResNet(nn.Module):
     def features(self, x):
         if not self.channels_last_input:
             x = x.permute(0, 2, 3, 1).contiguous()
-        x = conv_bn(self.conv1, self.bn1, x)
-        x = ops.max_pool2d(x, 3, 2, 1)
+        x = conv_bn_maxpool(self.conv1, self.bn1, x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return ops.global_avg_pool(x)
 

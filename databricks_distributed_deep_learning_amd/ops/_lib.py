@@ -119,6 +119,8 @@ _SIGS = {
     "ddl_bn_fwd_train": [I, P, L, I, P, P, P, P, F, F, P, P, P, P, P, P],
     "ddl_bn_eval_coeffs": [I, I, P, P, P, P, F, P, P, P],
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P, P],
+    "ddl_bn_apply2": [I, P, P, P, P, P, P, P, L, I, I, P, P],
+    "ddl_bn_relu_maxpool": [I, P, P, P, P, P, P, I, I, I, I, I, I, P],
     "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P, L],
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
     "ddl_conv_w_dgrad_batch": [P, P, I, P],

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import os
+from types import SimpleNamespace
 from typing import Optional
 
 import torch
@@ -33,6 +34,27 @@ def _group_sum(row: torch.Tensor, group) -> None:
     """In-place SUM all-reduce of a small fp32 row over the SyncBatchNorm group."""
     import torch.distributed as dist
     dist.all_reduce(row, op=dist.ReduceOp.SUM, group=group)
+
+
+def _bn_train_stats(x, weight, bias, running_mean, running_var, momentum, eps, given, stats) -> None:
+    """Training statistics of x into stats = [mean | invstd | scale | shift] (running stats
+    updated): from the producing GEMM's epilogue partials (``given``) or a statistics pass."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    dt = dcode(x)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    if given is not None:                          # partials from the producing GEMM's epilogue
+        part, nblk = given
+        # thousands of partial rows (one per 128 GEMM rows) are first collapsed 32:1
+        ws = torch.empty(-(-nblk // 32) * 2 * C, **f32) if nblk > 256 else None
+        call("ddl_bn_fwd_from_partials", dt, p(part), nblk, M, C, p(weight), p(bias), p(running_mean),
+             p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]),
+             p(ws), 0 if ws is None else ws.numel())
+    else:
+        nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
+        part = torch.empty(nblk * 2 * C, **f32)
+        call("ddl_bn_fwd_train", dt, p(x), M, C, p(weight), p(bias), p(running_mean), p(running_var),
+             float(momentum), float(eps), p(part), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
 
 
 class _BatchNormTrain(torch.autograd.Function):
@@ -68,18 +90,8 @@ class _BatchNormTrain(torch.autograd.Function):
                  p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]),
                  None, 0)
             ctx.m_total = M * world
-        elif given is not None:                    # partials from the producing GEMM's epilogue
-            part, nblk = given
-            # thousands of partial rows (one per 128 GEMM rows) are first collapsed 32:1
-            ws = torch.empty(-(-nblk // 32) * 2 * C, **f32) if nblk > 256 else None
-            call("ddl_bn_fwd_from_partials", dt, p(part), nblk, M, C, p(weight), p(bias), p(running_mean),
-                 p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]),
-                 p(ws), 0 if ws is None else ws.numel())
         else:
-            nblk = _lib.fn("ddl_bn_stats_nblk")(M, C)
-            part = torch.empty(nblk * 2 * C, **f32)
-            call("ddl_bn_fwd_train", dt, p(x), M, C, p(weight), p(bias), p(running_mean), p(running_var),
-                 float(momentum), float(eps), p(part), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]))
+            _bn_train_stats(x, weight, bias, running_mean, running_var, momentum, eps, given, stats)
         res = residual.contiguous() if residual is not None else None
         y = torch.empty_like(x)
         # ReLU: 1 bit per element for the backward instead of re-reading y
@@ -100,68 +112,179 @@ class _BatchNormTrain(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mask, weight, stats = ctx.saved_tensors
-        dy = dy.contiguous()
-        C = x.shape[-1]
-        M = x.numel() // C
-        nblk = _lib.fn("ddl_bn_bwd_nblk")(M, C)
-        f32 = dict(dtype=torch.float32, device=x.device)
-        # partial rows + room for their 32:1 collapse (see norm.hip collapse_partials)
-        part = torch.empty((nblk + -(-nblk // 32)) * 2 * C, **f32)
-        coef = torch.empty(3 * C, **f32)
-        dx = torch.empty_like(x)
-        sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
-        direct = sg is not None and sb is not None
-        if direct:
-            dgamma, dbeta = sg, sb
-        else:
-            dgamma = torch.empty_like(weight) if weight is not None else None
-            dbeta = torch.empty_like(weight) if weight is not None else None
-        given = ctx.bnb.take_for(dy) if ctx.bnb is not None else None
-        ctx.bnb = None
-        dres = torch.empty_like(x) if ctx.has_res and (given is None or ctx.group is not None) else None
-        if given is not None:
-            # dy is dz (ReLU mask applied) and [sum dz | sum dz*xhat] came from the dgrad epilogue
-            gpart, nrows = given
-            if ctx.group is not None:
-                row = torch.empty(2 * C, **f32)
-                call("ddl_bn_rows_sum", p(gpart), nrows, 2 * C, p(row), None)
-                local = row.clone()             # dgamma / dbeta stay this rank's partials
-                _group_sum(row, ctx.group)
-                call("ddl_bn_bwd_finish", dcode(x), p(dy), None, p(x), p(stats[0]), p(stats[1]), p(weight), M,
-                     ctx.m_total, C, 0, p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
-            else:
-                ws = gpart[nrows * 2 * C:]
-                # the residual gradient IS dz (mask applied, no affine): hand on the dgrad's
-                # output itself instead of copying it (one write pass per residual block)
-                call("ddl_bn_bwd_from_partials", dcode(x), p(gpart), nrows, p(ws), ws.numel(), p(dy), p(x),
-                     p(stats[0]), p(stats[1]), p(weight), M, C, p(dgamma), p(dbeta), p(coef), p(dx), None,
-                     int(direct))
-                if ctx.has_res:
-                    dres = dy
-        elif ctx.group is not None:
-            # SyncBatchNorm: [sum dz | sum dz*xhat] summed over the group before the finalize
-            call("ddl_bn_bwd_partials", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), M, C,
-                 int(ctx.relu), p(part))
-            row = torch.empty(2 * C, **f32)
-            call("ddl_bn_rows_sum", p(part), nblk, 2 * C, p(row), None)
-            # the group sum feeds the dx coefficients only: dgamma / dbeta are per-rank partials
-            # (the data-parallel reducer sums them), as in the CPU reference
-            local = row.clone()
-            _group_sum(row, ctx.group)
-            call("ddl_bn_bwd_finish", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M,
-                 ctx.m_total, C, int(ctx.relu), p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres),
-                 int(direct))
-        else:
-            call("ddl_bn_bwd", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M, C,
-                 int(ctx.relu), p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
-        if direct:
-            grad_ready(ctx.params[0])
-            grad_ready(ctx.params[1])
-            dgamma = dbeta = None
-        if dres is not None and ctx.bridge is not None:
-            ctx.bridge.put(dres)            # summed into the consumer's dgrad epilogue
-            dres = None
+        dx, dgamma, dbeta, dres = _bn_backward(ctx, dy, x, mask, weight, stats)
         return dx, dgamma, dbeta, None, None, None, None, None, dres, None, None, None
+
+
+def _bn_backward(ctx, dy, x, mask, weight, stats):
+    """Training BatchNorm backward -> (dx, dgamma, dbeta, dres).  ``ctx`` carries bnb (the
+    dgrad-epilogue hint), group, has_res, relu, params, bridge and m_total (SyncBN)."""
+    dy = dy.contiguous()
+    C = x.shape[-1]
+    M = x.numel() // C
+    nblk = _lib.fn("ddl_bn_bwd_nblk")(M, C)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    # partial rows + room for their 32:1 collapse (see norm.hip collapse_partials)
+    part = torch.empty((nblk + -(-nblk // 32)) * 2 * C, **f32)
+    coef = torch.empty(3 * C, **f32)
+    dx = torch.empty_like(x)
+    sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
+    direct = sg is not None and sb is not None
+    if direct:
+        dgamma, dbeta = sg, sb
+    else:
+        dgamma = torch.empty_like(weight) if weight is not None else None
+        dbeta = torch.empty_like(weight) if weight is not None else None
+    given = ctx.bnb.take_for(dy) if ctx.bnb is not None else None
+    ctx.bnb = None
+    dres = torch.empty_like(x) if ctx.has_res and (given is None or ctx.group is not None) else None
+    if given is not None:
+        # dy is dz (ReLU mask applied) and [sum dz | sum dz*xhat] came from the dgrad epilogue
+        gpart, nrows = given
+        if ctx.group is not None:
+            row = torch.empty(2 * C, **f32)
+            call("ddl_bn_rows_sum", p(gpart), nrows, 2 * C, p(row), None)
+            local = row.clone()             # dgamma / dbeta stay this rank's partials
+            _group_sum(row, ctx.group)
+            call("ddl_bn_bwd_finish", dcode(x), p(dy), None, p(x), p(stats[0]), p(stats[1]), p(weight), M,
+                 ctx.m_total, C, 0, p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+        else:
+            ws = gpart[nrows * 2 * C:]
+            # the residual gradient IS dz (mask applied, no affine): hand on the dgrad's
+            # output itself instead of copying it (one write pass per residual block)
+            call("ddl_bn_bwd_from_partials", dcode(x), p(gpart), nrows, p(ws), ws.numel(), p(dy), p(x),
+                 p(stats[0]), p(stats[1]), p(weight), M, C, p(dgamma), p(dbeta), p(coef), p(dx), None,
+                 int(direct))
+            if ctx.has_res:
+                dres = dy
+    elif ctx.group is not None:
+        # SyncBatchNorm: [sum dz | sum dz*xhat] summed over the group before the finalize
+        call("ddl_bn_bwd_partials", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), M, C,
+             int(ctx.relu), p(part))
+        row = torch.empty(2 * C, **f32)
+        call("ddl_bn_rows_sum", p(part), nblk, 2 * C, p(row), None)
+        # the group sum feeds the dx coefficients only: dgamma / dbeta are per-rank partials
+        # (the data-parallel reducer sums them), as in the CPU reference
+        local = row.clone()
+        _group_sum(row, ctx.group)
+        call("ddl_bn_bwd_finish", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M,
+             ctx.m_total, C, int(ctx.relu), p(row), p(local), p(dgamma), p(dbeta), p(coef), p(dx), p(dres),
+             int(direct))
+    else:
+        call("ddl_bn_bwd", dcode(x), p(dy), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), M, C,
+             int(ctx.relu), p(part), p(dgamma), p(dbeta), p(coef), p(dx), p(dres), int(direct))
+    if direct:
+        grad_ready(ctx.params[0])
+        grad_ready(ctx.params[1])
+        dgamma = dbeta = None
+    if dres is not None and ctx.bridge is not None:
+        ctx.bridge.put(dres)            # summed into the consumer's dgrad epilogue
+        dres = None
+    return dx, dgamma, dbeta, dres
+
+
+class _BatchNormAddBNTrain(torch.autograd.Function):
+    """relu(BN(x) + BN2(x2)) in training: a ResNet downsample block's output, both BatchNorms
+    applied in one pass (``ddl_bn_apply2``) instead of writing BN2's output and re-reading it as
+    the residual.  Backward: BN's as with a residual, then BN2's from the residual gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, x2, weight2, bias2, running_mean2,
+                running_var2, momentum2, eps2, pre=None, pre2=None):
+        x, x2 = x.contiguous(), x2.contiguous()
+        C = x.shape[-1]
+        f32 = dict(dtype=torch.float32, device=x.device)
+        stats = torch.empty(4, C, **f32)
+        stats2 = torch.empty(4, C, **f32)
+        _bn_train_stats(x, weight, bias, running_mean, running_var, momentum, eps,
+                        pre.take_for(x) if pre is not None else None, stats)
+        _bn_train_stats(x2, weight2, bias2, running_mean2, running_var2, momentum2, eps2,
+                        pre2.take_for(x2) if pre2 is not None else None, stats2)
+        y = torch.empty_like(x)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
+        call("ddl_bn_apply2", dcode(x), p(x), p(x2), p(stats[2]), p(stats[3]), p(stats2[2]), p(stats2[3]), p(y),
+             x.numel(), C, 1, p(mask))
+        ctx.bridge, ctx.group, ctx.relu, ctx.has_res = None, None, True, True
+        ctx.params, ctx.params2 = (weight, bias), (weight2, bias2)
+        ctx.save_for_backward(x, mask, weight, stats, x2, weight2, stats2)
+        ctx.bnb = None
+        if _BN_BWD_EPI and x.dtype == torch.bfloat16:
+            from .bridge import BNBackward
+            ctx.bnb = BNBackward(x, mask, stats[0], stats[1])
+            y._ddl_bnb = ctx.bnb
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, weight, stats, x2, weight2, stats2 = ctx.saved_tensors
+        dx, dgamma, dbeta, dres = _bn_backward(ctx, dy, x, mask, weight, stats)
+        c2 = SimpleNamespace(bnb=None, group=None, has_res=False, relu=False, params=ctx.params2, bridge=None)
+        dx2, dgamma2, dbeta2, _ = _bn_backward(c2, dres, x2, None, weight2, stats2)
+        return (dx, dgamma, dbeta, None, None, None, None, dx2, dgamma2, dbeta2, None, None, None, None, None, None)
+
+
+class _BNReluMaxPoolTrain(torch.autograd.Function):
+    """Training maxpool3x3/2(relu(BN(x))) -- the ResNet stem -- in one pass over the conv
+    output (``ddl_bn_relu_maxpool``: the full-resolution activation is never written).
+    Backward: the max-pool gather, then the BatchNorm backward with the ReLU mask."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, pre=None):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        P, Q = H // 2, W // 2
+        stats = torch.empty(4, C, dtype=torch.float32, device=x.device)
+        _bn_train_stats(x, weight, bias, running_mean, running_var, momentum, eps,
+                        pre.take_for(x) if pre is not None else None, stats)
+        y = torch.empty(N, P, Q, C, dtype=x.dtype, device=x.device)
+        idx = torch.empty(N, P, Q, C, dtype=torch.uint8, device=x.device)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
+        call("ddl_bn_relu_maxpool", dcode(x), p(x), p(stats[2]), p(stats[3]), p(y), p(idx), p(mask), N, H, W, C, P, Q)
+        ctx.params = (weight, bias)
+        ctx.save_for_backward(x, mask, weight, stats, idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, weight, stats, idx = ctx.saved_tensors
+        N, H, W, C = x.shape
+        dy = dy.contiguous()
+        da = torch.empty_like(x)
+        call("ddl_maxpool_bwd", dcode(dy), p(dy), p(idx), p(da), N, H, W, C, H // 2, W // 2, 3, 2, 1)
+        c = SimpleNamespace(bnb=None, group=None, has_res=False, relu=True, params=ctx.params, bridge=None)
+        dx, dgamma, dbeta, _ = _bn_backward(c, da, x, mask, weight, stats)
+        return dx, dgamma, dbeta, None, None, None, None, None
+
+
+def bn_relu_maxpool(x, weight, bias, running_mean, running_var, momentum, eps, pre=None):
+    """Training maxpool3x3/2/pad1(relu(BN(x))) in one pass; None when not covered."""
+    N, H, W, C = x.shape
+    if (not _FUSED_STEM or not _bn_supported(C) or x.dtype not in (torch.bfloat16, torch.float32)
+            or H % 2 or W % 2 or weight is None):
+        return None
+    if weight.dtype != x.dtype:
+        weight, bias = weight.to(x.dtype), bias.to(x.dtype)
+    return _BNReluMaxPoolTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, pre)
+
+
+_FUSED_STEM = os.environ.get("DDL_FUSED_STEM", "1") != "0"
+_DUAL_BN = os.environ.get("DDL_DUAL_BN", "1") != "0"
+
+
+def batch_norm_add_bn(x, weight, bias, running_mean, running_var, momentum, eps, x2, weight2, bias2,
+                      running_mean2, running_var2, momentum2, eps2, pre=None, pre2=None):
+    """Training relu(BN(x) + BN2(x2)) in one apply pass; None when not covered (the caller
+    then runs the two BatchNorms separately; DDL_DUAL_BN=0 always)."""
+    C = x.shape[-1]
+    if (not _DUAL_BN or not _bn_supported(C) or x.dtype not in (torch.bfloat16, torch.float32) or x2.dtype != x.dtype
+            or x2.shape != x.shape or weight is None or weight2 is None):
+        return None
+    if weight.dtype != x.dtype:
+        weight, bias = weight.to(x.dtype), bias.to(x.dtype)
+    if weight2.dtype != x.dtype:
+        weight2, bias2 = weight2.to(x.dtype), bias2.to(x.dtype)
+    return _BatchNormAddBNTrain.apply(x, weight, bias, running_mean, running_var, momentum, eps, x2, weight2, bias2,
+                                      running_mean2, running_var2, momentum2, eps2, pre, pre2)
 
 
 class _BatchNormEval(torch.autograd.Function):

@@ -108,3 +108,24 @@ def layer_norm(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Ten
     if dropout > 0.0:
         x = F.dropout(x, dropout, True)
     return layer_norm_reference(x, weight, bias, eps, residual)
+
+
+def batch_norm_add_bn(x, weight, bias, running_mean, running_var, momentum, eps, x2, weight2, bias2,
+                      running_mean2, running_var2, momentum2, eps2, stats=None, stats2=None):
+    """Training ``relu(BN(x) + BN2(x2))`` with both BatchNorms applied in one pass (a ResNet
+    downsample block's output).  Returns None when the native kernels do not cover it (CPU, odd
+    channel counts): the caller then runs the two BatchNorms separately."""
+    if not _lib.use_native(x, x2):
+        return None
+    from . import _native_norm
+    return _native_norm.batch_norm_add_bn(x, weight, bias, running_mean, running_var, momentum, eps, x2, weight2,
+                                          bias2, running_mean2, running_var2, momentum2, eps2, stats, stats2)
+
+
+def bn_relu_maxpool(x, weight, bias, running_mean, running_var, momentum, eps, stats=None):
+    """Training ``max_pool2d(relu(BN(x)), 3, 2, 1)`` in one pass over ``x`` (the ResNet stem).
+    Returns None when the native kernels do not cover it: the caller runs the ops separately."""
+    if not _lib.use_native(x):
+        return None
+    from . import _native_norm
+    return _native_norm.bn_relu_maxpool(x, weight, bias, running_mean, running_var, momentum, eps, stats)

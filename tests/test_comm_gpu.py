@@ -118,6 +118,11 @@ def test_reducer_native_per_bucket_ready(pg):
     from databricks_distributed_deep_learning_amd.parallel.ddp import DataParallel
     x = torch.randn(4, 64, 64, 3, device=pg)
     finals = []
+    # fp32 model: the convolutions run on the reference path (MIOpen), whose weight-gradient
+    # algorithm choice is not deterministic across runs -- pin it, and compare with a
+    # tolerance far below what a bucket stepped out of order would change
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
     for overlap in (False, True):
         torch.manual_seed(0)
         m = resnet18(num_classes=10).to(pg)
@@ -137,4 +142,5 @@ def test_reducer_native_per_bucket_ready(pg):
                 opt.step(ddp.finish())
         torch.cuda.synchronize()
         finals.append(arena.flat.float().clone())
-    torch.testing.assert_close(finals[0], finals[1])
+    torch.backends.cudnn.deterministic = det
+    torch.testing.assert_close(finals[0], finals[1], atol=1e-3, rtol=1e-3)

@@ -116,3 +116,73 @@ def test_bn_backward_epilogue_model_gradients(arch):
     # tight near the loss, loose at the stem
     for n, e in rel.items():
         assert e < (3e-2 if n.startswith(("layer3.", "layer4.", "fc.")) else 0.15), (n, e)
+
+
+@pytest.mark.parametrize("shape", [(8, 28, 28, 256), (4, 14, 14, 512), (6, 7, 7, 2048)])
+def test_downsample_block_dual_bn_apply(shape):
+    """relu(BN(y) + BN2(y2)) in one pass (ddl_bn_apply2, a downsample block's output): output,
+    input / affine gradients and running statistics equal the two separate BatchNorms."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    torch.manual_seed(5)
+    C = shape[-1]
+    y = torch.randn(*shape, device=dev).bfloat16()
+    y2 = (torch.randn(*shape, device=dev) * 2 + 0.5).bfloat16()
+    dout = torch.randn(*shape, device=dev).bfloat16()
+    prm = [(torch.rand(C, device=dev) + 0.5).bfloat16(), (torch.randn(C, device=dev) * 0.1).bfloat16(),
+           (torch.rand(C, device=dev) + 0.5).bfloat16(), (torch.randn(C, device=dev) * 0.1).bfloat16()]
+    res = []
+    for fused in (True, False):
+        a, a2 = y.clone().requires_grad_(True), y2.clone().requires_grad_(True)
+        g, b, g2, b2 = (t.clone().requires_grad_(True) for t in prm)
+        rm, rv, rm2, rv2 = (torch.zeros(C, device=dev), torch.ones(C, device=dev),
+                            torch.zeros(C, device=dev), torch.ones(C, device=dev))
+        if fused:
+            out = ops.batch_norm_add_bn(a, g, b, rm, rv, 0.1, 1e-5, a2, g2, b2, rm2, rv2, 0.1, 1e-5)
+            assert out is not None
+        else:
+            r = ops.batch_norm(a2, g2, b2, rm2, rv2, True, 0.1, 1e-5, False, None)
+            out = ops.batch_norm(a, g, b, rm, rv, True, 0.1, 1e-5, True, r)
+        out.backward(dout)
+        res.append([out.float(), a.grad.float(), a2.grad.float(), g.grad.float(), b.grad.float(), g2.grad.float(),
+                    b2.grad.float(), rm, rv, rm2, rv2])
+    names = ["out", "dy", "dy2", "dg", "db", "dg2", "db2", "rm", "rv", "rm2", "rv2"]
+    for n, u, v in zip(names, res[0], res[1]):
+        if n in ("out", "rm", "rv", "rm2", "rv2"):
+            torch.testing.assert_close(u, v, rtol=2e-2, atol=2e-2, msg=n)
+        else:
+            # the fused pass adds BN2's output unrounded, so ReLU-mask bits at |t| < ~1 bf16 ulp
+            # differ from the bf16-residual path (~2 % of the gradient norm at these sizes; a
+            # dropped or misrouted term would be O(1)): compare gradients by relative norm
+            assert ((u - v).norm() / v.norm().clamp_min(1e-12)).item() < 5e-2, n
+
+
+@pytest.mark.parametrize("shape", [(4, 112, 112, 64), (3, 30, 18, 16)])
+def test_stem_bn_relu_maxpool(shape):
+    """maxpool3x3/2(relu(BN(x))) in one pass (ddl_bn_relu_maxpool): pooled output equal to BN
+    apply -> max-pool (the same bf16-rounded activations are pooled), gradients and running
+    statistics equal."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    torch.manual_seed(6)
+    C = shape[-1]
+    x = torch.randn(*shape, device=dev).bfloat16()
+    g0, b0 = (torch.rand(C, device=dev) + 0.5).bfloat16(), (torch.randn(C, device=dev) * 0.3).bfloat16()
+    res = []
+    for fused in (True, False):
+        a = x.clone().requires_grad_(True)
+        g, b = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        if fused:
+            out = ops.bn_relu_maxpool(a, g, b, rm, rv, 0.1, 1e-5)
+            assert out is not None
+        else:
+            out = ops.max_pool2d(ops.batch_norm(a, g, b, rm, rv, True, 0.1, 1e-5, True, None), 3, 2, 1)
+        torch.manual_seed(0)
+        out.backward(torch.randn(out.shape, device=dev).bfloat16())
+        res.append((out.float(), a.grad.float(), g.grad.float(), b.grad.float(), rm, rv))
+    assert torch.equal(res[0][0], res[1][0])
+    for n, u, v in zip(["dx", "dg", "db"], res[0][1:4], res[1][1:4]):
+        assert ((u - v).norm() / v.norm().clamp_min(1e-12)).item() < 1e-2, n
+    torch.testing.assert_close(res[0][4], res[1][4])
+    torch.testing.assert_close(res[0][5], res[1][5])
