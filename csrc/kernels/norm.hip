@@ -857,6 +857,153 @@ DDL_API int ddl_bn_bwd(int dtype, const void* dy, const void* mask, const void* 
     DDL_RETURN_LAUNCH();
 }
 
+// ---------------------------------------------------------------- stem backward
+// BatchNorm + ReLU backward of the ResNet stem straight from the max-pool's output gradient:
+// the max-pool 3x3/2/pad1 backward (a gather over the <= 4 windows covering a pixel, matched
+// against the stored window argmax) is evaluated in both BatchNorm passes instead of
+// writing the full-resolution activation gradient and reading it twice.
+namespace {
+template <typename T>
+__device__ __forceinline__ void pool_grad8(const T* __restrict__ dy, const uint8_t* __restrict__ idx, long n, int h,
+                                           int w, int cg, int C, int P, int Q, float* acc) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int p_lo = h >> 1, p_hi = min(P - 1, (h + 1) >> 1);
+    const int q_lo = w >> 1, q_hi = min(Q - 1, (w + 1) >> 1);
+    for (int p = p_lo; p <= p_hi; ++p) {
+        const int r = h - 2 * p + 1;
+        for (int q = q_lo; q <= q_hi; ++q) {
+            const int s_ = w - 2 * q + 1;
+            const long o = ((n * P + p) * Q + q) * C + cg * 8;
+            float g[8];
+            load8(dy + o, g);
+            const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
+            const uint32_t want = (uint32_t)(r * 3 + s_);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t word = j < 4 ? packed.x : packed.y;
+                acc[j] += ((word >> (8 * (j & 3))) & 0xffu) == want ? g[j] : 0.f;
+            }
+        }
+    }
+}
+
+// per block: [sum dz | sum dz * xhat] (dz = relu_mask * maxpool_bwd(dy)); a thread keeps one
+// channel group for the whole launch (256 % (C / 8) == 0)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_pool_partial_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                             const uint8_t* __restrict__ mask, const T* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, int N, int H, int W,
+                                                             int C, int P, int Q, float* __restrict__ part) {
+    __shared__ float s_red[256 * 16];
+    const int c8 = C / 8, tid = threadIdx.x, cg = tid % c8;
+    float mu[8], is[8], a[8], b[8];
+    load8(mean + cg * 8, mu);
+    load8(invstd + cg * 8, is);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
+    const long total = (long)N * H * W * c8;
+    for (long i = (long)blockIdx.x * 256 + tid; i < total; i += (long)gridDim.x * 256) {
+        const long pix = i / c8;
+        const int w = (int)(pix % W);
+        const long t = pix / W;
+        const int h = (int)(t % H);
+        const long n = t / H;
+        float da[8], xv[8];
+        pool_grad8(dy, idx, n, h, w, cg, C, P, Q, da);
+        load8(x + i * 8, xv);
+        const uint32_t bits = mask[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float dz = ((bits >> j) & 1u) ? da[j] : 0.f;
+            a[j] += dz;
+            b[j] += dz * (xv[j] - mu[j]) * is[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        s_red[tid * 16 + j] = a[j];
+        s_red[tid * 16 + 8 + j] = b[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * C; c += 256) {
+        const int ch = c % C, g = ch / 8, j = ch % 8, off = c < C ? 0 : 8;
+        float s = 0.f;
+        for (int u = g; u < 256; u += c8) s += s_red[u * 16 + off + j];
+        part[(long)blockIdx.x * 2 * C + c] = s;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_pool_apply_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                           const uint8_t* __restrict__ mask, const T* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef, T* __restrict__ dx, int N,
+                                                           int H, int W, int C, int P, int Q) {
+    const int c8 = C / 8, cg = threadIdx.x % c8;
+    float A[8], B[8], D[8];
+    {
+        float mu[8], is[8], k1[8], mb[8], mg[8];
+        load8(mean + cg * 8, mu);
+        load8(invstd + cg * 8, is);
+        load8(coef + cg * 8, k1);
+        load8(coef + C + cg * 8, mb);
+        load8(coef + 2 * C + cg * 8, mg);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            A[j] = k1[j];
+            B[j] = -k1[j] * is[j] * mg[j];
+            D[j] = k1[j] * (mu[j] * is[j] * mg[j] - mb[j]);
+        }
+    }
+    const long total = (long)N * H * W * c8;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const long pix = i / c8;
+        const int w = (int)(pix % W);
+        const long t = pix / W;
+        const int h = (int)(t % H);
+        const long n = t / H;
+        float da[8], xv[8], o[8];
+        pool_grad8(dy, idx, n, h, w, cg, C, P, Q, da);
+        load8(x + i * 8, xv);
+        const uint32_t bits = mask[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = A[j] * (((bits >> j) & 1u) ? da[j] : 0.f) + B[j] * xv[j] + D[j];
+        store8(dx + i * 8, o);
+    }
+}
+}  // namespace
+
+DDL_API int ddl_bn_bwd_pool_nblk() { return 1024; }
+
+// dx = BatchNorm + ReLU backward of the stem given the max-pool 3x3/2/pad1 output gradient dy
+// [N, P, Q, C] and window argmax idx (ddl_bn_relu_maxpool); part: (nblk + ceil(nblk / 32)) * 2C
+DDL_API int ddl_bn_bwd_pool(int dtype, const void* dy, const uint8_t* idx, const uint8_t* mask, const void* x,
+                            const float* mean, const float* invstd, const void* gamma, int N, int H, int W, int C,
+                            int P, int Q, float* part, void* dgamma, void* dbeta, float* coef, void* dx,
+                            int acc_params, hipStream_t st) {
+    if (C % 8 || 256 % (C / 8) || H != 2 * P || W != 2 * Q || !mask) return -1;
+    const int nblk = ddl_bn_bwd_pool_nblk();
+    const long M = (long)N * H * W;
+    int nrows = nblk;
+#define BBP(T) do {                                                                                                     \
+        bn_bwd_pool_partial_k<T><<<nblk, 256, 0, st>>>((const T*)dy, idx, mask, (const T*)x, mean, invstd, N, H, W, C,  \
+                                                       P, Q, part);                                                     \
+        const float* fin = collapse_partials(part, nrows, 2 * C, st);                                                   \
+        bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(fin, nrows, C, M, (const T*)gamma, invstd, (T*)dgamma,    \
+                                                             (T*)dbeta, coef, acc_params);                              \
+        bn_bwd_pool_apply_k<T><<<grid_for(M * (C / 8), 256, 8192), 256, 0, st>>>((const T*)dy, idx, mask, (const T*)x,   \
+                                                                                mean, invstd, coef, (T*)dx, N, H, W, C, \
+                                                                                P, Q);                                   \
+    } while (0)
+    if (dtype == 1) BBP(bf16_t);
+    else BBP(float);
+#undef BBP
+    DDL_RETURN_LAUNCH();
+}
+
 // ---------------------------------------------------------------- LayerNorm
 template <typename T>
 static int ln_fwd_dispatch(const T* x, const T* res, long res_rows, const T* g, const T* b, T* y, float* mean,

@@ -121,6 +121,8 @@ _SIGS = {
     "ddl_bn_apply": [I, P, P, P, P, P, L, I, I, P, P],
     "ddl_bn_apply2": [I, P, P, P, P, P, P, P, L, I, I, P, P],
     "ddl_bn_relu_maxpool": [I, P, P, P, P, P, P, I, I, I, I, I, I, P],
+    "ddl_bn_bwd_pool_nblk": [],
+    "ddl_bn_bwd_pool": [I, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, P],
     "ddl_bn_fwd_from_partials": [I, P, I, L, I, P, P, P, P, F, F, P, P, P, P, P, L],
     "ddl_conv_w_dgrad": [P, P, I, I, I, I, I, I, P, P, P],
     "ddl_conv_w_dgrad_batch": [P, P, I, P],

@@ -249,10 +249,28 @@ class _BNReluMaxPoolTrain(torch.autograd.Function):
         x, mask, weight, stats, idx = ctx.saved_tensors
         N, H, W, C = x.shape
         dy = dy.contiguous()
-        da = torch.empty_like(x)
-        call("ddl_maxpool_bwd", dcode(dy), p(dy), p(idx), p(da), N, H, W, C, H // 2, W // 2, 3, 2, 1)
-        c = SimpleNamespace(bnb=None, group=None, has_res=False, relu=True, params=ctx.params, bridge=None)
-        dx, dgamma, dbeta, _ = _bn_backward(c, da, x, mask, weight, stats)
+        if not _FUSED_STEM_BWD:
+            da = torch.empty_like(x)
+            call("ddl_maxpool_bwd", dcode(dy), p(dy), p(idx), p(da), N, H, W, C, H // 2, W // 2, 3, 2, 1)
+            c = SimpleNamespace(bnb=None, group=None, has_res=False, relu=True, params=ctx.params, bridge=None)
+            dx, dgamma, dbeta, _ = _bn_backward(c, da, x, mask, weight, stats)
+            return dx, dgamma, dbeta, None, None, None, None, None
+        # the max-pool gather evaluated inside both BatchNorm backward passes (ddl_bn_bwd_pool):
+        # the full-resolution activation gradient is never written
+        nblk = _lib.fn("ddl_bn_bwd_pool_nblk")()
+        f32 = dict(dtype=torch.float32, device=x.device)
+        part = torch.empty((nblk + -(-nblk // 32)) * 2 * C, **f32)
+        coef = torch.empty(3 * C, **f32)
+        dx = torch.empty_like(x)
+        sg, sb = grad_sink(ctx.params[0]), grad_sink(ctx.params[1])
+        direct = sg is not None and sb is not None
+        dgamma, dbeta = (sg, sb) if direct else (torch.empty_like(weight), torch.empty_like(weight))
+        call("ddl_bn_bwd_pool", dcode(x), p(dy), p(idx), p(mask), p(x), p(stats[0]), p(stats[1]), p(weight), N, H, W,
+             C, H // 2, W // 2, p(part), p(dgamma), p(dbeta), p(coef), p(dx), int(direct))
+        if direct:
+            grad_ready(ctx.params[0])
+            grad_ready(ctx.params[1])
+            dgamma = dbeta = None
         return dx, dgamma, dbeta, None, None, None, None, None
 
 
@@ -268,6 +286,7 @@ def bn_relu_maxpool(x, weight, bias, running_mean, running_var, momentum, eps, p
 
 
 _FUSED_STEM = os.environ.get("DDL_FUSED_STEM", "1") != "0"
+_FUSED_STEM_BWD = os.environ.get("DDL_FUSED_STEM_BWD", "1") != "0"
 _DUAL_BN = os.environ.get("DDL_DUAL_BN", "1") != "0"
 
 
