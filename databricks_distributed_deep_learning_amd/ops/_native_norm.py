@@ -286,7 +286,10 @@ def bn_relu_maxpool(x, weight, bias, running_mean, running_var, momentum, eps, p
 
 
 _FUSED_STEM = os.environ.get("DDL_FUSED_STEM", "1") != "0"
-_FUSED_STEM_BWD = os.environ.get("DDL_FUSED_STEM_BWD", "1") != "0"
+# backward of the fused stem with the max-pool gather inside the BN backward passes: saves the
+# activation-gradient write but the gathers slow both passes about as much (same-box A/B neutral
+# within noise), so the default keeps max-pool backward + BN backward
+_FUSED_STEM_BWD = os.environ.get("DDL_FUSED_STEM_BWD", "0") != "0"
 _DUAL_BN = os.environ.get("DDL_DUAL_BN", "1") != "0"
 
 
