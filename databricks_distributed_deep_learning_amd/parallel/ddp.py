@@ -53,6 +53,7 @@ class Bucket:
     payload: Optional[torch.Tensor] = None
     grads_seen: set = field(default_factory=set)
     seq: int = 0                 # native engine: this bucket's all-reduce number (wait_upto)
+    eager_done: bool = False     # set_eager callback already issued on the side stream
 
 
 class DataParallel(nn.Module):
@@ -104,6 +105,9 @@ class DataParallel(nn.Module):
         for b in self.buckets:
             for ei in b.entry_ids:
                 self._entry_bucket[ei] = b.index
+        self._eager_cb: Optional[Callable[[torch.Tensor, int, int], None]] = None
+        self._eager_stream = None
+        self._eager_used = False
         self._hooks = []
         for ei, e in enumerate(self.arena.entries):
             hook = self._make_hook(ei)
@@ -140,6 +144,7 @@ class DataParallel(nn.Module):
             b.payload = None
             b.grads_seen = set()
             b.seq = 0
+            b.eager_done = False
         self._order: List[Bucket] = []       # buckets in all-reduce launch order
 
     def _make_hook(self, ei: int):
@@ -179,6 +184,36 @@ class DataParallel(nn.Module):
                 b.seq = seq if isinstance(seq, int) else 0
             else:
                 b.handle = dist.all_reduce(b.payload, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self._eager_cb is not None and self._eager_ok():
+            self._run_eager(b)
+
+    # ------------------------------------------------------------------ eager per-bucket callbacks
+    def _eager_ok(self) -> bool:
+        return (self.arena.grad.is_cuda and self.reduce_dtype == self.arena.dtype and not self._acc_active
+                and (self.native is None or hasattr(self.native, "wait_upto")))
+
+    def set_eager(self, cb: Optional[Callable[[torch.Tensor, int, int], None]]) -> None:
+        """Run ``cb(grad, lo, hi)`` for each bucket DURING backward, the moment the bucket's
+        gradients exist (and, with several ranks, its all-reduce is done), on a side stream:
+        the flat optimizer's HBM-bound update of the late layers then runs under the early
+        layers' backward GEMMs instead of after the whole backward.  :meth:`finish` joins the
+        side stream back into the compute stream.  ``None`` turns it off."""
+        self._eager_cb = cb
+        if cb is not None and self._eager_stream is None and self.arena.grad.is_cuda:
+            self._eager_stream = torch.cuda.Stream(device=self.arena.grad.device)
+
+    def _run_eager(self, b: Bucket) -> None:
+        compute = torch.cuda.current_stream(self.arena.grad.device)
+        side = self._eager_stream
+        side.wait_stream(compute)               # every kernel that produced this bucket's gradients
+        with torch.cuda.stream(side):
+            if b.handle is not None:
+                b.handle.wait()                 # the side stream waits for this bucket's ring
+            elif self.native is not None and b.seq > 0:
+                self.native.wait_upto(b.seq)
+            self._eager_cb(self.arena.grad, b.start, b.end)
+        b.eager_done = True
+        self._eager_used = True
 
     # ------------------------------------------------------------------
     def forward(self, *args, **kwargs):
@@ -214,6 +249,14 @@ class DataParallel(nn.Module):
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
+        if self._eager_used:
+            # the callbacks ran during backward on the side stream: the compute stream (next
+            # forward, zero_grad) waits for them; the rings were waited for on the side stream
+            torch.cuda.current_stream(self.arena.grad.device).wait_stream(self._eager_stream)
+            on_ready = None
+            self._eager_used = False
+        elif self._eager_cb is not None and on_ready is None:
+            on_ready = self._eager_cb           # requested but not possible this step: per bucket, now
         streamed = on_ready is not None and self.reduce_dtype == self.arena.dtype
         out_early = self._acc32 if self._acc_active else self.arena.grad
         if streamed:

@@ -68,6 +68,11 @@ class Trainer:
         self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
         self.overlap_optimizer = (self.world > 1 and cfg.overlap_optimizer and self.opt.supports_ranges()
                                   and self.ddp.reduce_dtype == self.arena.dtype)
+        # on the GPU the per-bucket updates start DURING backward, on a side stream, as soon as a
+        # bucket's gradients (and its all-reduce) are done (DataParallel.set_eager)
+        self.eager_optimizer = (cfg.overlap_optimizer and cfg.eager_optimizer and self.opt.supports_ranges()
+                                and os.environ.get("DDL_EAGER_OPTIMIZER", "1") != "0"
+                                and self.ddp.reduce_dtype == self.arena.dtype and self.arena.grad.is_cuda)
         if cfg.batch_size <= 0:
             cfg.batch_size = self._auto_batch()
         self.loader = self._make_loader()
@@ -113,15 +118,23 @@ class Trainer:
         c = self.cfg
         self.ddp.zero_grad()
         loss_sum = None
+        scale = 1.0 / (self.world * c.grad_accum)
         for micro in range(c.grad_accum):
             batch = self.loader.next()
-            ctx = self.ddp.no_sync() if micro < c.grad_accum - 1 else contextlib.nullcontext()
+            last = micro == c.grad_accum - 1
+            ctx = self.ddp.no_sync() if not last else contextlib.nullcontext()
+            if last and self.eager_optimizer:
+                self.opt.begin_step(lr=self.sched(self.step))
+                self.ddp.set_eager(lambda g, lo, hi: self.opt.step_range(g, scale, lo, hi))
             with ctx:
                 loss = self.loss_fn(batch)
                 loss.backward()
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
-        scale = 1.0 / (self.world * c.grad_accum)
-        if self.overlap_optimizer:
+        if self.eager_optimizer:
+            self.ddp.finish()               # joins the side stream (or runs the remaining updates)
+            self.ddp.set_eager(None)
+            self.opt.end_step()
+        elif self.overlap_optimizer:
             # each bucket's optimizer update starts as soon as ITS all-reduce is done, so
             # the last buckets' rings (BERT's 68 MB embedding bucket) run under the update
             # of everything else instead of in front of it

@@ -144,3 +144,26 @@ def test_reducer_native_per_bucket_ready(pg):
         finals.append(arena.flat.float().clone())
     torch.backends.cudnn.deterministic = det
     torch.testing.assert_close(finals[0], finals[1], atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("preset,over", [
+    ("resnet50_ddp", dict(model="resnet18", batch_size=8, image_size=64, num_classes=10)),
+    ("bert_base_ddp", dict(batch_size=4, seq_len=64)),
+])
+def test_eager_optimizer_matches_post_backward_step(pg, preset, over):
+    """Optimizer updates issued per bucket DURING backward on a side stream
+    (DataParallel.set_eager) give the same parameters and state as one step after backward."""
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    finals = []
+    for eager in (True, False):
+        cfg = get_preset(preset, steps=3, warmup_steps=0, log_every=0, eager_optimizer=eager, **over)
+        t = Trainer(cfg)
+        assert t.eager_optimizer == eager
+        t.run()
+        torch.cuda.synchronize()
+        st = [t.arena.flat.float().clone()] + [v.float().clone() for v in t.opt._state_tensors().values()]
+        finals.append(st)
+        del t
+    for a, b in zip(*finals):
+        torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
