@@ -707,10 +707,15 @@ __global__ __launch_bounds__(256) void bn_partials_collapse_k(const float* __res
 // Partial rows beyond this are first collapsed 32:1 (a single finalize block per
 // 64 columns is too little parallelism for ~1000 rows).  The caller allocates
 // `part` with room for the collapsed rows behind the nblk partial rows.
+// DDL_BN_COLLAPSE_MIN overrides both thresholds (this one and ddl_bn_partials_ws's 256)
+static int collapse_env() {
+    static const int v = [] { const char* e = getenv("DDL_BN_COLLAPSE_MIN"); return e ? atoi(e) : 0; }();
+    return v;
+}
 constexpr int COLLAPSE_OVER = 64;
 static const float* collapse_partials(const float* part, int& nblk, int width, hipStream_t st,
                                       float* ws = nullptr) {
-    if (nblk <= COLLAPSE_OVER) return part;
+    if (nblk <= (collapse_env() > 0 ? collapse_env() : COLLAPSE_OVER)) return part;
     if (!ws) ws = const_cast<float*>(part) + (long)nblk * width;
     const int chunks = (nblk + PC_ROWS - 1) / PC_ROWS;
     bn_partials_collapse_k<<<dim3((width + 255) / 256, chunks), 256, 0, st>>>(part, nblk, width, ws);
@@ -719,7 +724,7 @@ static const float* collapse_partials(const float* part, int& nblk, int width, h
 }
 
 DDL_API long ddl_bn_partials_ws(int nblk, int C) {
-    return nblk > 256 ? (long)((nblk + PC_ROWS - 1) / PC_ROWS) * 2 * C : 0;
+    return nblk > (collapse_env() > 0 ? collapse_env() : 256) ? (long)((nblk + PC_ROWS - 1) / PC_ROWS) * 2 * C : 0;
 }
 
 DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, long M, int C, const void* gamma,

@@ -46,7 +46,7 @@ def _bn_train_stats(x, weight, bias, running_mean, running_var, momentum, eps, g
     if given is not None:                          # partials from the producing GEMM's epilogue
         part, nblk = given
         # thousands of partial rows (one per 128 GEMM rows) are first collapsed 32:1
-        ws = torch.empty(-(-nblk // 32) * 2 * C, **f32) if nblk > 256 else None
+        ws = torch.empty(-(-nblk // 32) * 2 * C, **f32) if nblk > 32 else None
         call("ddl_bn_fwd_from_partials", dt, p(part), nblk, M, C, p(weight), p(bias), p(running_mean),
              p(running_var), float(momentum), float(eps), p(stats[0]), p(stats[1]), p(stats[2]), p(stats[3]),
              p(ws), 0 if ws is None else ws.numel())
