@@ -163,6 +163,7 @@ def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb
 # of a shape times every candidate into scratch outputs and caches the fastest;
 # the bench's warmup steps absorb this.  DDL_GEMM_TUNE=0 uses the static heuristic.
 _tuned: dict = {}
+_NARROW_STATS = os.environ.get("DDL_TUNE_NARROW_STATS", "0") != "0"   # same-box A/B neutral: off
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
 # optional persistent cache (JSON): later processes skip the timing runs
 _CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
@@ -216,6 +217,10 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     cs_s = None
     if colstats is not None:   # statistics epilogue: whole-K tiles only
         cands = [c for c in cands if c[1] == 1 and not c[0].startswith("t")]
+        # 128x64 tiles (three blocks per CU) for the epilogue-heavy statistics / BN-backward
+        # tiles even where N is a multiple of 128 (more blocks in flight per CU)
+        if _NARROW_STATS and N % 64 == 0 and ("narrow", 1) not in cands:
+            cands.append(("narrow", 1))
         cs_s = torch.empty_like(colstats)
     if len(cands) == 1:
         return cands[0]
