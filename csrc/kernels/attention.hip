@@ -636,8 +636,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                                                             const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
-                                                            int S, int H, float scale, float p_drop, uint64_t seed) {
+                                                            int S, int H, float scale, float p_drop, uint64_t seed,
+                                                            float* __restrict__ colsum) {
     __shared__ __attribute__((aligned(16))) char smem[3 * FS * ROWB];   // Q, K, dO; then dS^T halves over Q, dO
+    // colsum (nullable, [B][3 H D] fp32): this (b, h)'s column sums of dQ / dK / dV over the sequence --
+    // the QKV Linear's bias gradient without another pass over dQKV: per-wave sums, then over waves
+    __shared__ float s_cs[8][3][D];
     __shared__ __attribute__((aligned(16))) float s_lse[FS];
     __shared__ __attribute__((aligned(16))) float s_delta[FS];
     __shared__ float s_mask[FS];
@@ -781,6 +785,18 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                 store4(dvr + 16 * db + 4 * g, b4);
             }
         }
+        if (colsum) {   // keys past S hold zero gradients
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sk = row16_sum(dk[db][e] * scale), sv = row16_sum(dv[db][e]);
+                    if ((lane & 15) == 0) {
+                        s_cs[w][1][16 * db + 4 * g + e] = sk;
+                        s_cs[w][2][16 * db + 4 * g + e] = sv;
+                    }
+                }
+        }
     }
     __syncthreads();               // every wave is done with the Q and dO images
     {
@@ -820,6 +836,25 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                 store4(dqr + 16 * db + 4 * g, a4);
             }
         }
+        if (colsum) {   // queries past S hold zero gradients
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sq = row16_sum(dq[db][e] * scale);
+                    if ((lane & 15) == 0) s_cs[w][0][16 * db + 4 * g + e] = sq;
+                }
+        }
+    }
+    if (colsum) {
+        __syncthreads();
+        if (tid < 3 * D) {
+            const int part = tid / D, d = tid - part * D;
+            float acc = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < 8; ++ww) acc += s_cs[ww][part][d];
+            colsum[(long)b * 3 * H * D + part * H * D + h * D + d] = acc;
+        }
     }
 }
 }  // namespace
@@ -857,12 +892,14 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
 }
 
 // dqkv [B, S, 3*H*64] bf16 (fully written); delta scratch [B, H, S] fp32
+// colsum (nullable, [B][3 H 64] fp32): per-batch column sums of dqkv (the QKV bias gradient is their
+// column sum) -- single-workgroup path only (S <= 128): returns 1 when it was NOT written
 DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, const float* mask,
                          float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop, uint64_t seed,
-                         hipStream_t st) {
+                         float* colsum, hipStream_t st) {
     if (S <= FS && fused_bwd_enabled()) {   // the whole sequence fits one workgroup's LDS
 #define BWD_FUSED(F, DR) attn_bwd_fused_k<F, DR><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, \
-        (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, seed)
+        (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, seed, colsum)
         if (S == FS) { if (p_drop > 0.f) BWD_FUSED(true, true); else BWD_FUSED(true, false); }
         else { if (p_drop > 0.f) BWD_FUSED(false, true); else BWD_FUSED(false, false); }
 #undef BWD_FUSED
@@ -875,5 +912,6 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
                                          S, H, scale, p_drop, seed);
     attn_bwd_dq_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B, S,
                                         H, scale, p_drop, seed);
-    DDL_RETURN_LAUNCH();
+    const int rc = (int)hipGetLastError();
+    return rc ? rc : (colsum ? 1 : 0);
 }

@@ -7,6 +7,7 @@ ViT-B/16); other head dims use the reference path.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -16,8 +17,12 @@ from ._native_elementwise import new_seed
 
 _lib.register({
     "ddl_attn_fwd": [P, P, P, P, I, I, I, CF, CF, U64, P],
-    "ddl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, CF, CF, U64, P],
+    "ddl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, CF, CF, U64, P, P],
 })
+
+# the fused backward (S <= 128) also writes per-batch column sums of dQKV, from which the QKV
+# Linear takes its bias gradient instead of another pass over dQKV (DDL_ATTN_COLSUM=0: off)
+_COLSUM = os.environ.get("DDL_ATTN_COLSUM", "1") != "0"
 
 
 class _Attention(torch.autograd.Function):
@@ -45,8 +50,16 @@ class _Attention(torch.autograd.Function):
         dout = dout.contiguous()
         delta = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
         dqkv = torch.empty_like(qkv)
-        _lib.call("ddl_attn_bwd", qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _lib.p(m),
-                  delta.data_ptr(), dqkv.data_ptr(), B, S, H, scale, p_drop, seed)
+        cs = torch.empty(B, 3 * H * 64, dtype=torch.float32, device=qkv.device) if _COLSUM and S <= 128 else None
+        rc = _lib.fn("ddl_attn_bwd")(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _lib.p(m),
+                                     delta.data_ptr(), dqkv.data_ptr(), B, S, H, scale, p_drop, seed, _lib.p(cs),
+                                     _lib.stream())
+        if rc not in (0, 1):
+            raise RuntimeError(f"native kernel ddl_attn_bwd failed with HIP error {rc}")
+        if cs is not None and rc == 0:
+            # rides on the gradient: the producing Linear's bias gradient = column sums of these rows
+            # (the version guards against autograd accumulating another gradient into dqkv)
+            dqkv._ddl_colsum_rows = (cs, dqkv._version)
         return dqkv, None, None, None
 
 

@@ -97,3 +97,31 @@ def test_attention_dropout_mask_parity(S):
     out.backward(g.to(torch.bfloat16))
     ref.backward(g.to(torch.bfloat16).float())
     assert (qkv.grad.float() - q32.grad).abs().max().item() < 3e-2 * q32.grad.abs().max().item() + 1e-2
+
+
+@pytest.mark.parametrize("S,sink", [(128, False), (128, True), (100, True), (197, False)])
+def test_qkv_bias_gradient_from_attention_column_sums(S, sink):
+    """The fused attention backward (S <= 128) writes per-batch column sums of dQKV; the QKV
+    Linear takes its bias gradient from them (into the DataParallel slot, or a fresh tensor)
+    instead of another pass over dQKV.  S = 197 takes the two-kernel path and the plain sum."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd import ops
+    torch.manual_seed(2)
+    B, H, hid = 3, 4, 256
+    mod = torch.nn.Module()
+    mod.lin = torch.nn.Linear(hid, 3 * H * 64).to(dev).to(torch.bfloat16)
+    if sink:
+        from databricks_distributed_deep_learning_amd.parallel import DataParallel
+        dp = DataParallel(mod, broadcast_init=False, comm="torch")
+    x = torch.randn(B, S, hid, device=dev).bfloat16()
+    g = torch.randn(B, S, H * 64, device=dev).bfloat16()
+    qkv = ops.linear(x, mod.lin.weight, mod.lin.bias, None)
+    ops.attention(qkv, H, None, 0.0).backward(g)
+    if sink:
+        dp.finish()
+    got = mod.lin.bias.grad.float()
+    b32 = mod.lin.bias.detach().float().requires_grad_(True)
+    ref = ref_attention(x.float() @ mod.lin.weight.detach().float().t() + b32, H)
+    ref.backward(g.float())
+    err = (got - b32.grad).abs().max().item()
+    assert err < 2e-2 * b32.grad.abs().max().item() + 1e-2, err
