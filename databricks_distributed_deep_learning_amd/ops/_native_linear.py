@@ -199,9 +199,8 @@ class _Linear(torch.autograd.Function):
                     grad_ready(ctx.b_param)
                 else:
                     db = pre.to(w.dtype)
-            elif self_rows(dy, ctx.act, N) is not None:
+            elif (rows := _colsum_rows(dy, ctx.act, N)) is not None:
                 # per-batch column sums from the attention backward that produced dy
-                rows = dy._ddl_colsum_rows[0]
                 out = sink if sink is not None else torch.empty(N, dtype=w.dtype, device=w.device)
                 ws = torch.empty(-(-rows.shape[0] // 32) * N, dtype=torch.float32, device=rows.device)
                 call("ddl_rows_sum_sink", dcode(out), p(rows), rows.shape[0], N, N, p(out), int(sink is not None),
@@ -219,7 +218,7 @@ class _Linear(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
-def self_rows(dy, act, N):
+def _colsum_rows(dy, act, N):
     """The [rows, N] fp32 column-sum rows riding on ``dy`` (attention backward), if they
     describe exactly this gradient (no activation in between, untouched since)."""
     r = getattr(dy, "_ddl_colsum_rows", None)
