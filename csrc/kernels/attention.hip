@@ -21,6 +21,7 @@
 // indices ((b*H+h)*S + q)*S + k (attn_hash below), regenerated in backward.
 #include "ddl_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -82,6 +83,12 @@ __device__ __forceinline__ bf16x8 pack_acc(const f32x4& a, const f32x4& b) {
     return r;
 }
 
+// ok ? v : 0 per component: a select of whole vectors made hipcc park both in scratch and
+// select a scratch POINTER (a scratch store + load on every staged chunk)
+__device__ __forceinline__ uint4 zero_unless(bool ok, uint4 v) {
+    return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
+}
+
 // stage a [64 rows][64] bf16 tile (rows >= nrows -> 0) with 256 threads: 2 chunks each
 struct Stager {
     uint4 v[2];
@@ -92,7 +99,7 @@ struct Stager {
             const int r = (t >> 3) + 32 * i, c = t & 7;
             const bool ok = row0 + r < nrows;
             const uint4 x = *reinterpret_cast<const uint4*>(base + (long)(ok ? row0 + r : 0) * row_stride + c * 8);
-            v[i] = ok ? x : make_uint4(0, 0, 0, 0);
+            v[i] = zero_unless(ok, x);
         }
     }
     template <bool TR>
@@ -506,43 +513,65 @@ template <bool FULL, bool MASK, bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restrict__ qkv,
                                                             const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse, int S, int H, float scale,
-                                                            float p_drop, uint64_t seed) {
-    // K (row image), V (transposed-read image), the key-padding mask row (additive, fp32)
-    __shared__ __attribute__((aligned(16))) char smem[2 * FS * ROWB + FS * 4];
-    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+                                                            float p_drop, uint64_t seed, int BH) {
+    // persistent: a workgroup walks (b, h) = blockIdx.x, + gridDim.x, ...; the next pair's K / V rows,
+    // mask entry and Q fragments are loaded into registers while the current pair computes, and
+    // staged into the other half of the double-buffered LDS images (the single-pair version
+    // waited out every pair's loads: ~40 % of its wave time)
+    // per buffer: K (row image), V (transposed-read image), the key-padding mask row (fp32)
+    constexpr int BUF = 2 * FS * ROWB + FS * 4;
+    __shared__ __attribute__((aligned(16))) char smem_all[2 * BUF];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
-    const bf16_t* qb = qkv + (long)b * S * rs + h * D;
-    const bf16_t* kb = qb + H * D;
-    const bf16_t* vb = qb + 2 * H * D;
-    char* sK = smem;
-    char* sV = smem + FS * ROWB;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (tid >> 3) + 64 * i, c = tid & 7;
-        const bool ok = r < S;
-        const int rr = ok ? r : 0;
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
-        const uint4 v4 = *reinterpret_cast<const uint4*>(vb + (long)rr * rs + c * 8);
-        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = ok ? k4 : z;
-        *reinterpret_cast<uint4*>(sV + lds_off<true>(r, c)) = ok ? v4 : z;
-    }
     const int myq = 16 * w + (lane & 15);
     const bool qok = myq < S;
-    bf16x8 qf[2];
-    {
+    // next pair, in registers (plain arrays: a struct copy went through scratch)
+    uint4 nk4[2], nv4[2];
+    float nm = 0.f;
+    bf16x8 nq[2], qf[2];
+    auto fetch = [&](int bhp) __attribute__((always_inline)) {
+        const int bp = bhp / H, hp = bhp - bp * H;
+        const bf16_t* qb = qkv + (long)bp * S * rs + hp * D;
+        const bf16_t* kb = qb + H * D;
+        const bf16_t* vb = qb + 2 * H * D;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int r = (tid >> 3) + 64 * i, c = tid & 7;
+            const int rr = r < S ? r : 0;
+            nk4[i] = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
+            nv4[i] = *reinterpret_cast<const uint4*>(vb + (long)rr * rs + c * 8);
+        }
+        if (MASK) nm = tid < FS ? mask[(long)bp * S + (tid < S ? tid : 0)] : 0.f;
         const bf16_t* qr = qb + (long)(qok ? myq : 0) * rs;
-        qf[0] = load_frag_global(qr, 0);
-        qf[1] = load_frag_global(qr, 1);
-    }
-    const float c2 = scale * LOG2E;
-    const float* mrow = MASK ? mask + (long)b * S : nullptr;
-    // the mask row goes through LDS with K and V: read per score block from global, its
-    // loads sat between the QK MFMAs and the softmax, each waited for on its own
-    float* sM = reinterpret_cast<float*>(smem + 2 * FS * ROWB);
-    if (MASK && tid < FS) sM[tid] = tid < S ? mrow[tid] : 0.f;
+        nq[0] = load_frag_global(qr, 0);
+        nq[1] = load_frag_global(qr, 1);
+    };
+    auto stage = [&](char* smem) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int r = (tid >> 3) + 64 * i, c = tid & 7;
+            const bool ok = r < S;
+            *reinterpret_cast<uint4*>(smem + lds_off<false>(r, c)) = zero_unless(ok, nk4[i]);
+            *reinterpret_cast<uint4*>(smem + FS * ROWB + lds_off<true>(r, c)) = zero_unless(ok, nv4[i]);
+        }
+        if (MASK && tid < FS) reinterpret_cast<float*>(smem + 2 * FS * ROWB)[tid] = tid < S ? nm : 0.f;
+        qf[0] = nq[0];
+        qf[1] = nq[1];
+    };
+    int bh = blockIdx.x;
+    if (bh >= BH) return;
+    fetch(bh);
+    stage(smem_all);
     __syncthreads();
+    for (int it = 0; bh < BH; ++it, bh += gridDim.x) {
+    const int nbh = bh + gridDim.x;
+    if (nbh < BH) fetch(nbh);
+    char* smem = smem_all + (it & 1) * BUF;
+    const int b = bh / H, h = bh - b * H;
+    char* sK = smem;
+    char* sV = smem + FS * ROWB;
+    const float c2 = scale * LOG2E;
+    float* sM = reinterpret_cast<float*>(smem + 2 * FS * ROWB);
     const int nblk = FULL ? 8 : (S + 15) / 16;
     // S^T blocks: lane holds s[blk][r] = score(q = myq, k = 16 blk + 4 g + r)
     f32x4 s[8];
@@ -606,15 +635,21 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
         for (int db = 0; db < 4; ++db)
             o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sV, 32 * st, 16 * db), pf, o[db], 0, 0, 0);
     }
-    if (!qok) return;
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-    bf16_t* orow = out + ((long)b * S + myq) * H * D + h * D;
+    if (qok) {
+        const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+        bf16_t* orow = out + ((long)b * S + myq) * H * D + h * D;
 #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-        float v[4] = {o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv};
-        store4(orow + 16 * db + 4 * g, v);
+        for (int db = 0; db < 4; ++db) {
+            float v[4] = {o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv};
+            store4(orow + 16 * db + 4 * g, v);
+        }
+        if (g == 0) lse[(long)bh * S + myq] = (mx + log2f(lsum)) / LOG2E;
     }
-    if (g == 0) lse[(long)bh * S + myq] = (mx + log2f(lsum)) / LOG2E;
+    // the next pair into the other buffer (last read by the previous pair, before the barrier
+    // that ended it); the barrier below publishes it
+    if (nbh < BH) stage(smem_all + ((it + 1) & 1) * BUF);
+    __syncthreads();
+    }
 }
 
 // ============================================================ fused backward, S <= 128
@@ -667,13 +702,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
         const int r = (tid >> 3) + 64 * i, c = tid & 7;
         const bool ok = r < S;
         const int rr = ok ? r : 0;
-        const uint4 z = make_uint4(0, 0, 0, 0);
         const uint4 q4 = *reinterpret_cast<const uint4*>(qb + (long)rr * rs + c * 8);
         const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
         const uint4 o4 = *reinterpret_cast<const uint4*>(dob + (long)rr * ors + c * 8);
-        *reinterpret_cast<uint4*>(sQ + lds_off<false>(r, c)) = ok ? q4 : z;
-        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = ok ? k4 : z;
-        *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = ok ? o4 : z;
+        *reinterpret_cast<uint4*>(sQ + lds_off<false>(r, c)) = zero_unless(ok, q4);
+        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = zero_unless(ok, k4);
+        *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = zero_unless(ok, o4);
     }
     {
         // delta[q] = sum_d dO[q][d] O[q][d]: 4 threads per query, 16 d each
@@ -860,6 +894,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
 }  // namespace
 
 namespace {
+int num_cus() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
 // DDL_ATTN_FUSED_BWD=0: the tiled forward and two-kernel backward for every S (A/B timing, tests)
 bool fused_bwd_enabled() {
     static const bool on = [] {
@@ -875,7 +918,8 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
                          float p_drop, uint64_t seed, hipStream_t st) {
     if (S <= FS && fused_bwd_enabled()) {
         const bool full = S == FS, msk = mask != nullptr, drp = p_drop > 0.f;
-#define FWD_SHORT(F, M, D) attn_fwd_short_k<F, M, D><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed)
+        const int grid = std::min(B * H, 2 * num_cus());   // persistent: two workgroups per CU
+#define FWD_SHORT(F, M, D) attn_fwd_short_k<F, M, D><<<grid, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed, B * H)
         if (full) {
             if (msk) { if (drp) FWD_SHORT(true, true, true); else FWD_SHORT(true, true, false); }
             else { if (drp) FWD_SHORT(true, false, true); else FWD_SHORT(true, false, false); }
