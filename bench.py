@@ -7,6 +7,16 @@ W untimed warm-up steps, then EXACTLY K optimizer steps timed between
 barrier + device synchronisation on both sides; the max over ranks is the step
 time.  Rank 0 prints ONE JSON line on stdout (everything else goes to stderr).
 
+``python bench.py --gpus N`` with N > 1 and no launcher environment (no
+``WORLD_SIZE``) launches the N ranks itself: N child processes of this script with
+the torchrun variables set, started BEFORE anything in the parent touches the GPU
+(the parent never imports torch); the parent relays rank 0's JSON line and exits
+with the first failing child's code (the others are terminated).
+
+``--native stock`` measures the stock PyTorch-ROCm arm instead: plain nn.Conv2d /
+nn.BatchNorm2d / nn.Linear / SDPA models under bf16 autocast with fused torch
+optimizers and torch DistributedDataParallel (``baselines/stock.py``).
+
 Workload (BASELINE.json:8,9): ResNet-50 bf16 data-parallel training on synthetic
 ImageNet-shape batches (NHWC 224x224, 1000 classes, SGD-momentum, fp32 master
 weights), random-init weights; weak scaling (fixed per-GPU batch).  BERT-base
@@ -25,7 +35,49 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def self_launch(n: int) -> int:
+    """Run this script as ``n`` local ranks (one per GPU) and relay rank 0's stdout."""
+    import socket
+    import subprocess
+    import tempfile
+    import time
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"[bench] rank {procs.index(p)} exited with {code}; stopping the others")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    out.seek(0)
+    sys.stdout.write(out.read())
+    sys.stdout.flush()
+    return rc
+
+
 def run_one(model: str, args, world: int):
+    if args.native == "stock":
+        from databricks_distributed_deep_learning_amd.baselines import run_stock
+        batch = (args.batch or 256) if model == "resnet50" else (args.bert_batch or 128)
+        return run_stock(model, batch, args.steps, args.warmup, seq_len=128, bucket_mb=args.bucket_mb)
     from databricks_distributed_deep_learning_amd.config import get_preset
     from databricks_distributed_deep_learning_amd.training.loop import Trainer
     if model == "resnet50":
@@ -49,7 +101,9 @@ def main() -> int:
     ap.add_argument("--model", default="both", choices=["both", "resnet50", "bert_base"])
     ap.add_argument("--batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
     ap.add_argument("--bert-batch", type=int, default=0, help="BERT-base per-GPU batch (default 128)")
-    ap.add_argument("--native", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--native", default="auto", choices=["auto", "on", "off", "stock"],
+                    help="auto/on: HIP kernels; stock: plain PyTorch-ROCm + torch DDP arm; "
+                         "off: the framework's CPU-oracle ops (correctness reference, not a baseline)")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--zero", action="store_true", help="ZeRO-1: shard fp32 master + optimizer state over ranks")
     ap.add_argument("--sync-bn", action="store_true", help="SyncBatchNorm (CV models)")
@@ -59,6 +113,8 @@ def main() -> int:
     # the first step times GEMM kernel candidates per shape (ops/_native_gemm.py);
     # it must never land inside the timed region
     args.warmup = max(1, args.warmup)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args.gpus)
 
     import torch
     from databricks_distributed_deep_learning_amd.parallel import dist as ddist
@@ -67,6 +123,7 @@ def main() -> int:
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     ddist.init(args.backend)
+    world = ddist.world_size()
     results = {}
     order = ["resnet50", "bert_base"] if args.model == "both" else [args.model]
     for m in order:
@@ -80,7 +137,7 @@ def main() -> int:
         "metric": "ResNet-50 images/sec (whole node)" if is_r50 else "BERT-base samples/sec (whole node)",
         "value": round(head["samples_per_sec"], 2),
         "unit": "images/s" if is_r50 else "samples/s",
-        "n_gpus": world,
+        "n_gpus": ddist.world_size(),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(head["ms_per_step"], 3),
@@ -96,7 +153,7 @@ def main() -> int:
             "seq_len": head["seq_len"],
             "image_size": 224 if is_r50 else None,
             "optimizer": head["optimizer"],
-            "parallelism": f"dp{world}",
+            "parallelism": f"dp{ddist.world_size()}",
             "native_kernels": head["native"],
             "grad_comm": head.get("comm"),
         },

@@ -60,6 +60,7 @@ class TrainConfig:
     seed: int = 1234
     log_every: int = 10
     log_file: str = ""               # JSONL metrics (rank 0)
+    phase_timing: bool = True        # fwd/bwd/comm_wait/opt HIP-event breakdown in the log + summary
     checkpoint_dir: str = ""
     checkpoint_every: int = 0
     resume: bool = False
@@ -67,6 +68,7 @@ class TrainConfig:
     fault_step: int = -1
     data: str = "synthetic"          # synthetic (Petastorm/Delta replacement)
     synthetic_pool: int = 4          # distinct device-resident batches cycled
+    pad_fraction: float = 0.0        # NLP: random right-padding up to this fraction (attention-mask path)
 
     # ---------------------------------------------------------------------
     @property

@@ -59,6 +59,13 @@ class SyntheticImageNet:
     def __len__(self):
         return self.steps_per_epoch
 
+    def state_dict(self):
+        """Loader position (checkpoint / resume replays the same batch sequence)."""
+        return {"index": self._i}
+
+    def load_state_dict(self, st) -> None:
+        self._i = int(st["index"])
+
 
 class SyntheticTokens:
     def __init__(self, batch_size: int, seq_len: int = 128, vocab_size: int = 30522, num_labels: int = 2,
@@ -93,6 +100,13 @@ class SyntheticTokens:
 
     def __len__(self):
         return self.steps_per_epoch
+
+    def state_dict(self):
+        """Loader position (checkpoint / resume replays the same batch sequence)."""
+        return {"index": self._i}
+
+    def load_state_dict(self, st) -> None:
+        self._i = int(st["index"])
 
 
 def shard_indices(n: int, rank: int, world: int, shuffle: bool = False, seed: int = 0, drop_last: bool = True):

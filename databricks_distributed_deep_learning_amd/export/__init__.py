@@ -203,7 +203,10 @@ def bench_runtimes(model: ResNet, x: torch.Tensor, iters: int = 50, warmup: int 
     ref_model = copy.deepcopy(model).float().to(device)
     with torch.no_grad():
         ref, ms = _timed(ref_model, x.float(), iters, warmup, device)
-    results["pytorch_eager_fp32"] = {"ms": ms, "top5": top5(ref, categories)}
+    t2 = ref.float().topk(2, dim=-1).values
+    results["pytorch_eager_fp32"] = {"ms": ms, "top5": top5(ref, categories),
+                                     "logit_absmax": float(ref.float().abs().max()),
+                                     "top12_margin": float((t2[..., 0] - t2[..., 1]).min())}
     # TorchScript trace of the fp32 model
     ts_path = os.path.join(workdir, "traced_resnet_model.pt")
     export_model(ref_model, x.float(), "torchscript", ts_path)

@@ -1,17 +1,17 @@
-"""Model zoo (N11): ResNet-18/34/50/101/152, BERT-base/large, ViT-B/16."""
+"""Model zoo (N11): ResNet-18/34/50/101/152, BERT-base/large (+ a tiny test size), ViT-B/16."""
 from __future__ import annotations
 
 import torch.nn as nn
 
 from .resnet import ResNet, resnet18, resnet34, resnet50, resnet101, resnet152  # noqa: F401
-from .bert import BertConfig, BertForSequenceClassification, bert_base, bert_large  # noqa: F401
+from .bert import BertConfig, BertForSequenceClassification, bert_base, bert_large, bert_tiny  # noqa: F401
 from .vit import ViTConfig, ViTForImageClassification, vit_b16  # noqa: F401
 from .layers import cast_params, convert_sync_batchnorm  # noqa: F401
 
 _REGISTRY = {
     "resnet18": resnet18, "resnet34": resnet34, "resnet50": resnet50,
     "resnet101": resnet101, "resnet152": resnet152,
-    "bert_base": bert_base, "bert_large": bert_large,
+    "bert_base": bert_base, "bert_large": bert_large, "bert_tiny": bert_tiny,
     "vit_b16": vit_b16,
 }
 

@@ -151,6 +151,15 @@ def bert_large(num_labels: int = 2, dropout: float = 0.1, **kw) -> BertForSequen
                                                           attention_probs_dropout_prob=dropout, **kw))
 
 
+def bert_tiny(num_labels: int = 2, dropout: float = 0.1, **kw) -> BertForSequenceClassification:
+    """2 layers, hidden 128, 2 heads: the BERT code path at test / smoke size."""
+    d = dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=512,
+             vocab_size=1024, max_position_embeddings=128)
+    d.update(kw)
+    return BertForSequenceClassification(BertConfig(num_labels=num_labels, hidden_dropout_prob=dropout,
+                                                    attention_probs_dropout_prob=dropout, **d))
+
+
 # ------------------------------------------------------------ HF conversion
 _HF_LAYER_MAP = {
     "attention.output.dense": "attn_out",

@@ -163,6 +163,9 @@ def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb
 # of a shape times every candidate into scratch outputs and caches the fastest;
 # the bench's warmup steps absorb this.  DDL_GEMM_TUNE=0 uses the static heuristic.
 _tuned: dict = {}
+# candidate timings behind each tuned choice (ms per call, this process): what
+# agree_across_ranks() pools so every data-parallel rank runs the same kernel plan
+_timings: dict = {}
 _NARROW_STATS = os.environ.get("DDL_TUNE_NARROW_STATS", "0") != "0"   # same-box A/B neutral: off
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
 # optional persistent cache (JSON): later processes skip the timing runs
@@ -199,6 +202,44 @@ def tuned_choices() -> dict:
     return dict(_tuned)
 
 
+def agree_across_ranks(group=None) -> int:
+    """Make every rank of ``group`` run the SAME kernel for every tuned GEMM signature.
+
+    Each rank times candidates on its own GPU during warm-up; independent choices can
+    differ (timer noise on close calls) and the slowest rank's plan then gates every
+    data-parallel step.  This all-gathers the per-candidate timings (a small object
+    collective on the host group -- call it between steps, never inside backward),
+    sums them over the ranks that tuned the signature and sets the argmin everywhere.
+    All ranks compute the same answer from the same gathered data.  Returns how many
+    choices changed on this rank (a caller re-runs a warm-up step when > 0: a changed
+    plan may route later GEMMs through signatures not tuned yet)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return 0
+    mine = {k: {f"{kind}:{s}": t for (kind, s), t in v.items()} for k, v in _timings.items()}
+    gathered = [None] * dist.get_world_size(group)
+    dist.all_gather_object(gathered, mine, group=group)
+    keys = set()
+    for g in gathered:
+        keys.update(g.keys())
+    changed = 0
+    for key in sorted(keys):
+        tot: dict = {}
+        for g in gathered:
+            for c, t in g.get(key, {}).items():
+                tot.setdefault(c, []).append(t)
+        n = max(len(v) for v in tot.values())
+        # only candidates every tuning rank timed compete (the same list on each rank)
+        best = min((sum(v), c) for c, v in tot.items() if len(v) == n)[1]
+        kind, s = best.split(":")
+        choice = (kind, int(s))
+        if _tuned.get(key) != choice:
+            changed += 1
+        _tuned[key] = choice
+    _save_cache()
+    return changed
+
+
 def _time_runs(run, reps: int) -> float:
     """Mean milliseconds per call over ``reps`` back-to-back launches."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -223,6 +264,7 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
             cands.append(("narrow", 1))
         cs_s = torch.empty_like(colstats)
     if len(cands) == 1:
+        _timings[key] = {cands[0]: 0.0}
         return cands[0]
     Cs = torch.empty_like(C)
     aux_s = aux
@@ -239,6 +281,7 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
             t = _time_runs(run, reps)
         timed.append((t, kind, s))
     timed.sort()
+    _timings[key] = {(kind, s): t for t, kind, s in timed}
     if len(timed) > 1 and timed[1][0] < 1.15 * timed[0][0]:
         # a close call: re-time the two leaders with more runs before committing
         final = []
@@ -248,6 +291,8 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
             reps = min(48, max(6, int(3.0 / max(timed[0][0], 1e-3))))
             final.append((_time_runs(run, reps), kind, s))
         final.sort()
+        for t, kind, s in final:
+            _timings[key][(kind, s)] = t
         return (final[0][1], final[0][2])
     return (timed[0][1], timed[0][2])
 

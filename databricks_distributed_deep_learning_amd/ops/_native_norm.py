@@ -31,8 +31,19 @@ def _bn_supported(C: int) -> bool:
 
 
 def _group_sum(row: torch.Tensor, group) -> None:
-    """In-place SUM all-reduce of a small fp32 row over the SyncBatchNorm group."""
+    """In-place SUM all-reduce of a small fp32 row over the SyncBatchNorm group.
+
+    When the data-parallel reducer drives the native RCCL engine over the whole world,
+    the row goes through that SAME engine (its communicator and comm stream, then the
+    compute stream waits for it): one communicator carries every collective issued
+    during backward, in the same program order on every rank."""
     import torch.distributed as dist
+    from ..parallel import comm as _comm
+    eng = _comm.active()
+    if eng is not None and row.is_cuda and (group is None or group is dist.group.WORLD
+                                            or dist.get_world_size(group) == eng.world):
+        eng.wait_upto(eng.all_reduce(row))
+        return
     dist.all_reduce(row, op=dist.ReduceOp.SUM, group=group)
 
 

@@ -120,8 +120,11 @@ class FlatOptimizer:
         if hi <= lo:
             return
         if self._native():
-            self._step_native(grad, self._range_scratch.setdefault(
-                "scale", torch.full((1,), float(grad_scale), dtype=torch.float32, device=grad.device)), (lo, hi))
+            s = self._range_scratch.get("scale")
+            if s is None:     # one device scalar per step, not one allocation + fill per bucket
+                s = self._range_scratch["scale"] = torch.full((1,), float(grad_scale), dtype=torch.float32,
+                                                              device=grad.device)
+            self._step_native(grad, s, (lo, hi))
         else:
             self._step_torch(grad[lo:hi].float() * grad_scale, lo, hi)
             if self.master is not None:

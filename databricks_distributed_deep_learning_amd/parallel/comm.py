@@ -47,6 +47,23 @@ class CommError(RuntimeError):
     pass
 
 
+# The engine the data-parallel reducer of this process drives (set by DataParallel).
+# Other in-backward collectives (SyncBatchNorm statistics) go through the SAME
+# communicator and stream, so only one RCCL communicator carries traffic while
+# gradient buckets are in flight: two communicators whose kernels interleave in
+# different orders on different ranks can deadlock once the CUs are full.
+_ACTIVE: Optional["NativeComm"] = None
+
+
+def set_active(engine: Optional["NativeComm"]) -> None:
+    global _ACTIVE
+    _ACTIVE = engine
+
+
+def active() -> Optional["NativeComm"]:
+    return _ACTIVE
+
+
 def _fn(name):
     lib = _lib.get()
     f = getattr(lib, name)
@@ -102,7 +119,6 @@ class NativeComm:
         dist.broadcast_object_list(obj, src=src, group=group)
         if isinstance(obj[0], str):
             raise CommError(obj[0])
-        self._seq = 0          # all-reduces issued (the engine's numbering for wait_upto)
         self._h = _fn("ddl_comm_create")(path, obj[0], self.world, self.rank, self.device.index)
         ok = torch.tensor([1 if self._h else 0], device=self.device)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
@@ -116,13 +132,15 @@ class NativeComm:
 
     def all_reduce(self, t: torch.Tensor, average: bool = False) -> int:
         """In-place all-reduce of a contiguous GPU tensor on the comm stream (async).
-        Returns its sequence number for :meth:`wait_upto` (0: nothing was issued)."""
+        Returns its sequence number for :meth:`wait_upto` (0: nothing was issued).
+
+        The number is read back from the engine (``ddl_comm_stats``), never mirrored in
+        Python: a call that fails after the engine counted it must not leave a stale
+        count behind that would make a later ``wait_upto`` wait on an older collective."""
         assert t.is_cuda and t.is_contiguous()
         self._check(_fn("ddl_comm_allreduce")(self._h, t.data_ptr(), t.numel(), _DTYPES[t.dtype], int(average),
                                               _stream()), "all_reduce")
-        if t.numel() > 0:
-            self._seq += 1
-        return self._seq if t.numel() > 0 else 0
+        return self.collectives_launched if t.numel() > 0 else 0
 
     def all_reduce_many(self, ts: Sequence[torch.Tensor], average: bool = False) -> int:
         if not ts:
@@ -133,8 +151,7 @@ class NativeComm:
         counts = (L * len(ts))(*[t.numel() for t in ts])
         self._check(_fn("ddl_comm_allreduce_many")(self._h, bufs, counts, len(ts), _DTYPES[dt], int(average),
                                                    _stream()), "all_reduce_many")
-        self._seq += sum(1 for t in ts if t.numel() > 0)
-        return self._seq
+        return self.collectives_launched
 
     def wait_upto(self, seq: int) -> None:
         """Current (compute) stream waits for all-reduce number ``seq`` and every earlier
@@ -168,9 +185,14 @@ class NativeComm:
         return int(_fn("ddl_comm_stats")(self._h, 0))
 
     def close(self, abort: bool = False) -> None:
+        """Destroy the communicator.  ``abort=True`` (``ncclCommAbort``) is the failure
+        path: it returns without waiting for peers and unblocks collectives stuck on a
+        rank that died, so this rank can raise instead of hanging until the timeout."""
         if getattr(self, "_h", None):
             _fn("ddl_comm_destroy")(self._h, int(abort))
             self._h = None
+        if _ACTIVE is self:
+            set_active(None)
 
     # no __del__: destroying a communicator during interpreter teardown can block
     # on peers that already exited; process exit releases it.

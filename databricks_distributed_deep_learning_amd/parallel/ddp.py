@@ -68,7 +68,7 @@ class DataParallel(nn.Module):
                  bucket_mb: float = 25.0, first_bucket_mb: float = 4.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast_buffers: bool = False,
                  accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True,
-                 comm: str = "auto"):
+                 comm: str = "auto", backward_passes_per_step: int = 1):
         super().__init__()
         self.module = module
         self.arena = arena if arena is not None else ParamArena(list(module.named_parameters()))
@@ -78,6 +78,10 @@ class DataParallel(nn.Module):
         self.reduce_dtype = reduce_dtype or self.arena.dtype
         self.accumulate_fp32 = accumulate_fp32
         self._sync = True
+        # Horovod semantics: a parameter's gradient is communicated on its k-th arrival
+        # (k backward passes accumulate locally in the arena first); see _make_hook
+        self.passes = max(1, int(backward_passes_per_step))
+        self._arrivals: dict = {}
         self._acc32: Optional[torch.Tensor] = None
         self._acc_active = False
         if broadcast_init and self.world > 1:
@@ -100,6 +104,9 @@ class DataParallel(nn.Module):
             elif comm == "native":
                 raise RuntimeError("comm='native' needs CUDA tensors, the native library and the nccl backend")
         self.comm = "native" if self.native is not None else "torch"
+        if self.native is not None and hasattr(self.native, "world"):
+            from . import comm as _comm
+            _comm.set_active(self.native)   # SyncBatchNorm rides the same communicator
         self.buckets = self._build_buckets(bucket_mb, first_bucket_mb)
         self._entry_bucket = {}
         for b in self.buckets:
@@ -114,7 +121,7 @@ class DataParallel(nn.Module):
             self._hooks.append(e.param.register_post_accumulate_grad_hook(hook))
             # native backward kernels accumulate straight into the arena view and call this
             e.param._ddl_main_grad = self.arena.grad[e.offset:e.offset + e.numel].view(e.shape)
-            e.param._ddl_grad_ready = (lambda h=hook, prm=e.param: h(prm))
+            e.param._ddl_grad_ready = (lambda h=hook, prm=e.param: h(prm, native=True))
         self._reset()
 
     # ------------------------------------------------------------------
@@ -146,11 +153,37 @@ class DataParallel(nn.Module):
             b.seq = 0
             b.eager_done = False
         self._order: List[Bucket] = []       # buckets in all-reduce launch order
+        self._arrivals = {}
+        self._native_seen: set = set()
 
     def _make_hook(self, ei: int):
-        def hook(_p):
+        # Ordering rule for native backward ops (grad_sink / grad_ready): an op calls
+        # grad_ready(param) only AFTER the last kernel of this backward that reads the
+        # parameter (dgrad before wgrad; BN / LN read gamma before reporting it).  With the
+        # eager optimizer on, the bucket's update runs on a side stream from that point
+        # and rewrites the weight.
+        def hook(_p, native: bool = False):
+            # a native backward reports through grad_ready (native=True) and autograd's
+            # post-accumulate hook then fires for the same parameter (its returned gradient
+            # is None): the second, autograd, report is the expected echo
             if not self._sync:
                 return
+            if native:
+                if ei in self._native_seen and self._eager_cb is not None and \
+                        self.buckets[self._entry_bucket[ei]].launched:
+                    # two native uses of one weight in one step: the side stream may already be
+                    # rewriting it while the second use's backward still reads it -- refuse
+                    raise RuntimeError(
+                        f"parameter {self.arena.entries[ei].name} reported its gradient twice in one step "
+                        "with the eager optimizer on; turn eager_optimizer off for this model")
+                self._native_seen.add(ei)
+            elif ei in self._native_seen:
+                return
+            if self.passes > 1:
+                n = self._arrivals.get(ei, 0) + 1
+                self._arrivals[ei] = n
+                if n < self.passes:          # accumulate locally; communicate on pass k
+                    return
             b = self.buckets[self._entry_bucket[ei]]
             if ei in b.grads_seen:   # parameter used twice in one graph: count once
                 return

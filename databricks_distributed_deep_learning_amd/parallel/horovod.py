@@ -144,10 +144,13 @@ class _DistributedOptimizer:
 
         class _Holder(torch.nn.Module):
             pass
-        self._reducer = DataParallel(_Holder(), arena=self.arena, bucket_mb=bucket_mb, broadcast_init=False)
+        # backward_passes_per_step = k: each gradient is all-reduced on its k-th arrival
+        # (the reducer counts per parameter, as Horovod does); passes 1..k-1 accumulate
+        # locally into the arena and launch nothing
+        self._reducer = DataParallel(_Holder(), arena=self.arena, bucket_mb=bucket_mb, broadcast_init=False,
+                                     backward_passes_per_step=backward_passes_per_step)
         self.backward_passes_per_step = backward_passes_per_step
         self.op = op
-        self._passes = 0
 
     @property
     def param_groups(self):

@@ -8,6 +8,11 @@ its GPU, initialises the process group (RCCL on GPU, gloo on CPU), runs
 re-raised in the parent with the child's traceback and the surviving siblings
 are terminated (failure detection).
 
+``train_fn`` may be defined in a notebook cell or an interactive ``__main__``:
+the function and its arguments are serialised by value with ``cloudpickle``
+(when importable; plain pickle otherwise) and rebuilt in each child before the
+call, the way TorchDistributor ships a notebook-local function to its workers.
+
 If the caller is already inside a torchrun / launcher world (``RANK`` set and
 ``WORLD_SIZE`` matches) the function runs in-process instead of re-spawning, so
 the same notebook ``train()`` works under ``python -m torch.distributed.run``.
@@ -38,7 +43,28 @@ class ChildFailed(RuntimeError):
         self.child_traceback = tb
 
 
-def _child_entry(rank: int, world: int, fn: Callable, args, kwargs, env: Dict[str, str],
+def _dumps(obj) -> bytes:
+    """By-value serialisation of a callable + arguments: cloudpickle pickles functions and
+    classes defined in ``__main__`` / a notebook cell (plain pickle only references them by
+    name, which a spawned child cannot resolve)."""
+    try:
+        import cloudpickle
+    except ImportError:      # pragma: no cover - cloudpickle ships in this image
+        return pickle.dumps(obj)
+    try:
+        return cloudpickle.dumps(obj)
+    except Exception as e:  # noqa: BLE001
+        # cloudpickle trips over some extension objects a function's code merely names
+        # (e.g. a local ``from pkg import ops`` next to a global ``torch``: it drags in
+        # ``torch.ops``).  By-reference pickling still works for functions of an
+        # importable module or of a script file (spawned children re-import it).
+        try:
+            return pickle.dumps(obj)
+        except Exception:
+            raise e from None
+
+
+def _child_entry(rank: int, world: int, payload: bytes, env: Dict[str, str],
                  result_q, init_pg: bool, backend: str, use_gpu: bool) -> None:
     os.environ.update(env)
     os.environ["RANK"] = str(rank)
@@ -46,6 +72,7 @@ def _child_entry(rank: int, world: int, fn: Callable, args, kwargs, env: Dict[st
     os.environ["WORLD_SIZE"] = str(world)
     os.environ["LOCAL_WORLD_SIZE"] = str(world)
     try:
+        fn, args, kwargs = pickle.loads(payload)   # cloudpickle output loads with pickle
         if init_pg:
             ddist.init(backend=backend, use_gpu=use_gpu)
         out = fn(*args, **kwargs)
@@ -122,12 +149,13 @@ class Distributor:
             "DDL_LAUNCHER_CHILD": "1",
         }
         env.update(self.extra_env)
+        payload = _dumps((fn, args, kwargs))
         ctx = mp.get_context("spawn")
         q = ctx.SimpleQueue()
         procs = []
         for r in range(self.num_processes):
             p = ctx.Process(target=_child_entry,
-                            args=(r, self.num_processes, fn, args, kwargs, env, q,
+                            args=(r, self.num_processes, payload, env, q,
                                   self.init_process_group, self.backend, self.use_gpu),
                             daemon=False)
             p.start()

@@ -29,8 +29,9 @@ from ..optim import LRSchedule, ParamArena, build_optimizer
 from ..parallel import dist as ddist
 from ..parallel.ddp import DataParallel
 from ..utils import checkpoint as ckpt
+from ..utils import profiling
 from ..utils.faults import maybe_fail
-from ..utils.metrics import JsonlLogger, StepTimer, ThroughputMeter, memory_stats
+from ..utils.metrics import JsonlLogger, PhaseTimer, StepTimer, ThroughputMeter, memory_stats
 
 DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
 
@@ -78,8 +79,9 @@ class Trainer:
         self.loader = self._make_loader()
         self.step = 0
         self.logger = JsonlLogger(cfg.log_file, enabled=ddist.is_main())
+        self.phases = PhaseTimer(self.device, enabled=cfg.phase_timing)
         if cfg.resume and cfg.checkpoint_dir and ckpt.latest(cfg.checkpoint_dir):
-            meta = ckpt.load(cfg.checkpoint_dir, model, self.opt)
+            meta = ckpt.load(cfg.checkpoint_dir, model, self.opt, loader=self.loader)
             self.step = int(meta["step"])
 
     # ------------------------------------------------------------------
@@ -88,8 +90,10 @@ class Trainer:
         if self.task == "cv":
             return SyntheticImageNet(c.batch_size, c.image_size, c.num_classes, self.device, self.dtype,
                                      rank=self.rank, seed=c.seed, pool=c.synthetic_pool)
-        return SyntheticTokens(c.batch_size, c.seq_len, c.vocab_size, c.num_classes, self.device,
-                               rank=self.rank, seed=c.seed, pool=c.synthetic_pool)
+        mc = getattr(self.model, "config", None)
+        vocab = min(c.vocab_size, getattr(mc, "vocab_size", c.vocab_size))
+        return SyntheticTokens(c.batch_size, c.seq_len, vocab, c.num_classes, self.device,
+                               rank=self.rank, seed=c.seed, pool=c.synthetic_pool, pad_fraction=c.pad_fraction)
 
     def _auto_batch(self) -> int:
         from ..utils.memory import fit_batch_size
@@ -115,7 +119,12 @@ class Trainer:
         return loss
 
     def train_step(self) -> torch.Tensor:
+        """One optimizer step: grad_accum micro-steps (communication on the last), then
+        the fused optimizer.  Phases are bracketed by roctx ranges (``DDL_ROCTX=1``, seen
+        by ``rocprofv3 --marker-trace``) and HIP-event marks (:class:`PhaseTimer`)."""
         c = self.cfg
+        ph = self.phases
+        ph.begin()
         self.ddp.zero_grad()
         loss_sum = None
         scale = 1.0 / (self.world * c.grad_accum)
@@ -127,25 +136,62 @@ class Trainer:
                 self.opt.begin_step(lr=self.sched(self.step))
                 self.ddp.set_eager(lambda g, lo, hi: self.opt.step_range(g, scale, lo, hi))
             with ctx:
-                loss = self.loss_fn(batch)
-                loss.backward()
+                with profiling.range("fwd"):
+                    loss = self.loss_fn(batch)
+                ph.mark("fwd")
+                with profiling.range("bwd"):
+                    loss.backward()
+                ph.mark("bwd")
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
         if self.eager_optimizer:
-            self.ddp.finish()               # joins the side stream (or runs the remaining updates)
-            self.ddp.set_eager(None)
-            self.opt.end_step()
+            with profiling.range("comm_wait+opt"):
+                self.ddp.finish()               # joins the side stream (or runs the remaining updates)
+                self.ddp.set_eager(None)
+                self.opt.end_step()
+            ph.mark("comm_wait+opt")
         elif self.overlap_optimizer:
             # each bucket's optimizer update starts as soon as ITS all-reduce is done, so
             # the last buckets' rings (BERT's 68 MB embedding bucket) run under the update
             # of everything else instead of in front of it
-            self.opt.begin_step(lr=self.sched(self.step))
-            self.ddp.finish(on_ready=lambda g, lo, hi: self.opt.step_range(g, scale, lo, hi))
-            self.opt.end_step()
+            with profiling.range("comm_wait+opt"):
+                self.opt.begin_step(lr=self.sched(self.step))
+                self.ddp.finish(on_ready=lambda g, lo, hi: self.opt.step_range(g, scale, lo, hi))
+                self.opt.end_step()
+            ph.mark("comm_wait+opt")
         else:
-            grad = self.ddp.finish()
-            self.opt.step(grad, grad_scale=scale, lr=self.sched(self.step))
+            with profiling.range("comm_wait"):
+                grad = self.ddp.finish()
+            ph.mark("comm_wait")
+            with profiling.range("opt"):
+                self.opt.step(grad, grad_scale=scale, lr=self.sched(self.step))
+            ph.mark("opt")
+        ph.end_step()
         self.step += 1
         return loss_sum / c.grad_accum
+
+    def agree_kernel_plans(self, max_rounds: int = 3) -> None:
+        """Data-parallel ranks run identical GEMM kernel plans (ops/_native_gemm.py
+        ``agree_across_ranks``): a rank that tuned differently would gate every step.
+        A changed plan can route GEMMs through signatures not tuned yet, so one more
+        untimed step runs and the agreement repeats (same count on every rank: every
+        rank computes the same answer)."""
+        if self.world == 1 or not self.arena.flat.is_cuda:
+            return
+        from ..ops import _native_gemm
+        for _ in range(max_rounds):
+            if _native_gemm.agree_across_ranks() == 0:
+                return
+            self.train_step()
+
+    def _abort_comm(self) -> None:
+        """Failure path: abort the native RCCL communicator so collectives blocked on a
+        dead peer return and this rank exits instead of hanging until the timeout."""
+        eng = getattr(self.ddp, "native", None)
+        if eng is not None and hasattr(eng, "close"):
+            try:
+                eng.close(abort=True)
+            except Exception:  # noqa: BLE001 - already failing; keep the original error
+                pass
 
     @property
     def samples_per_step(self) -> int:
@@ -153,38 +199,64 @@ class Trainer:
 
     def run(self, steps: Optional[int] = None, warmup: Optional[int] = None,
             callback: Optional[Callable[[int, float], None]] = None) -> Dict[str, Any]:
+        try:
+            return self._run(steps, warmup, callback)
+        except BaseException:
+            self._abort_comm()
+            raise
+
+    def _global_loss(self, loss: torch.Tensor) -> float:
+        """Mean loss over ranks (collective C4; log points only)."""
+        v = float(loss)
+        if self.world > 1:
+            v = ddist.all_reduce_scalars([v], op="sum")[0] / self.world
+        return v
+
+    def _run(self, steps, warmup, callback) -> Dict[str, Any]:
         c = self.cfg
         steps = c.steps if steps is None else steps
         warmup = c.warmup_steps if warmup is None else warmup
         self.model.train()
         for _ in range(warmup):
             self.train_step()
+        if warmup:
+            self.agree_kernel_plans()
+        self.phases.summary(reset=True)          # warm-up (and tuning) steps are not reported
         timer = StepTimer(self.device)
         meter = ThroughputMeter(self.samples_per_step)
         ddist.barrier()
         timer.start()
         t_seg = 0.0
-        last_loss = float("nan")
-        seg_steps = 0
+        last = None
         for i in range(steps):
             maybe_fail(self.step, c.fault_rank, c.fault_step)
             loss = self.train_step()
-            seg_steps += 1
-            if c.log_every and (i + 1) % c.log_every == 0 or i == steps - 1:
-                last_loss = float(loss)          # device sync only at log points
+            last = loss
+            if c.log_every and (i + 1) % c.log_every == 0 and i != steps - 1:
+                t_pause = timer.stop()            # log points are outside the timed region
+                t_seg += t_pause
+                gl = self._global_loss(loss)
                 if callback:
-                    callback(self.step, last_loss)
-                self.logger.log({"step": self.step, "loss": last_loss, "lr": self.opt.lr,
-                                 **memory_stats(self.device)})
+                    callback(self.step, gl)
+                self.logger.log({"step": self.step, "loss": gl, "lr": self.opt.lr,
+                                 **self.phases.summary(reset=True), **memory_stats(self.device)})
+                timer.start()
             if c.checkpoint_every and c.checkpoint_dir and self.step % c.checkpoint_every == 0:
                 t_pause = timer.stop()
                 t_seg += t_pause
-                ckpt.save(c.checkpoint_dir, self.model, self.opt, self.step, c.to_dict())
+                self.save_checkpoint()
                 timer.start()
         ddist.barrier()
         t_seg += timer.stop()
         meter.update(t_seg, steps)
         t_max = ddist.all_reduce_scalars([t_seg], op="max")[0]
+        last_loss = self._global_loss(last) if last is not None else float("nan")
+        phases = self.phases.summary(reset=True)
+        if last is not None:
+            if callback:
+                callback(self.step, last_loss)
+            self.logger.log({"step": self.step, "loss": last_loss, "lr": self.opt.lr, **phases,
+                             **memory_stats(self.device)})
         summary = {
             "model": c.model, "task": self.task, "world_size": self.world, "steps": steps, "warmup": warmup,
             "per_rank_batch": c.batch_size, "grad_accum": c.grad_accum, "global_batch": self.samples_per_step,
@@ -194,12 +266,15 @@ class Trainer:
             "samples_per_sec": self.samples_per_step * steps / t_max if t_max > 0 else 0.0,
             "final_loss": last_loss, "native": ops.native_mode(),
             "buckets_mb": [round(b, 2) for b in self.ddp.bucket_sizes_mb()],
-            "comm": self.ddp.comm,
+            "comm": self.ddp.comm, "phases_ms": {k: round(v, 3) for k, v in phases.items()},
         }
         summary.update(memory_stats(self.device))
         if c.checkpoint_dir and not c.checkpoint_every:
-            ckpt.save(c.checkpoint_dir, self.model, self.opt, self.step, c.to_dict())
+            self.save_checkpoint()
         return summary
+
+    def save_checkpoint(self) -> None:
+        ckpt.save(self.cfg.checkpoint_dir, self.model, self.opt, self.step, self.cfg.to_dict(), loader=self.loader)
 
 
 def train(cfg: Optional[TrainConfig] = None, **overrides) -> Dict[str, Any]:

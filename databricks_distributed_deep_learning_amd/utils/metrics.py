@@ -57,6 +57,65 @@ class EventTimer:
         return self.a.elapsed_time(self.b)
 
 
+class PhaseTimer:
+    """Per-phase step-time breakdown (fwd / bwd / comm_wait / opt).
+
+    ``mark(name)`` closes the phase that ran since the previous mark.  On the GPU a
+    mark is one HIP event recorded on the compute stream (no host sync, so the timed
+    loop is not perturbed); the events are resolved only in :meth:`summary`, at log
+    points.  ``comm_wait`` is what the compute stream spent waiting for the last
+    gradient all-reduces after its own backward work -- the EXPOSED communication.
+    On the CPU marks are host clock readings."""
+
+    def __init__(self, device: torch.device, enabled: bool = True):
+        self.cuda = device.type == "cuda"
+        self.enabled = enabled
+        self._pending: list = []       # per step: [(name, event or time), ...]
+        self._cur: list = []
+        self.totals: Dict[str, float] = {}
+        self.steps = 0
+
+    def _stamp(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def begin(self) -> None:
+        if self.enabled:
+            self._cur = [("", self._stamp())]
+
+    def mark(self, name: str) -> None:
+        if self.enabled and self._cur:
+            self._cur.append((name, self._stamp()))
+
+    def end_step(self) -> None:
+        if self.enabled and len(self._cur) > 1:
+            self._pending.append(self._cur)
+        self._cur = []
+
+    def _resolve(self) -> None:
+        for marks in self._pending:
+            for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
+                if self.cuda:
+                    b.synchronize()
+                    ms = a.elapsed_time(b)
+                else:
+                    ms = 1000.0 * (b - a)
+                self.totals[name] = self.totals.get(name, 0.0) + ms
+            self.steps += 1
+        self._pending = []
+
+    def summary(self, reset: bool = False) -> Dict[str, float]:
+        """Mean milliseconds per step of each phase since the last reset."""
+        self._resolve()
+        out = {f"{k}_ms": v / max(1, self.steps) for k, v in self.totals.items()}
+        if reset:
+            self.totals, self.steps = {}, 0
+        return out
+
+
 class ThroughputMeter:
     def __init__(self, items_per_step: int):
         self.items_per_step = items_per_step

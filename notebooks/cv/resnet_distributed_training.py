@@ -19,7 +19,8 @@ from databricks_distributed_deep_learning_amd import get_preset
 from databricks_distributed_deep_learning_amd.parallel import Distributor
 from databricks_distributed_deep_learning_amd.training import train
 
-SMOKE = os.environ.get("DDL_NOTEBOOK_SMOKE") == "1"
+SMOKE = os.environ.get("DDL_NOTEBOOK_SMOKE") == "1"          # CPU / gloo, 2 ranks
+GPU_SMOKE = os.environ.get("DDL_NOTEBOOK_SMOKE") == "gpu"    # the GPU branch, a few small steps
 
 # COMMAND ----------
 
@@ -29,6 +30,8 @@ if SMOKE or not torch.cuda.is_available():
     nproc, use_gpu = 2, False
 else:
     cfg = get_preset("resnet50_ddp", steps=50, warmup_steps=5)
+    if GPU_SMOKE:
+        cfg = cfg.replace(batch_size=32, steps=3, warmup_steps=1, log_every=1)
     nproc, use_gpu = torch.cuda.device_count(), True
 print(cfg)
 

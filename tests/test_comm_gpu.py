@@ -108,6 +108,38 @@ def test_sync_batchnorm_native_world1(pg, fused_stats):
         torch.testing.assert_close(a, c, rtol=2e-2, atol=2e-2)
 
 
+def test_sync_batchnorm_rides_the_reducer_engine(pg):
+    """With the reducer's native engine active, SyncBatchNorm's statistic all-reduces go
+    through that same communicator / comm stream (one RCCL communicator carries every
+    in-backward collective) and give the same result as the torch process group."""
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.parallel import comm as C
+    torch.manual_seed(4)
+    x = torch.randn(8, 14, 14, 64, device=pg).to(torch.bfloat16)
+    g = (torch.rand(64, device=pg) + 0.5).to(torch.bfloat16)
+    b = (torch.randn(64, device=pg) * 0.1).to(torch.bfloat16)
+    dy = torch.randn(8, 14, 14, 64, device=pg).to(torch.bfloat16)
+    eng = C.NativeComm()
+    outs = []
+    try:
+        for active in (None, eng):
+            C.set_active(active)
+            before = eng.collectives_launched
+            xs, gs, bs = (t.clone().requires_grad_(True) for t in (x, g, b))
+            rm, rv = torch.zeros(64, device=pg), torch.ones(64, device=pg)
+            z = ops.batch_norm(xs, gs, bs, rm, rv, True, 0.1, 1e-5, True, None, group=dist.group.WORLD)
+            z.backward(dy)
+            torch.cuda.synchronize()
+            outs.append((z.float(), xs.grad.float(), gs.grad.float(), rm, rv))
+            # forward statistics + backward coefficients: two all-reduces on the engine when active
+            assert eng.collectives_launched - before == (2 if active is not None else 0)
+    finally:
+        C.set_active(None)
+        eng.close()
+    for a, c in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a, c, rtol=1e-2, atol=1e-2)
+
+
 def test_reducer_native_per_bucket_ready(pg):
     """finish(on_ready=...) with the native engine: the compute stream waits for each
     bucket's own all-reduce (wait_upto on the engine's completion ring), and a

@@ -39,3 +39,16 @@ def test_bench_runtimes_gpu(tmp_path):
     rt = rep["runtimes"]
     assert "native_bf16_folded_hipgraph" in rt
     print({k: round(v["ms"], 3) for k, v in rt.items()})
+    oracle = rt["pytorch_eager_fp32"]
+    # fp32 graph runtimes: the reference's allclose gate (cv/onnx:144, rtol 1e-5 / atol 1e-4)
+    for name in ("torchscript_fp32", "torch_export_fp32"):
+        assert rt[name]["allclose_ref_tol"] and rt[name]["top1_agrees"], (name, rt[name])
+    # bf16 native runtimes: within bf16 error of the fp32 oracle, and the same top-1 whenever
+    # the oracle's top-1 / top-2 margin exceeds that error
+    for name in ("native_bf16_eager", "native_bf16_folded", "native_bf16_folded_hipgraph"):
+        r = rt[name]
+        assert r["max_abs_err"] / oracle["logit_absmax"] < 5e-2, (name, r, oracle)
+        if oracle["top12_margin"] > 2 * r["max_abs_err"]:
+            assert r["top1_agrees"], (name, r, oracle)
+    # the replayed graph is the folded model, bit for bit
+    assert rt["native_bf16_folded_hipgraph"]["max_abs_err"] == rt["native_bf16_folded"]["max_abs_err"]
