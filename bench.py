@@ -86,7 +86,8 @@ def run_one(model: str, args, world: int):
         cfg = get_preset("bert_base_ddp", batch_size=args.bert_batch or 128, dropout=0.1)
     cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
                       bucket_mb=args.bucket_mb, backend=args.backend,
-                      zero_optimizer=args.zero, sync_bn=args.sync_bn)
+                      zero_optimizer=args.zero, sync_bn=args.sync_bn,
+                      phase_timing=os.environ.get("DDL_PHASE_TIMING", "1") != "0")
     tr = Trainer(cfg)
     s = tr.run()
     del tr
@@ -157,6 +158,7 @@ def main() -> int:
             "native_kernels": head["native"],
             "grad_comm": head.get("comm"),
         },
+        "phases_ms": head.get("phases_ms"),
     }
     if "bert_base" in results and is_r50:
         b = results["bert_base"]

@@ -675,7 +675,11 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
 // tile's loads instead of in a chip-wide burst between waves of blocks.
 // BNB: the BatchNorm-backward epilogue variant (its own instantiation, so the extra
 // registers it needs never weigh on the other epilogues)
-template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false>
+// EDGE = false: every tile is interior and the epilogue kind is one of the lean ones
+// (M, N multiples of 256 -- every BERT / ViT GEMM): the bounds-checked general epilogue
+// is not compiled in.  Its 64-bit per-site addresses were what spilled (35-72 VGPRs of
+// scratch in the persistent kernels); without it the NT kernel allocates spill-free.
+template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false, bool EDGE = true>
 __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
     // makes the compiler's LDS-DMA alias tracking wait vmcnt(0) before fragment reads)
@@ -896,7 +900,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                                              : vt + (int)gridDim.x;
             const bool next = vn < nwg;
             const int m0c = m0, n0c = n0, tm_c = tm;
-            const bool interior = m0c + TB <= p.M && n0c + TB <= p.N;
+            const bool interior = !EDGE || (m0c + TB <= p.M && n0c + TB <= p.N);
             // Store-behind: when this tile's epilogue issues a KNOWN number of vector-memory
             // ops (lean bf16 variant: one 8-byte store per site, +8 statistics stores), the
             // WHOLE next prologue (E and O halves) is issued first and only the E loads are
@@ -935,7 +939,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 epi_direct<EK_GELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_DGELU)
                 epi_direct<EK_DGELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
-            else
+            else if constexpr (EDGE)
                 epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             if (!next) {
                 if constexpr (DYN) break;    // the ticket slot's exit bookkeeping below the loop
@@ -1143,6 +1147,15 @@ bool direct_enabled() {
     return on;
 }
 
+// DDL_GEMM_LEAN=0 keeps the general-epilogue kernel for all-interior GEMMs too (A/B timing)
+bool edge_split_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_LEAN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // DDL_GEMM_DYNAMIC=0 keeps the static tile striding of the persistent grid (A/B timing)
 bool dynamic_enabled() {
     static const bool on = [] {
@@ -1247,8 +1260,16 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
             }
         }
         if (p.act == ACT_BNB) return -8;
-        if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true>), grid, dim3(NTH), 0, st, kp);
-        else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true>), grid, dim3(NTH), 0, st, kp);
+        // all tiles interior with a lean epilogue kind: the variant without the general epilogue
+        const bool lean = p.M % TB == 0 && p.N % TB == 0 && p.ek != EK_GEN && edge_split_enabled();
+        if (lean) {
+            if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true, false, false>), grid, dim3(NTH), 0, st, kp);
+            else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true, false, false>), grid, dim3(NTH), 0, st, kp);
+        } else if (ktail) {
+            hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true>), grid, dim3(NTH), 0, st, kp);
+        } else {
+            hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true>), grid, dim3(NTH), 0, st, kp);
+        }
     } else {
         if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, false>), grid, dim3(NTH), 0, st, kp);
         else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, false>), grid, dim3(NTH), 0, st, kp);

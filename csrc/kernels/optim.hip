@@ -2,10 +2,16 @@
 //
 // The whole model's parameters / gradients / optimizer state are flat arrays
 // with one layout (optim/arena.py), so a step is ONE launch over the arena.  A
-// block table int32[nblk][4] = (start, len, tensor_index, decay_flag) maps each
-// 256-thread block to <= 8192 contiguous elements of a single tensor, which
-// gives per-tensor hyper-parameters (weight-decay masks, LAMB trust ratios)
+// block table int32[nblk][4] = (start, len | decay << 30, tensor_index, param_delta)
+// maps each 256-thread block to <= 8192 contiguous elements of a single tensor,
+// which gives per-tensor hyper-parameters (weight-decay masks, LAMB trust ratios)
 // without per-tensor launches.  Each lane moves 8 elements per access.
+//
+// `start` indexes the optimizer's own (local) arrays -- gradient, fp32 master,
+// moments; the compute-dtype parameter copy is written at start + param_delta.
+// Unsharded, local == arena and the delta is 0; a ZeRO-1 rank owns one chunk per
+// gradient bucket, stored back to back locally, and each chunk's rows carry the
+// offset of that chunk in the arena.
 //
 // Gradients may be bf16 or fp32; the fp32 master weights are updated in place
 // and, when the model computes in bf16, the bf16 copy is written in the same
@@ -26,8 +32,10 @@ __global__ __launch_bounds__(OPT_NT) void sgd_k(const G* __restrict__ grad, floa
                                                  const int4* __restrict__ table, const float* __restrict__ scale_p,
                                                  float lr, float mu, float wd, int nesterov, int first) {
     const int4 e = table[blockIdx.x];
+    const int len = e.y & 0x3fffffff;
+    const bool dec = (e.y >> 30) & 1;
     const float scale = scale_p[0];
-    for (int k = threadIdx.x * 8; k < e.y; k += OPT_NT * 8) {
+    for (int k = threadIdx.x * 8; k < len; k += OPT_NT * 8) {
         const long i = (long)e.x + k;
         float g[8], p[8], b[8];
         load_grad8(grad, i, g);
@@ -36,7 +44,7 @@ __global__ __launch_bounds__(OPT_NT) void sgd_k(const G* __restrict__ grad, floa
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float d = g[j] * scale;
-            if (e.w) d += wd * p[j];
+            if (dec) d += wd * p[j];
             if (mu != 0.f) {
                 b[j] = first ? d : mu * b[j] + d;
                 d = nesterov ? d + mu * b[j] : b[j];
@@ -45,7 +53,7 @@ __global__ __launch_bounds__(OPT_NT) void sgd_k(const G* __restrict__ grad, floa
         }
         store8(master + i, p);
         if (mu != 0.f) store8(mom + i, b);
-        if (param) store8(param + i, p);
+        if (param) store8(param + i + e.w, p);
     }
 }
 
@@ -56,11 +64,12 @@ __global__ __launch_bounds__(OPT_NT) void adamw_k(const G* __restrict__ grad, fl
                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
                                                    float bc2) {
     const int4 e = table[blockIdx.x];
+    const int len = e.y & 0x3fffffff;
     const float scale = scale_p[0];
     const float step_size = lr / bc1;
     const float inv_sqrt_bc2 = rsqrtf(bc2);
-    const float decay = e.w ? (1.f - lr * wd) : 1.f;
-    for (int k = threadIdx.x * 8; k < e.y; k += OPT_NT * 8) {
+    const float decay = ((e.y >> 30) & 1) ? (1.f - lr * wd) : 1.f;
+    for (int k = threadIdx.x * 8; k < len; k += OPT_NT * 8) {
         const long i = (long)e.x + k;
         float g[8], p[8], m[8], v[8];
         load_grad8(grad, i, g);
@@ -77,7 +86,7 @@ __global__ __launch_bounds__(OPT_NT) void adamw_k(const G* __restrict__ grad, fl
         store8(master + i, p);
         store8(m_ + i, m);
         store8(v_ + i, v);
-        if (param) store8(param + i, p);
+        if (param) store8(param + i + e.w, p);
     }
 }
 
@@ -90,9 +99,11 @@ __global__ __launch_bounds__(OPT_NT) void lamb_phase1_k(const G* __restrict__ gr
                                                          float* __restrict__ norms) {
     __shared__ float red[4];
     const int4 e = table[blockIdx.x];
+    const int len = e.y & 0x3fffffff;
+    const bool dec = (e.y >> 30) & 1;
     const float scale = scale_p[0];
     float pn = 0.f, un = 0.f;
-    for (int k = threadIdx.x * 8; k < e.y; k += OPT_NT * 8) {
+    for (int k = threadIdx.x * 8; k < len; k += OPT_NT * 8) {
         const long i = (long)e.x + k;
         float g[8], p[8], m[8], v[8];
         load_grad8(grad, i, g);
@@ -105,7 +116,7 @@ __global__ __launch_bounds__(OPT_NT) void lamb_phase1_k(const G* __restrict__ gr
             m[j] = b1 * m[j] + (1.f - b1) * gg;
             v[j] = b2 * v[j] + (1.f - b2) * gg * gg;
             float u = (m[j] / bc1) / (sqrtf(v[j] / bc2) + eps);
-            if (e.w) u += wd * p[j];
+            if (dec) u += wd * p[j];
             pn += p[j] * p[j];
             un += u * u;
         }
@@ -126,10 +137,12 @@ __global__ __launch_bounds__(OPT_NT) void lamb_phase2_k(float* __restrict__ mast
                                                          const int4* __restrict__ table, float lr, float eps, float wd,
                                                          float bc1, float bc2, const float* __restrict__ norms) {
     const int4 e = table[blockIdx.x];
+    const int len = e.y & 0x3fffffff;
+    const bool dec = (e.y >> 30) & 1;
     const float pn = sqrtf(norms[2 * e.z]), un = sqrtf(norms[2 * e.z + 1]);
     const float ratio = (pn > 0.f && un > 0.f) ? pn / un : 1.f;
     const float step = lr * ratio;
-    for (int k = threadIdx.x * 8; k < e.y; k += OPT_NT * 8) {
+    for (int k = threadIdx.x * 8; k < len; k += OPT_NT * 8) {
         const long i = (long)e.x + k;
         float p[8], m[8], v[8];
         load8(master + i, p);
@@ -138,11 +151,11 @@ __global__ __launch_bounds__(OPT_NT) void lamb_phase2_k(float* __restrict__ mast
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float u = (m[j] / bc1) / (sqrtf(v[j] / bc2) + eps);
-            if (e.w) u += wd * p[j];
+            if (dec) u += wd * p[j];
             p[j] -= step * u;
         }
         store8(master + i, p);
-        if (param) store8(param + i, p);
+        if (param) store8(param + i + e.w, p);
     }
 }
 

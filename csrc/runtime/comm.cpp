@@ -215,27 +215,33 @@ DDL_API int ddl_comm_broadcast(void* h, void* buf, long count, int dtype, int ro
     return 0;
 }
 
+// reduce-scatter / all-gather (ZeRO-1 buckets) are numbered with the all-reduces, so
+// ddl_comm_wait_upto covers them: the optimizer waits on one bucket's shard, the next
+// forward on one bucket's gathered parameters
 DDL_API int ddl_comm_reduce_scatter(void* h, const void* send, void* recv, long recv_count, int dtype, int avg,
                                     hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
-    if (!e) return -1;
+    if (!e || recv_count <= 0) return recv_count == 0 ? 0 : -1;
     if (!order_after(e, compute)) return -3;
-    return ok(g_rccl.reduceScatter(send, recv, (size_t)recv_count, dtype_of(dtype), avg ? ncclAvg : ncclSum, e->comm,
-                                   e->stream),
-              "ncclReduceScatter")
-               ? 0
-               : -2;
+    if (!ok(g_rccl.reduceScatter(send, recv, (size_t)recv_count, dtype_of(dtype), avg ? ncclAvg : ncclSum, e->comm,
+                                 e->stream),
+            "ncclReduceScatter"))
+        return -2;
+    e->launched += 1;
+    e->bytes += recv_count * e->world * (dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2);
+    return mark_done(e) ? 0 : -3;
 }
 
 DDL_API int ddl_comm_all_gather(void* h, const void* send, void* recv, long send_count, int dtype,
                                 hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
-    if (!e) return -1;
+    if (!e || send_count <= 0) return send_count == 0 ? 0 : -1;
     if (!order_after(e, compute)) return -3;
-    return ok(g_rccl.allGather(send, recv, (size_t)send_count, dtype_of(dtype), e->comm, e->stream),
-              "ncclAllGather")
-               ? 0
-               : -2;
+    if (!ok(g_rccl.allGather(send, recv, (size_t)send_count, dtype_of(dtype), e->comm, e->stream), "ncclAllGather"))
+        return -2;
+    e->launched += 1;
+    e->bytes += send_count * e->world * (dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2);
+    return mark_done(e) ? 0 : -3;
 }
 
 // compute stream waits for every collective issued so far
@@ -248,7 +254,7 @@ DDL_API int ddl_comm_wait(void* h, hipStream_t compute) {
                : -3;
 }
 
-// compute stream waits for all-reduce number `seq` (1-based, as counted by ddl_comm_stats(h, 0))
+// compute stream waits for collective number `seq` (all-reduce / reduce-scatter / all-gather; 1-based, as counted by ddl_comm_stats(h, 0))
 // and, the comm stream being in order, everything issued before it.  A number more than
 // RING behind the newest waits for a later one instead (still correct, just later).
 DDL_API int ddl_comm_wait_upto(void* h, long seq, hipStream_t compute) {

@@ -11,22 +11,25 @@ _BLOCK = 8192
 
 
 def _table(opt):
-    """Block table over the arena index range this optimizer updates ([lo, hi): the
-    whole arena, or this rank's slice when sharded -- slices start and end on 64-element
-    boundaries, so rows never straddle another rank's elements)."""
+    """Block table over the optimizer's owned ranges: rows (local start, length | decay << 30,
+    tensor index, arena - local offset).  Unsharded the local index IS the arena index;
+    sharded (ZeRO-1), every owned chunk starts and ends on a 64-element boundary, so rows
+    never straddle another rank's elements."""
     t = getattr(opt, "_native_table", None)
     if t is None:
         rows = []
-        for ti, e in enumerate(opt.arena.entries):
-            n8 = (e.numel + 7) // 8 * 8   # pads are zero and inside the arena's aligned slot
-            a, b = max(e.offset, opt.lo), min(e.offset + n8, opt.hi)
-            s = a
-            while s < b:
-                ln = min(_BLOCK, b - s)
-                rows.append((s, ln, ti, 1 if e.decay else 0))
-                s += ln
+        for lo, hi, off in opt.ranges:
+            delta = lo - off
+            for ti, e in enumerate(opt.arena.entries):
+                n8 = (e.numel + 7) // 8 * 8   # pads are zero and inside the arena's aligned slot
+                a, b = max(e.offset, lo), min(e.offset + n8, hi)
+                s = a
+                while s < b:
+                    ln = min(_BLOCK, b - s)
+                    rows.append((s - delta, ln | ((1 if e.decay else 0) << 30), ti, delta))
+                    s += ln
         if not rows:
-            rows.append((opt.lo, 0, 0, 0))
+            rows.append((0, 0, 0, 0))
         t = torch.tensor(rows, dtype=torch.int32, device=opt.arena.device)
         opt._native_table = t
         opt._native_starts = [r[0] for r in rows]
@@ -34,7 +37,7 @@ def _table(opt):
 
 
 def _rows(opt, rng):
-    """(table pointer, row count) for the whole table or the rows of arena range [lo, hi)
+    """(table pointer, row count) for the whole table or the rows of local range [lo, hi)
     (range steps: bucket boundaries are tensor boundaries, so whole rows)."""
     tab = _table(opt)
     if rng is None:
@@ -45,15 +48,15 @@ def _rows(opt, rng):
 
 
 def _state(t: torch.Tensor, opt) -> int:
-    """Pointer such that ptr[i] is this rank's state for arena index i (state tensors
-    hold [lo, hi) only when the optimizer is sharded)."""
-    return t.data_ptr() - opt.lo * t.element_size()
+    """State tensors are indexed by the table's local start (no shift)."""
+    return t.data_ptr()
 
 
 def _targets(opt):
-    """(master fp32 pointer, param-copy or None, pdtype)."""
+    """(master fp32 pointer, param-copy or None, pdtype); the kernels write the param copy at
+    local index + the row's arena offset."""
     if opt.master is not None:
-        return _state(opt.master, opt), opt.arena.flat, dcode(opt.arena.flat)
+        return opt.master.data_ptr(), opt.arena.flat, dcode(opt.arena.flat)
     return opt.arena.flat.data_ptr(), None, 0
 
 
@@ -103,12 +106,12 @@ def lamb(opt, grad, scale, rng=None):
              float(bc2), p(norms))
         return
     tab = _table(opt)
-    # sharded: the per-tensor norms of every rank's slice are summed between the phases
-    import torch.distributed as dist
+    # sharded: the per-tensor norms of every rank's pieces are summed between the phases
+    from ..optim.flat import _sum_over_ranks
     m, v = _state(opt.m, opt), _state(opt.v, opt)
     call("ddl_lamb_phase1", dcode(grad), p(grad), master, m, v, p(tab), tab.shape[0], p(s), float(opt.b1),
          float(opt.b2), float(opt.eps), float(opt.weight_decay), float(bc1), float(bc2), p(norms))
-    dist.all_reduce(norms)
+    _sum_over_ranks(norms)
     call("ddl_lamb_phase2", master, pdt, p(param), m, v, p(tab), tab.shape[0], float(opt.lr), float(opt.eps),
          float(opt.weight_decay), float(bc1), float(bc2), p(norms))
 

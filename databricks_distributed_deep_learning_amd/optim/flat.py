@@ -22,13 +22,36 @@ from .arena import ParamArena
 from ..ops import _lib
 
 
+def _sum_over_ranks(t: torch.Tensor) -> None:
+    """In-place SUM over the data-parallel ranks: through the reducer's native RCCL engine
+    when one is active (one communicator for every collective of a step), else torch."""
+    from ..parallel import comm as _comm
+    eng = _comm.active()
+    if eng is not None and t.is_cuda:
+        eng.wait_upto(eng.all_reduce(t))
+        return
+    import torch.distributed as dist
+    dist.all_reduce(t)
+
+
 class FlatOptimizer:
-    """``shard=(rank, world)`` -- ZeRO-1: this rank keeps the fp32 master copy and the
-    optimizer state only for its contiguous 1/world slice ``[lo, hi)`` of the arena
-    (the arena is padded to ``world * 64`` elements), updates that slice from the
-    all-reduced gradient and all-gathers the updated compute-dtype parameters.  State
-    memory per rank drops by ``world``; the optimizer kernels see the same arena index
-    space (their state pointers are offset by ``-lo``), so no kernel changes."""
+    """``shard`` -- ZeRO-1: this rank keeps the fp32 master copy and the optimizer state
+    only for the arena ranges it owns, stored back to back in a LOCAL index space.
+
+    * ``shard=(rank, world)``: one contiguous 1/world slice of the arena (padded to
+      ``world * 64`` elements);
+    * ``shard=(rank, world, groups)``: ``groups`` = ``[(start, end), ...]`` gradient
+      buckets (``DataParallel(shard=True).buckets``, each a multiple of ``world * 64``
+      elements); the rank owns chunk ``rank`` of every bucket -- exactly what a per-bucket
+      reduce-scatter leaves it, so the reduced gradient shard IS the local gradient.
+
+    ``step(grad)`` takes the local gradient shard (or a full-arena gradient, whose owned
+    pieces are gathered), updates the owned elements, writes their compute-dtype copy
+    into the arena and all-gathers every group's chunks back into ``arena.flat`` -- through
+    ``gather_fn`` when set (the reducer's async, stream-ordered all-gathers that the next
+    forward waits on bucket by bucket), synchronously otherwise.  The kernels' block
+    table carries, per row, the offset from local index to arena index, so one launch
+    still covers every owned range."""
     name = "base"
 
     def __init__(self, arena: ParamArena, lr: float, weight_decay: float = 0.0,
@@ -39,25 +62,52 @@ class FlatOptimizer:
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
         self.shard = None
-        self.lo, self.hi = 0, arena.numel
+        # ranges: (arena lo, arena hi, local offset); groups: (start, end) gathered per rank chunk
+        self.ranges = [(0, arena.numel, 0)]
+        self.groups = []
+        self.gather_fn = None
         if shard is not None and shard[1] > 1:
-            rank, world = shard
-            if arena.numel % (world * 64):
-                raise ValueError("sharded optimizer: build the arena with pad_multiple = world * 64 "
-                                 "(64-element-aligned slice boundaries)")
-            size = arena.numel // world
+            rank, world = shard[0], shard[1]
+            groups = list(shard[2]) if len(shard) > 2 else [(0, arena.numel)]
+            ranges, off = [], 0
+            for a, b in groups:
+                if (b - a) % (world * 64):
+                    raise ValueError("sharded optimizer: every group must be a multiple of world * 64 elements "
+                                     "(build the arena with pad_multiple = world * 64)")
+                n = (b - a) // world
+                ranges.append((a + rank * n, a + (rank + 1) * n, off))
+                off += n
             self.shard = (rank, world)
-            self.lo, self.hi = rank * size, (rank + 1) * size
+            self.ranges, self.groups = ranges, groups
+        self.local_numel = sum(hi - lo for lo, hi, _ in self.ranges)
         self.master: Optional[torch.Tensor] = None
         if arena.dtype != torch.float32 or self.shard is not None:
-            self.master = arena.flat[self.lo:self.hi].detach().float().clone()
+            self.master = self._local(arena.flat).detach().float().clone()
         self._decay_mask: Optional[torch.Tensor] = None
         self.last_grad_norm: Optional[torch.Tensor] = None
 
     @property
+    def lo(self) -> int:          # first owned arena index (the whole arena when unsharded)
+        return self.ranges[0][0]
+
+    @property
+    def hi(self) -> int:
+        return self.ranges[-1][1]
+
+    @property
     def state_numel(self) -> int:
         """Elements of optimizer state this rank holds (the whole arena unless sharded)."""
-        return self.hi - self.lo
+        return self.local_numel
+
+    def _local(self, full: torch.Tensor) -> torch.Tensor:
+        """The owned pieces of a full-arena tensor, back to back (a view when unsharded)."""
+        if self.shard is None:
+            return full
+        return torch.cat([full[lo:hi] for lo, hi, _ in self.ranges])
+
+    def _scatter_local(self, local: torch.Tensor, full: torch.Tensor) -> None:
+        for lo, hi, off in self.ranges:
+            full[lo:hi].copy_(local[off:off + hi - lo])
 
     def _zeros_state(self) -> torch.Tensor:
         return torch.zeros(self.state_numel, dtype=torch.float32, device=self.arena.device)
@@ -69,15 +119,25 @@ class FlatOptimizer:
 
     def decay_mask(self) -> torch.Tensor:
         if self._decay_mask is None:
-            self._decay_mask = self.arena.decay_mask().to(torch.float32)[self.lo:self.hi]
+            self._decay_mask = self._local(self.arena.decay_mask().to(torch.float32))
         return self._decay_mask
 
+    def local_grad(self, grad: torch.Tensor) -> torch.Tensor:
+        """The gradient in local index space (``grad`` is either already the shard or the
+        full arena gradient)."""
+        if self.shard is None or grad.numel() == self.local_numel:
+            return grad
+        return self._local(grad)
+
     def _all_gather_params(self) -> None:
-        """Every rank's updated slice -> the full compute-dtype arena (in place)."""
+        """Every rank's updated chunks -> the full compute-dtype arena (in place)."""
+        if self.gather_fn is not None:
+            self.gather_fn(self.groups, self.ranges)
+            return
         import torch.distributed as dist
         flat = self.arena.flat
-        dist.all_gather_into_tensor(flat, flat[self.lo:self.hi].clone() if not flat.is_cuda else
-                                    flat[self.lo:self.hi])
+        for (a, b), (lo, hi, _) in zip(self.groups, self.ranges):
+            dist.all_gather_into_tensor(flat[a:b], flat[lo:hi].clone() if not flat.is_cuda else flat[lo:hi])
 
     def _native(self) -> bool:
         return _lib.use_native(self.arena.flat)
@@ -88,7 +148,12 @@ class FlatOptimizer:
     def _clip_scale(self, grad: torch.Tensor, grad_scale: float) -> torch.Tensor:
         """Returns a device scalar multiplier (grad_scale, times the clip factor)."""
         if self.max_grad_norm and self.max_grad_norm > 0:
-            if self._native():
+            if self.shard is not None:
+                # the local shard: sum of squares over ranks, then the root
+                sq = (grad.float().pow(2).sum()).reshape(1)
+                _sum_over_ranks(sq)
+                norm = sq.sqrt().reshape(()) * grad_scale
+            elif self._native():
                 from ..ops import _native_optim
                 norm = _native_optim.global_norm(grad) * grad_scale
             else:
@@ -138,6 +203,7 @@ class FlatOptimizer:
     def step(self, grad: Optional[torch.Tensor] = None, grad_scale: float = 1.0, lr: Optional[float] = None):
         if grad is None:
             grad = self.arena.grad
+        grad = self.local_grad(grad)
         self.step_count += 1
         if lr is not None:
             self.lr = lr
@@ -145,22 +211,26 @@ class FlatOptimizer:
         if self._native():
             self._step_native(grad, scale)
         else:
-            self._step_torch(grad[self.lo:self.hi].float() * scale)
+            self._step_torch(grad.float() * scale)
             if self.master is not None:
-                self.arena.flat[self.lo:self.hi].copy_(self.master)
+                if self.shard is None:
+                    self.arena.flat.copy_(self.master)
+                else:
+                    self._scatter_local(self.master, self.arena.flat)
         if self.shard is not None:
             self._all_gather_params()
         self.arena.bump()
 
     # ------------------------------------------------------------------
     def _full(self, t: torch.Tensor) -> torch.Tensor:
-        """A sharded state tensor gathered to the whole arena (checkpoints stay
-        independent of the world size)."""
+        """A sharded (local) state tensor gathered to the whole arena (checkpoints stay
+        independent of the world size and of the bucket layout)."""
         if self.shard is None:
             return t
         import torch.distributed as dist
-        out = torch.empty(self.arena.numel, dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
+        out = torch.zeros(self.arena.numel, dtype=t.dtype, device=t.device)
+        for (a, b), (lo, hi, off) in zip(self.groups, self.ranges):
+            dist.all_gather_into_tensor(out[a:b], t[off:off + hi - lo].contiguous())
         return out
 
     def state_dict(self) -> Dict[str, object]:
@@ -185,13 +255,12 @@ class FlatOptimizer:
     def load_state_dict(self, st: Dict[str, object]) -> None:
         self.step_count = int(st["step"])
         self.lr = float(st["lr"])
-        lo, hi = self.lo, self.hi
         if self.master is not None and "master" in st:
             full = self._fit(st["master"])
-            self.master.copy_(full[lo:hi])
+            self.master.copy_(self._local(full))
             self.arena.flat.copy_(full.to(self.arena.flat.dtype))
         for k, t in self._state_tensors().items():
-            t.copy_(self._fit(st[k])[lo:hi])
+            t.copy_(self._local(self._fit(st[k])))
         self.arena.bump()
 
     def _state_tensors(self) -> Dict[str, torch.Tensor]:
@@ -288,26 +357,30 @@ class FlatLAMB(FlatOptimizer):
         u = (m / bc1) / ((v / bc2).sqrt() + self.eps)
         if self.weight_decay:
             u = u + self.weight_decay * self.decay_mask()[ra:rb] * p
-        # per-tensor ||p||^2, ||u||^2 over this rank's part of each tensor (summed over ranks when sharded),
-        # restricted to the tensors of local range [ra, rb); offsets relative to ra
-        segs = []
-        for e in self.arena.entries:
-            a, b = max(e.offset, self.lo + ra), min(e.offset + e.numel, self.lo + rb)
-            segs.append((a - self.lo - ra, b - self.lo - ra) if a < b else None)
+        # per-tensor ||p||^2, ||u||^2 over this rank's pieces of each tensor (summed over ranks when
+        # sharded), restricted to local range [ra, rb); segment offsets relative to ra
+        segs = [[] for _ in self.arena.entries]
+        for ti, e in enumerate(self.arena.entries):
+            for lo, hi, off in self.ranges:
+                a, b = max(e.offset, lo), min(e.offset + e.numel, hi)
+                if a < b:
+                    la, lb = max(a - lo + off, ra), min(b - lo + off, rb)
+                    if la < lb:
+                        segs[ti].append((la - ra, lb - ra))
         sq = torch.zeros(2 * len(segs), dtype=torch.float32, device=p.device)
         for ti, sg in enumerate(segs):
-            if sg is not None:
-                sq[2 * ti] = p[sg[0]:sg[1]].pow(2).sum()
-                sq[2 * ti + 1] = u[sg[0]:sg[1]].pow(2).sum()
+            for a, b in sg:
+                sq[2 * ti] += p[a:b].pow(2).sum()
+                sq[2 * ti + 1] += u[a:b].pow(2).sum()
         if self.shard is not None:
-            import torch.distributed as dist
-            dist.all_reduce(sq)
+            _sum_over_ranks(sq)
         for ti, sg in enumerate(segs):
-            if sg is None:
+            if not sg:
                 continue
             pn, un = sq[2 * ti].sqrt(), sq[2 * ti + 1].sqrt()
             ratio = torch.where((pn > 0) & (un > 0), pn / un, torch.ones_like(pn))
-            p[sg[0]:sg[1]].add_(u[sg[0]:sg[1]] * ratio, alpha=-self.lr)
+            for a, b in sg:
+                p[a:b].add_(u[a:b] * ratio, alpha=-self.lr)
 
     def _step_native(self, grad, scale, rng=None):
         from ..ops import _native_optim

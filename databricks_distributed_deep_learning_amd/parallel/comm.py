@@ -163,15 +163,21 @@ class NativeComm:
         self._check(_fn("ddl_comm_broadcast")(self._h, t.data_ptr(), t.numel(), _DTYPES[t.dtype], root, _stream()),
                     "broadcast")
 
-    def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, average: bool = False) -> None:
-        assert send.numel() == recv.numel() * self.world
+    def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, average: bool = False) -> int:
+        """``recv`` = this rank's 1/world chunk of the sum of ``send`` over ranks (async on
+        the comm stream); returns its sequence number for :meth:`wait_upto`."""
+        assert send.numel() == recv.numel() * self.world and send.is_contiguous() and recv.is_contiguous()
         self._check(_fn("ddl_comm_reduce_scatter")(self._h, send.data_ptr(), recv.data_ptr(), recv.numel(),
                                                    _DTYPES[send.dtype], int(average), _stream()), "reduce_scatter")
+        return self.collectives_launched if recv.numel() > 0 else 0
 
-    def all_gather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
-        assert recv.numel() == send.numel() * self.world
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor) -> int:
+        """``recv`` = every rank's ``send`` in rank order (in place when ``send`` is
+        ``recv``'s own rank slice); async, returns its sequence number."""
+        assert recv.numel() == send.numel() * self.world and send.is_contiguous() and recv.is_contiguous()
         self._check(_fn("ddl_comm_all_gather")(self._h, send.data_ptr(), recv.data_ptr(), send.numel(),
                                                _DTYPES[send.dtype], _stream()), "all_gather")
+        return self.collectives_launched if send.numel() > 0 else 0
 
     def wait(self) -> None:
         """Current (compute) stream waits for every collective issued so far."""

@@ -21,6 +21,16 @@ Design (MI355X-first, not a DDP re-implementation):
   into an fp32 arena so bf16 accumulation error does not grow with grad_accum;
 * the 1/world average is folded into the optimizer (``grad_scale``) instead of
   an extra pass over the buckets;
+* ``shard=True`` (ZeRO-1, world > 1): each bucket is REDUCE-SCATTERED instead of
+  all-reduced -- bucket boundaries are multiples of ``world * 64`` elements, rank r
+  receives the reduced chunk r of every bucket into a local gradient shard, which is
+  exactly the gradient its sharded optimizer (``optim.flat``, ``shard=(r, w, groups)``)
+  updates.  After the step the updated chunks are ALL-GATHERED back per bucket on the
+  comm stream (``gather_params``) in the order the next forward needs them (the last
+  bucket holds the first layers), and a forward pre-hook per module waits for exactly
+  the buckets holding that module's parameters: the gathers overlap the forward.
+  Traffic per step equals one all-reduce (reduce-scatter + all-gather) instead of
+  all-reduce + all-gather;
 * ``comm="native"`` (default on GPU + RCCL) issues the bucket all-reduces
   through the C++ engine in ``csrc/runtime/comm.cpp`` (its own RCCL
   communicator and high-priority HIP stream, event-ordered after the producing
@@ -51,6 +61,7 @@ class Bucket:
     handle: Optional[object] = None
     launched: bool = False
     payload: Optional[torch.Tensor] = None
+    shard_off: int = 0           # ZeRO-1: this rank's chunk of the bucket in the local gradient shard
     grads_seen: set = field(default_factory=set)
     seq: int = 0                 # native engine: this bucket's all-reduce number (wait_upto)
     eager_done: bool = False     # set_eager callback already issued on the side stream
@@ -68,7 +79,7 @@ class DataParallel(nn.Module):
                  bucket_mb: float = 25.0, first_bucket_mb: float = 4.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast_buffers: bool = False,
                  accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True,
-                 comm: str = "auto", backward_passes_per_step: int = 1):
+                 comm: str = "auto", backward_passes_per_step: int = 1, shard: bool = False):
         super().__init__()
         self.module = module
         self.arena = arena if arena is not None else ParamArena(list(module.named_parameters()))
@@ -107,11 +118,23 @@ class DataParallel(nn.Module):
         if self.native is not None and hasattr(self.native, "world"):
             from . import comm as _comm
             _comm.set_active(self.native)   # SyncBatchNorm rides the same communicator
-        self.buckets = self._build_buckets(bucket_mb, first_bucket_mb)
-        self._entry_bucket = {}
+        self.shard = bool(shard) and self.world > 1
+        if self.shard:
+            unit = self.world * 64
+            if self.arena.numel % unit:
+                raise ValueError("DataParallel(shard=True): build the arena with pad_multiple = world * 64")
+            self.buckets = self._build_shard_buckets(bucket_mb, first_bucket_mb, unit)
+        else:
+            self.buckets = self._build_buckets(bucket_mb, first_bucket_mb)
+        self._entry_buckets: dict = {}
         for b in self.buckets:
             for ei in b.entry_ids:
-                self._entry_bucket[ei] = b.index
+                self._entry_buckets.setdefault(ei, []).append(b.index)
+        self._gshard: Optional[torch.Tensor] = None
+        self._gather_marks: dict = {}        # bucket index -> native seq / torch handle of its all-gather
+        self._prehooks = []
+        if self.shard:
+            self._install_gather_waits()
         self._eager_cb: Optional[Callable[[torch.Tensor, int, int], None]] = None
         self._eager_stream = None
         self._eager_used = False
@@ -143,6 +166,79 @@ class DataParallel(nn.Module):
             buckets.append(Bucket(len(buckets), start, self.arena.numel, cur))
         return buckets
 
+    def _build_shard_buckets(self, bucket_mb: float, first_bucket_mb: float, unit: int) -> List[Bucket]:
+        """ZeRO-1 buckets: boundaries rounded UP to a multiple of ``unit`` = world * 64 elements
+        (past the first tensor end that fills the bucket), so every rank's chunk is whole and
+        64-aligned; a tensor may straddle two buckets (both wait for it)."""
+        esz = torch.empty((), dtype=self.reduce_dtype).element_size()
+        bounds, start = [], 0
+        cap = int(first_bucket_mb * (1 << 20)) // esz
+        for e in self.arena.entries:
+            end = e.offset + e.numel
+            if end - start >= cap:
+                b = min(self.arena.numel, -(-end // unit) * unit)
+                if b > start:
+                    bounds.append((start, b))
+                    start = b
+                cap = int(bucket_mb * (1 << 20)) // esz
+        if start < self.arena.numel:
+            bounds.append((start, self.arena.numel))
+        buckets, off = [], 0
+        for i, (a, b) in enumerate(bounds):
+            ids = [ei for ei, e in enumerate(self.arena.entries) if e.offset < b and e.offset + e.numel > a]
+            bk = Bucket(i, a, b, ids)
+            bk.shard_off = off
+            off += (b - a) // self.world
+            buckets.append(bk)
+        return buckets
+
+    def shard_groups(self) -> List[tuple]:
+        """(start, end) of every bucket: the ``groups`` a sharded optimizer takes."""
+        return [(b.start, b.end) for b in self.buckets]
+
+    def _install_gather_waits(self) -> None:
+        """Forward pre-hook per module with parameters: wait for the all-gathers of the
+        buckets holding them (stream waits, no host sync)."""
+        index = {id(e.param): ei for ei, e in enumerate(self.arena.entries)}
+        for mod in self.module.modules():
+            bks = set()
+            for prm in mod.parameters(recurse=False):
+                ei = index.get(id(prm))
+                if ei is not None:
+                    bks.update(self._entry_buckets.get(ei, []))
+            if bks:
+                need = sorted(bks)
+                self._prehooks.append(mod.register_forward_pre_hook(
+                    lambda _m, _a, need=need: self._wait_gathers(need)))
+
+    def _wait_gathers(self, idx) -> None:
+        for i in idx:
+            mark = self._gather_marks.pop(i, None)
+            if mark is None:
+                continue
+            if isinstance(mark, int):
+                self.native.wait_upto(mark)
+            else:
+                mark.wait()
+
+    def wait_params(self) -> None:
+        """Make the current stream wait for every outstanding parameter all-gather
+        (before reading parameters outside a forward: checkpoints, evaluation)."""
+        self._wait_gathers(list(self._gather_marks))
+
+    def gather_params(self, groups, ranges) -> None:
+        """Sharded optimizer's ``gather_fn``: all-gather every bucket's updated chunks into
+        the arena, asynchronously, last bucket (the first layers) first."""
+        flat = self.arena.flat
+        order = sorted(range(len(groups)), key=lambda i: -groups[i][0])
+        for i in order:
+            (a, b), (lo, hi, _) = groups[i], ranges[i]
+            if self.native is not None:
+                self._gather_marks[i] = self.native.all_gather(flat[lo:hi], flat[a:b])
+            else:
+                send = flat[lo:hi] if flat.is_cuda else flat[lo:hi].clone()
+                self._gather_marks[i] = dist.all_gather_into_tensor(flat[a:b], send, group=self.pg, async_op=True)
+
     def _reset(self) -> None:
         for b in self.buckets:
             b.pending = len(b.entry_ids)
@@ -170,7 +266,7 @@ class DataParallel(nn.Module):
                 return
             if native:
                 if ei in self._native_seen and self._eager_cb is not None and \
-                        self.buckets[self._entry_bucket[ei]].launched:
+                        any(self.buckets[bi].launched for bi in self._entry_buckets[ei]):
                     # two native uses of one weight in one step: the side stream may already be
                     # rewriting it while the second use's backward still reads it -- refuse
                     raise RuntimeError(
@@ -184,13 +280,14 @@ class DataParallel(nn.Module):
                 self._arrivals[ei] = n
                 if n < self.passes:          # accumulate locally; communicate on pass k
                     return
-            b = self.buckets[self._entry_bucket[ei]]
-            if ei in b.grads_seen:   # parameter used twice in one graph: count once
-                return
-            b.grads_seen.add(ei)
-            b.pending -= 1
-            if b.pending == 0:
-                self._launch(b)
+            for bi in self._entry_buckets[ei]:
+                b = self.buckets[bi]
+                if ei in b.grads_seen:   # parameter used twice in one graph: count once
+                    continue
+                b.grads_seen.add(ei)
+                b.pending -= 1
+                if b.pending == 0:
+                    self._launch(b)
         return hook
 
     def _payload(self, b: Bucket) -> torch.Tensor:
@@ -209,6 +306,9 @@ class DataParallel(nn.Module):
         b.launched = True
         self._order.append(b)
         b.payload = self._payload(b)
+        if self.shard:
+            self._launch_scatter(b)
+            return
         if self.native is not None or self.world > 1:
             if self.native is not None:
                 # payload is the arena slice / fp32 accumulator / a converted copy held
@@ -220,9 +320,20 @@ class DataParallel(nn.Module):
         if self._eager_cb is not None and self._eager_ok():
             self._run_eager(b)
 
+    def _launch_scatter(self, b: Bucket) -> None:
+        """ZeRO-1: reduce-scatter the bucket; chunk ``rank`` lands in the local gradient shard."""
+        n = (b.end - b.start) // self.world
+        if self._gshard is None or self._gshard.dtype != b.payload.dtype:
+            self._gshard = torch.empty(self.arena.numel // self.world, dtype=b.payload.dtype, device=self.arena.device)
+        recv = self._gshard[b.shard_off:b.shard_off + n]
+        if self.native is not None:
+            b.seq = self.native.reduce_scatter(b.payload, recv)
+        else:
+            b.handle = dist.reduce_scatter_tensor(recv, b.payload, group=self.pg, async_op=True)
+
     # ------------------------------------------------------------------ eager per-bucket callbacks
     def _eager_ok(self) -> bool:
-        return (self.arena.grad.is_cuda and self.reduce_dtype == self.arena.dtype and not self._acc_active
+        return (not self.shard and self.arena.grad.is_cuda and self.reduce_dtype == self.arena.dtype and not self._acc_active
                 and (self.native is None or hasattr(self.native, "wait_upto")))
 
     def set_eager(self, cb: Optional[Callable[[torch.Tensor, int, int], None]]) -> None:
@@ -279,9 +390,19 @@ class DataParallel(nn.Module):
         covers -- a range-stepping optimizer updates the early buckets while the last
         all-reduces (the embedding's, in BERT) are still on the wire.
         """
+        self.wait_params()           # a step without a forward in between still sees gathered params
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
+        if self.shard:
+            for b in self.buckets:
+                if b.handle is not None:
+                    b.handle.wait()
+            if self.native is not None:
+                self.native.wait()
+            out = self._gshard
+            self._reset()
+            return out
         if self._eager_used:
             # the callbacks ran during backward on the side stream: the compute stream (next
             # forward, zero_grad) waits for them; the rings were waited for on the side stream

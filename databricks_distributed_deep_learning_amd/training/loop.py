@@ -63,9 +63,13 @@ class Trainer:
         rd = {"auto": None, "fp32": torch.float32, "bf16": torch.bfloat16}[cfg.grad_reduce_dtype]
         self.ddp = DataParallel(model, self.arena, bucket_mb=cfg.bucket_mb, first_bucket_mb=cfg.first_bucket_mb,
                                 reduce_dtype=rd, broadcast_buffers=cfg.broadcast_buffers,
-                                accumulate_fp32=accumulate_fp32, comm=cfg.comm)
+                                accumulate_fp32=accumulate_fp32, comm=cfg.comm, shard=zero)
+        # ZeRO-1: the optimizer owns chunk `rank` of every reduce-scattered bucket and hands its
+        # updated chunks back through the reducer's overlapped per-bucket all-gathers
         self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg,
-                                   shard=(self.rank, self.world) if zero else None)
+                                   shard=(self.rank, self.world, self.ddp.shard_groups()) if zero else None)
+        if zero:
+            self.opt.gather_fn = self.ddp.gather_params
         self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
         self.overlap_optimizer = (self.world > 1 and cfg.overlap_optimizer and self.opt.supports_ranges()
                                   and self.ddp.reduce_dtype == self.arena.dtype)
@@ -246,6 +250,7 @@ class Trainer:
                 t_seg += t_pause
                 self.save_checkpoint()
                 timer.start()
+        self.ddp.wait_params()               # ZeRO-1: the last step's parameter all-gathers
         ddist.barrier()
         t_seg += timer.stop()
         meter.update(t_seg, steps)
@@ -274,6 +279,7 @@ class Trainer:
         return summary
 
     def save_checkpoint(self) -> None:
+        self.ddp.wait_params()
         ckpt.save(self.cfg.checkpoint_dir, self.model, self.opt, self.step, self.cfg.to_dict(), loader=self.loader)
 
 

@@ -72,12 +72,13 @@ class PhaseTimer:
         self.enabled = enabled
         self._pending: list = []       # per step: [(name, event or time), ...]
         self._cur: list = []
+        self._pool: list = []          # resolved events, re-recorded by later marks
         self.totals: Dict[str, float] = {}
         self.steps = 0
 
     def _stamp(self):
         if self.cuda:
-            e = torch.cuda.Event(enable_timing=True)
+            e = self._pool.pop() if self._pool else torch.cuda.Event(enable_timing=True)
             e.record()
             return e
         return time.perf_counter()
@@ -104,6 +105,8 @@ class PhaseTimer:
                 else:
                     ms = 1000.0 * (b - a)
                 self.totals[name] = self.totals.get(name, 0.0) + ms
+            if self.cuda:
+                self._pool.extend(e for _, e in marks)
             self.steps += 1
         self._pending = []
 

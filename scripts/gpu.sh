@@ -10,6 +10,7 @@
 #   stock [args]          bench.py --native stock (plain PyTorch-ROCm + torch DDP arm)
 #   ab LIB MODEL [RUNS]   same-box A/B of libddl_LIB.so (scripts/build_ab.sh) vs the tree's library,
 #                         alternating RUNS times (default 3) on MODEL (resnet50 | bert_base)
+#   abenv VAR=VAL MODEL [RUNS]  same-box A/B of an environment toggle (unset vs VAR=VAL), alternating
 #   prof MODEL            rocprofv3 kernel table (steady state) -> gpurun_out/kernels_MODEL.md
 #   pmc MODEL             3 PMC passes summarised             -> gpurun_out/pmc_MODEL.md
 #   presets               every BASELINE preset through the train() CLI
@@ -66,6 +67,20 @@ step() {
         done
       done
       unset DDL_NATIVE_LIB ;;
+    abenv)
+      local kv=$1 model=$2 runs=${3:-3}
+      for i in $(seq 1 "$runs"); do
+        for arm in base env; do
+          if [ "$arm" = base ]; then
+            timeout -k 10 300 python bench.py --model "$model" --steps 30 --warmup 5 > "gpurun_out/abenv_${arm}_$i.log" 2>&1 \
+              || { tail -20 "gpurun_out/abenv_${arm}_$i.log"; return 1; }
+          else
+            env "$kv" timeout -k 10 300 python bench.py --model "$model" --steps 30 --warmup 5 > "gpurun_out/abenv_${arm}_$i.log" 2>&1 \
+              || { tail -20 "gpurun_out/abenv_${arm}_$i.log"; return 1; }
+          fi
+          echo "$arm($kv) $model run=$i $(tail -1 "gpurun_out/abenv_${arm}_$i.log" | python3 -c 'import sys,json; print(json.loads(sys.stdin.read())["value"])')"
+        done
+      done ;;
     prof)
       local m=$1 cmd
       cmd=$(run_model "$m" 5 3) || return 1

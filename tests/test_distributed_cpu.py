@@ -327,3 +327,54 @@ def test_zero1_checkpoint_save_and_resume_world2(tmp_path):
 def test_optimizer_overlapped_with_bucket_allreduce(opt_name):
     out = Distributor(num_processes=2, use_gpu=False).run(_overlap_equivalence, opt_name)
     assert out["nbuckets"] > 1 and out["err"] < 1e-6, out
+
+
+def _zero_rs_equivalence(opt_name, accum):
+    """ZeRO-1 through the reducer: buckets reduce-scattered into the local gradient shard,
+    sharded step, per-bucket all-gathers waited by forward pre-hooks == replicated DP."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.optim import ParamArena
+    from databricks_distributed_deep_learning_amd.optim.flat import FlatAdamW, FlatLAMB, FlatSGD
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    rank, world = dist.get_rank(), dist.get_world_size()
+    cls = {"sgd": FlatSGD, "adamw": FlatAdamW, "lamb": FlatLAMB}[opt_name]
+    kw = {"sgd": dict(lr=0.1, momentum=0.9, weight_decay=1e-3), "adamw": dict(lr=1e-2, weight_decay=0.01),
+          "lamb": dict(lr=1e-2, weight_decay=0.01)}[opt_name]
+    x, y = _data(16 * accum)
+    x, y = x[rank::world], y[rank::world]
+    finals, info = [], {}
+    for shard in (False, True):
+        torch.manual_seed(11)
+        model = torch.nn.Sequential(torch.nn.Linear(10, 96), torch.nn.Tanh(), torch.nn.Linear(96, 64),
+                                    torch.nn.Tanh(), torch.nn.Linear(64, 3))
+        arena = ParamArena(list(model.named_parameters()), pad_multiple=world * 64 if shard else 1)
+        ddp = DataParallel(model, arena, bucket_mb=0.004, first_bucket_mb=0.001, shard=shard,
+                           accumulate_fp32=accum > 1)
+        opt = cls(arena, shard=(rank, world, ddp.shard_groups()) if shard else None, **kw)
+        if shard:
+            opt.gather_fn = ddp.gather_params
+            info = {"nbuckets": len(ddp.buckets), "local": opt.state_numel, "arena": arena.numel,
+                    "straddle": sum(len(v) > 1 for v in ddp._entry_buckets.values())}
+        for _ in range(3):
+            ddp.zero_grad()
+            for i in range(accum):
+                ctx = ddp.no_sync() if i < accum - 1 else torch.enable_grad()
+                with ctx:
+                    torch.nn.functional.cross_entropy(ddp(x[i::accum]), y[i::accum]).backward()
+            g = ddp.finish()
+            if shard:
+                assert g.numel() == opt.state_numel
+            opt.step(g, grad_scale=1.0 / (world * accum))
+        ddp.wait_params()
+        finals.append(torch.cat([p.detach().flatten() for p in model.parameters()]))
+        sd = opt.state_dict()
+    info["err"] = (finals[0] - finals[1]).abs().max().item()
+    info["sd"] = sd["master"].numel()
+    return info
+
+
+@pytest.mark.parametrize("opt_name,accum", [("sgd", 1), ("adamw", 2), ("lamb", 1)])
+def test_zero1_reduce_scatter_matches_replicated(opt_name, accum):
+    out = Distributor(num_processes=2, use_gpu=False).run(_zero_rs_equivalence, opt_name, accum)
+    assert out["err"] < 1e-5, out
+    assert out["nbuckets"] > 1 and out["local"] * 2 == out["arena"] and out["sd"] == out["arena"], out

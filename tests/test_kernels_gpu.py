@@ -279,6 +279,53 @@ def test_flat_optimizers_match_torch_path(name, pdtype):
     _close(outs[0][1], outs[1][1], 1e-2 if pdtype == torch.bfloat16 else 1e-5, 1e-5, f"{name} param")
 
 
+@pytest.mark.parametrize("name", ["sgd", "adamw", "lamb"])
+def test_sharded_flat_optimizers_match_torch_path(name, monkeypatch):
+    """ZeRO-1 rank 0 of 2 owning chunk 0 of two buckets (local index space, per-row arena
+    offsets in the block table): native kernels == torch path on the owned elements; the
+    unowned arena elements are left alone (the all-gather is stubbed out)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.config import TrainConfig
+    from databricks_distributed_deep_learning_amd.ops import _lib
+    from databricks_distributed_deep_learning_amd.optim import ParamArena, build_optimizer
+    from databricks_distributed_deep_learning_amd.optim import flat as F_
+    monkeypatch.setattr(F_, "_sum_over_ranks", lambda t: None)
+
+    def make():
+        torch.manual_seed(3)
+        m = torch.nn.Sequential(torch.nn.Linear(67, 129), torch.nn.LayerNorm(129), torch.nn.Linear(129, 5)).to(dev)
+        for prm in m.parameters():
+            prm.data = prm.data.to(torch.bfloat16)
+        return m
+
+    cfg = TrainConfig(lr=1e-2, weight_decay=0.1, momentum=0.9, max_grad_norm=1.0 if name == "lamb" else 0.0)
+    outs = []
+    for mode in ("auto", "off"):
+        _lib.set_mode(mode)
+        m = make()
+        arena = ParamArena(list(m.named_parameters()), pad_multiple=128)
+        split = (arena.numel // 2) // 128 * 128
+        opt = build_optimizer(name, arena, cfg, shard=(0, 2, [(0, split), (split, arena.numel)]))
+        opt.gather_fn = lambda groups, ranges: None
+        before = arena.flat.clone()
+        pad_mask = torch.zeros(arena.numel, dtype=torch.bool, device=dev)
+        for e in arena.entries:
+            pad_mask[e.offset:e.offset + e.numel] = True
+        lmask = opt._local(pad_mask)        # gradients are zero in the alignment padding
+        g = torch.Generator(device=dev).manual_seed(7)
+        for _ in range(3):
+            local = (torch.randn(opt.state_numel, generator=g, device=dev) * lmask).to(torch.bfloat16)
+            opt.step(local, grad_scale=0.5)
+        owned = torch.zeros(arena.numel, dtype=torch.bool, device=dev)
+        for lo, hi, _ in opt.ranges:
+            owned[lo:hi] = True
+        assert torch.equal(arena.flat[~owned], before[~owned])
+        outs.append((opt.params32.clone(), arena.flat[owned].clone()))
+    _lib.set_mode("auto")
+    _close(outs[0][0], outs[1][0], 1e-5, 1e-5, f"{name} sharded master")
+    _close(outs[0][1], outs[1][1], 1e-2, 1e-5, f"{name} sharded param")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,C,k", [(1, 1000, 5), (3, 1000, 5), (4, 37, 3), (2, 4096, 10)])
 def test_softmax_topk(dtype, B, C, k):
