@@ -103,8 +103,9 @@ class Linear(nn.Module):
                 bound = 1.0 / math.sqrt(fin)
                 nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x, grad_residual=None, fuse_dgelu: bool = False):
-        return ops.linear(x, self.weight, self.bias, self.act, grad_residual=grad_residual, fuse_dgelu=fuse_dgelu)
+    def forward(self, x, grad_residual=None, fuse_dgelu: bool = False, residual=None):
+        return ops.linear(x, self.weight, self.bias, self.act, grad_residual=grad_residual, fuse_dgelu=fuse_dgelu,
+                          residual=residual)
 
     def extra_repr(self):
         return f"{self.fin}, {self.fout}, bias={self.bias is not None}, act={self.act}"

@@ -50,9 +50,15 @@ class ViTLayer(nn.Module):
     def forward(self, h):
         y = self.layernorm_before(h)
         ctx = ops.attention(self.qkv(y), self.num_heads, None, self.attn_dropout, self.training)
-        h = h + self.dropout(self.attn_out(ctx))
+        if self.dropout.p > 0.0 and self.training:
+            h = h + self.dropout(self.attn_out(ctx))
+            y = self.layernorm_after(h)
+            return h + self.dropout(self.fc2(self.fc1(y), fuse_dgelu=True))
+        # no hidden dropout (the ViT-B/16 recipe): both residual-stream adds ride the output
+        # GEMMs' epilogues; fc2's dgrad epilogue applies fc1's GELU backward
+        h = self.attn_out(ctx, residual=h)
         y = self.layernorm_after(h)
-        return h + self.dropout(self.fc2(self.fc1(y)))
+        return self.fc2(self.fc1(y), fuse_dgelu=True, residual=h)
 
 
 class ViTForImageClassification(nn.Module):
@@ -81,7 +87,8 @@ class ViTForImageClassification(nn.Module):
 
     def forward(self, x):
         B = x.shape[0]
-        t = self.patch_embed(self.patchify(x))
+        # implicit im2col on the image (ops.patch_embed): no patchify copy on the GPU
+        t = ops.patch_embed(x, self.patch_embed.weight, self.patch_embed.bias, self.config.patch_size)
         t = torch.cat([self.cls_token.expand(B, -1, -1).to(t.dtype), t], 1) + self.position_embeddings.to(t.dtype)
         h = self.dropout(t)
         for layer in self.layers:

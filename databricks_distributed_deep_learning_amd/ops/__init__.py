@@ -11,7 +11,7 @@ a 16-byte vector), conv weights are [Cout, KH, KW, Cin], linear weights are
 """
 from ._lib import available as native_available, set_mode as set_native_mode, mode as native_mode  # noqa: F401
 from ._lib import NativeUnavailable  # noqa: F401
-from .conv import conv2d, conv2d_bias_act  # noqa: F401
+from .conv import conv2d, conv2d_bias_act, patch_embed  # noqa: F401
 from .norm import batch_norm, batch_norm_add_bn, bn_relu_maxpool, layer_norm  # noqa: F401
 from .linear import linear  # noqa: F401
 from .activation import gelu, dropout, relu  # noqa: F401

@@ -215,3 +215,49 @@ def grad_ready(param) -> None:
     cb = getattr(param, "_ddl_grad_ready", None)
     if cb is not None:
         cb()
+
+
+# ------------------------------------------------------------------ concurrent weight gradients
+# A layer's input gradient (dgrad) and its weight gradient (wgrad) are independent GEMMs.
+# With DDL_WGRAD_STREAM=1 the wgrad is issued on a side stream, ordered after everything
+# the compute stream has issued so far (its operands, the arena's zeroing), and the compute
+# stream joins it right after: the two GEMMs of ONE layer run concurrently -- a dgrad
+# whose tile grid leaves CUs idle (BERT's N = 768 GEMMs: 192 tiles on 256 CUs) shares the
+# chip with the wgrad -- while the next layer's backward and the gradient reducer's
+# bucket launch (ordered after the compute stream) still see the finished gradient.
+import contextlib as _contextlib  # noqa: E402
+
+_WGRAD_STREAM = os.environ.get("DDL_WGRAD_STREAM", "0") != "0"
+_side: dict = {}
+
+
+def wgrad_stream_enabled() -> bool:
+    return _WGRAD_STREAM
+
+
+def set_wgrad_stream(enabled: bool) -> None:
+    global _WGRAD_STREAM
+    _WGRAD_STREAM = bool(enabled)
+
+
+@_contextlib.contextmanager
+def side_stream(*tensors: torch.Tensor):
+    """Run the block on this device's side stream (when enabled and not capturing), then
+    make the compute stream wait for it.  ``tensors`` are the block's inputs allocated on
+    the compute stream: recorded on the side stream so the caching allocator does not
+    hand their memory out again before the side stream is done with it."""
+    if not _WGRAD_STREAM or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+        yield
+        return
+    compute = torch.cuda.current_stream()
+    dev = compute.device
+    s = _side.get(dev)
+    if s is None:
+        s = _side[dev] = torch.cuda.Stream(device=dev)
+    s.wait_stream(compute)
+    with torch.cuda.stream(s):
+        yield
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(s)
+    compute.wait_stream(s)

@@ -466,8 +466,10 @@ class _Conv(torch.autograd.Function):
                 dx = None       # the sibling conv's dgrad epilogue adds it
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
+            # concurrent with the dgrad just issued (DDL_WGRAD_STREAM, _lib.side_stream)
             if sink is not None and sink.shape == w.shape:
-                _wgrad(dy, x, w.shape, ctx.stride, ctx.pad, out=sink)
+                with _lib.side_stream(dy, x):
+                    _wgrad(dy, x, w.shape, ctx.stride, ctx.pad, out=sink)
                 grad_ready(ctx.w_param)
             else:
                 dw = _wgrad(dy, x, w.shape, ctx.stride, ctx.pad)
@@ -543,6 +545,65 @@ class _StemConvS2D(torch.autograd.Function):
 
 
 _STEM_S2D = os.environ.get("DDL_STEM_S2D", "1") != "0"
+
+
+class _PatchEmbed(torch.autograd.Function):
+    """ViT patch embedding (P x P patches, stride P) as an implicit-im2col GEMM on the
+    image itself -- no patchify copy.
+
+    NHWC ``[B, H, W, C]`` is reinterpreted (a view) as ``[B*H/P, P, W/P, P*C]``: one
+    "image" per patch row, ``P`` rows of ``W/P`` super-pixels of ``P*C`` contiguous
+    channels.  The patch embedding is then a ``P x 1`` stride-1 convolution of it with
+    output ``[B*H/P, 1, W/P, D]`` = ``[B, patches, D]`` in patch order, and the reduction
+    index ``(kh, kw*C + c)`` is exactly the ``(kh, kw, c)`` order of the weight (HF's
+    ``[D, C, P, P]`` projection permuted, ``models/vit.py`` ``from_hf_state_dict``).  The
+    bias rides the GEMM epilogue.  Backward: the weight gradient as the conv's wgrad
+    (implicit im2col again), the bias gradient as column sums; no input gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, P):
+        B, H, W_, C = x.shape
+        D = w.shape[0]
+        xv = x.contiguous().view(B * (H // P), P, W_ // P, P * C)
+        wv = w.contiguous().view(D, P, 1, P * C)
+        y = _fwd(xv, wv, 1, 0, bias=b)
+        ctx.save_for_backward(xv)
+        ctx.params = (w, b)
+        ctx.wshape = wv.shape
+        return y.view(B, (H // P) * (W_ // P), D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xv,) = ctx.saved_tensors
+        w, b = ctx.params
+        D = w.shape[0]
+        dy4 = dy.contiguous().view(xv.shape[0], 1, xv.shape[2], D)
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            sink = grad_sink(w)
+            if sink is not None:
+                _wgrad(dy4, xv, ctx.wshape, 1, 0, out=sink.view(ctx.wshape))
+                grad_ready(w)
+            else:
+                dw = _wgrad(dy4, xv, ctx.wshape, 1, 0).view(w.shape)
+        if b is not None and ctx.needs_input_grad[2]:
+            from ._native_elementwise import colsum
+            sink = grad_sink(b)
+            if sink is not None:
+                colsum(dy4.view(-1, D), sink, accumulate=True)
+                grad_ready(b)
+            else:
+                db = colsum(dy4.view(-1, D), torch.empty(D, dtype=torch.float32, device=dy.device)).to(b.dtype)
+        return None, dw, db, None
+
+
+def patch_embed(x, w, b, P):
+    """[B, H, W, C] NHWC image -> [B, (H/P)(W/P), D] patch embeddings (None if not covered)."""
+    B, H, W_, C = x.shape
+    if (x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or (b is not None and b.dtype != w.dtype)
+            or H % P or W_ % P or (P * C) % 8 or w.shape[0] % 8 or w.shape[1] != P * P * C or x.requires_grad):
+        return None
+    return _PatchEmbed.apply(x, w, b, P)
 
 
 def conv2d(x, w, stride, padding, bridge=None, stats=None, grad_to=None):

@@ -54,7 +54,7 @@ def _transposed(param, w: torch.Tensor) -> torch.Tensor:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, bridge=None, fuse_dgelu=False):
+    def forward(ctx, x, w, b, act, bridge=None, fuse_dgelu=False, residual=None):
         ctx.w_param, ctx.b_param = w, b
         ctx.bridge = bridge
         # GELU chain (FFN): this layer's input is the output of a GELU Linear whose only
@@ -73,8 +73,14 @@ class _Linear(torch.autograd.Function):
         z = None
         if act == "gelu" and any(ctx.needs_input_grad[:3]):   # grad mode is off inside forward
             z = torch.empty_like(y)
-        gemm(MODE_NT, x2, K, w, K, y, N, M, N, K, bias=b, act=act, aux=z)
+        res = None
+        if residual is not None:
+            res = residual.reshape(M, N)
+            if not res.is_contiguous() or res.dtype != y.dtype:
+                res = res.contiguous().to(y.dtype)
+        gemm(MODE_NT, x2, K, w, K, y, N, M, N, K, bias=b, act=act, aux=z, residual=res)
         ctx.act = act
+        ctx.has_res = residual is not None
         ctx.has_bias = b is not None
         ctx.save_for_backward(x2, w, z if act == "gelu" else (y if act in ("tanh", "relu") else None))
         ctx.xshape = x.shape
@@ -82,7 +88,7 @@ class _Linear(torch.autograd.Function):
         if z is not None:
             ctx.gelu_token = object()
             out._ddl_gelu_pre = (z, ctx.gelu_token)
-        elif b is not None and act is None:
+        elif b is not None and act is None and residual is None:
             # a LayerNorm consuming ``out`` may add the column sums of its input gradient
             # (this bias's gradient) straight into the bias's arena slot
             out._ddl_bias_param = b
@@ -93,6 +99,8 @@ class _Linear(torch.autograd.Function):
         x2, w, saved = ctx.saved_tensors
         M, K = x2.shape
         N = w.shape[0]
+        # the residual's gradient is dy itself (identity add in the epilogue)
+        dres = dy if ctx.has_res else None
         dy2 = dy.reshape(M, N)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
@@ -167,12 +175,16 @@ class _Linear(torch.autograd.Function):
             ctx.bridge.take()
         if ctx.needs_input_grad[1]:
             sink = grad_sink(ctx.w_param)
-            if sink is not None:       # accumulate straight into the reducer's gradient arena
-                gemm(MODE_TN, dz, N, x2, K, sink, K, N, K, M, accumulate=True)
-                grad_ready(ctx.w_param)
-            else:
+            if sink is None:
                 dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
-                gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
+            # concurrent with the dgrad just issued (DDL_WGRAD_STREAM, _lib.side_stream)
+            with _lib.side_stream(dz, x2):
+                if sink is not None:       # accumulate straight into the reducer's gradient arena
+                    gemm(MODE_TN, dz, N, x2, K, sink, K, N, K, M, accumulate=True)
+                else:
+                    gemm(MODE_TN, dz, N, x2, K, dw, K, N, K, M)
+            if sink is not None:
+                grad_ready(ctx.w_param)
         sunk = getattr(ctx.b_param, "_ddl_sunk", None) if ctx.has_bias else None
         if sunk is not None:
             ctx.b_param._ddl_sunk = None
@@ -215,7 +227,7 @@ class _Linear(torch.autograd.Function):
             else:
                 db = torch.empty(N, dtype=w.dtype, device=w.device)
                 E.colsum(dz, db)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, dres
 
 
 def _colsum_rows(dy, act, N):
@@ -258,9 +270,11 @@ class _DgeluHandoff:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str],
-           bridge=None, fuse_dgelu: bool = False) -> torch.Tensor:
-    if not _ok(x, w) or (b is not None and b.dtype != w.dtype):
+           bridge=None, fuse_dgelu: bool = False, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _ok(x, w) or (b is not None and b.dtype != w.dtype) or \
+            (residual is not None and residual.shape[-1] != w.shape[0]):
         from .bridge import join
         from .linear import linear_reference
-        return linear_reference(join(x, bridge), w, b, act)
-    return _Linear.apply(x, w, b, act, bridge, fuse_dgelu)
+        y = linear_reference(join(x, bridge), w, b, act)
+        return y if residual is None else y + residual
+    return _Linear.apply(x, w, b, act, bridge, fuse_dgelu, residual)

@@ -60,3 +60,18 @@ def conv2d_bias_act(x, w, b, stride=1, padding=0, relu=False, residual=None):
         from . import _native_conv
         return _native_conv.conv2d_bias_act(x, w, b, stride, padding, relu, residual)
     return conv2d_bias_act_reference(x, w, b, stride, padding, relu, residual)
+
+
+def patch_embed(x: torch.Tensor, w: torch.Tensor, b, patch: int) -> torch.Tensor:
+    """ViT patch embedding of an NHWC image with a ``[D, P*P*C]`` weight in (kh, kw, c)
+    order: ``[B, H, W, C] -> [B, (H/P)(W/P), D]``.  GPU: implicit-im2col GEMM on the image
+    (``_native_conv._PatchEmbed``); otherwise patchify + Linear."""
+    if _lib.use_native(x):
+        from . import _native_conv
+        y = _native_conv.patch_embed(x, w, b, patch)
+        if y is not None:
+            return y
+    from .linear import linear
+    B, Hh, Ww, C = x.shape
+    t = x.view(B, Hh // patch, patch, Ww // patch, patch, C).permute(0, 1, 3, 2, 4, 5)
+    return linear(t.reshape(B, (Hh // patch) * (Ww // patch), patch * patch * C), w, b)

@@ -4,7 +4,7 @@
 #   bash scripts/gpu.sh STEP [STEP ...]       e.g.  bash scripts/gpu.sh tests smoke bench "prof resnet50"
 #
 # Steps (each under its own time limit; the script stops at the first failing step):
-#   tests                 full GPU test suite                 -> gpurun_out/test_gpu.log
+#   tests [FILES]         GPU test suite (default all of tests/) -> gpurun_out/test_gpu.log
 #   smoke                 __graft_entry__.smoke()             -> gpurun_out/smoke.log
 #   bench [args]          bench.py (default 20 steps, 5 warm-up) -> gpurun_out/bench.log
 #   stock [args]          bench.py --native stock (plain PyTorch-ROCm + torch DDP arm)
@@ -40,7 +40,8 @@ step() {
   echo "=== [$name] $*" >&2
   case $name in
     tests)
-      timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread "$@" \
+      # args: test files / node ids (default: the whole tests/ directory)
+      timeout -k 10 700 python -u -m pytest "${@:-tests}" -m gpu -x -q --timeout 180 --timeout-method thread \
         > gpurun_out/test_gpu.log 2>&1 || { tail -40 gpurun_out/test_gpu.log; return 1; }
       tail -1 gpurun_out/test_gpu.log ;;
     smoke)

@@ -355,3 +355,29 @@ def test_conv_dgrad_weight_layout(K, R, S, C, rs, ss):
     out = _w_dgrad(w, rs, ss)
     ref = w[:, rs][:, :, ss].permute(3, 1, 2, 0).contiguous()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("B,H,P,D", [(4, 224, 16, 768), (3, 64, 16, 256), (2, 32, 8, 64)])
+def test_patch_embed_implicit_im2col(B, H, P, D):
+    """ViT patch embedding as an implicit-im2col GEMM on the NHWC image (no patchify copy)
+    == patchify + Linear in fp32, forward and weight / bias gradients (arena sinks)."""
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    torch.manual_seed(2)
+    x = torch.randn(B, H, H, 3, device=dev).bfloat16()
+    w = (torch.randn(D, P * P * 3, device=dev) * 0.05).bfloat16().requires_grad_(True)
+    b = (torch.randn(D, device=dev) * 0.1).bfloat16().requires_grad_(True)
+    y = NC.patch_embed(x, w, b, P)
+    assert y is not None
+    xr = x.float().view(B, H // P, P, H // P, P, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, (H // P) ** 2, P * P * 3)
+    wr, br = w.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
+    yr = xr @ wr.t() + br
+    _close(y, yr, 2e-2, 1e-2, "patch embed fwd")
+    g = torch.randn_like(yr).bfloat16()
+    y.backward(g)
+    yr.backward(g.float())
+    _close(w.grad, wr.grad, 3e-2, 1e-2, "patch embed dW")
+    _close(b.grad, br.grad, 3e-2, 1e-2, "patch embed db")
+    assert ops.patch_embed(x, w, b, P).shape == (B, (H // P) ** 2, D)

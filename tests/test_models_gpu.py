@@ -183,3 +183,29 @@ def test_downsample_sibling_bridge(kind, stride):
         finally:
             R._BRIDGE = True
     assert _rel(grads[True], grads[False]) < 1e-2
+
+
+@pytest.mark.parametrize("preset,over", [
+    ("resnet50_ddp", dict(model="resnet18", batch_size=16, image_size=64, num_classes=10)),
+    ("bert_base_ddp", dict(batch_size=8, seq_len=64)),
+])
+def test_side_stream_weight_gradients_match(preset, over):
+    """Weight-gradient GEMMs on the side stream (concurrent with the same layer's dgrad,
+    _lib.side_stream) give bit-identical training to the single-stream order."""
+    gpu_device()
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.ops import _lib
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    finals = []
+    prev = _lib.wgrad_stream_enabled()
+    try:
+        for on in (False, True):
+            _lib.set_wgrad_stream(on)
+            t = Trainer(get_preset(preset, steps=3, warmup_steps=1, log_every=0, **over))
+            t.run()
+            torch.cuda.synchronize()
+            finals.append(t.arena.flat.float().clone())
+            del t
+    finally:
+        _lib.set_wgrad_stream(prev)
+    assert torch.equal(finals[0], finals[1]), (finals[0] - finals[1]).abs().max()
