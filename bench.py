@@ -77,13 +77,17 @@ def run_one(model: str, args, world: int):
     if args.native == "stock":
         from databricks_distributed_deep_learning_amd.baselines import run_stock
         batch = (args.batch or 256) if model == "resnet50" else (args.bert_batch or 128)
-        return run_stock(model, batch, args.steps, args.warmup, seq_len=128, bucket_mb=args.bucket_mb)
+        return run_stock(model, batch, args.steps, args.warmup, seq_len=128, bucket_mb=args.bucket_mb,
+                         pad_fraction=args.bert_pad_fraction)
     from databricks_distributed_deep_learning_amd.config import get_preset
     from databricks_distributed_deep_learning_amd.training.loop import Trainer
     if model == "resnet50":
         cfg = get_preset("resnet50_ddp", batch_size=args.batch or 256)
     else:
-        cfg = get_preset("bert_base_ddp", batch_size=args.bert_batch or 128, dropout=0.1)
+        # --bert-pad-fraction > 0: HF-style right-padded batches with an attention mask (the
+        # masked attention path a real fine-tune runs); 0 = full-length sequences, no mask
+        cfg = get_preset("bert_base_ddp", batch_size=args.bert_batch or 128, dropout=0.1,
+                         pad_fraction=args.bert_pad_fraction)
     cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
                       bucket_mb=args.bucket_mb, backend=args.backend,
                       zero_optimizer=args.zero, sync_bn=args.sync_bn,
@@ -102,6 +106,8 @@ def main() -> int:
     ap.add_argument("--model", default="both", choices=["both", "resnet50", "bert_base"])
     ap.add_argument("--batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
     ap.add_argument("--bert-batch", type=int, default=0, help="BERT-base per-GPU batch (default 128)")
+    ap.add_argument("--bert-pad-fraction", type=float, default=0.0,
+                    help="BERT: random right-padding up to this fraction of the sequence, with attention mask")
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off", "stock"],
                     help="auto/on: HIP kernels; stock: plain PyTorch-ROCm + torch DDP arm; "
                          "off: the framework's CPU-oracle ops (correctness reference, not a baseline)")

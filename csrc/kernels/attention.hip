@@ -18,7 +18,10 @@
 // kernel (one workgroup per 64 queries, loops over keys): every sum stays on
 // chip, no atomics; P is recomputed from the saved log-sum-exp.
 // Dropout on the attention probabilities: one lowbias32 hash per pair of score
-// indices ((b*H+h)*S + q)*S + k (attn_hash below), regenerated in backward.
+// indices ((b*H+h)*S + q)*S + k (attn_hash below), drawn in the forward, which also
+// stores the keep decisions as a bit mask (1 bit per score, dmask_word below); the
+// backward kernels read the bits instead of re-hashing every score (lane = key in
+// the dK/dV passes: one hash per score there cost ~2.4x the pass's MFMA time).
 #include "ddl_common.h"
 
 #include <algorithm>
@@ -89,17 +92,21 @@ __device__ __forceinline__ uint4 zero_unless(bool ok, uint4 v) {
     return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
 }
 
-// stage a [64 rows][64] bf16 tile (rows >= nrows -> 0) with 256 threads: 2 chunks each
+// stage a [64 rows][64] bf16 tile (rows >= nrows -> 0) with 256 threads: 2 chunks each.
+// load() keeps the RAW loaded chunks and only records which rows are past the end; the zero
+// select happens in store(): a select right after the load made the compiler wait for the
+// load there (s_waitcnt vmcnt(0) straight behind the prefetch), so a tile "prefetched" under
+// the previous tile's compute was in fact waited for before that compute started
 struct Stager {
     uint4 v[2];
+    bool ok[2];
     __device__ __forceinline__ void load(const bf16_t* base, long row_stride, int row0, int nrows) {
         const int t = threadIdx.x;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int r = (t >> 3) + 32 * i, c = t & 7;
-            const bool ok = row0 + r < nrows;
-            const uint4 x = *reinterpret_cast<const uint4*>(base + (long)(ok ? row0 + r : 0) * row_stride + c * 8);
-            v[i] = zero_unless(ok, x);
+            ok[i] = row0 + r < nrows;
+            v[i] = *reinterpret_cast<const uint4*>(base + (long)(ok[i] ? row0 + r : 0) * row_stride + c * 8);
         }
     }
     template <bool TR>
@@ -108,7 +115,7 @@ struct Stager {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int r = (t >> 3) + 32 * i, c = t & 7;
-            *reinterpret_cast<uint4*>(lds + lds_off<TR>(r, c)) = v[i];
+            *reinterpret_cast<uint4*>(lds + lds_off<TR>(r, c)) = zero_unless(ok[i], v[i]);
         }
     }
 };
@@ -147,16 +154,41 @@ __device__ __forceinline__ void mask4(const float* mrow, int k0, int S, float (&
     }
 }
 
+// Dropout keep-bit layout: word ((bh * NKW + kw) * 4 + g) * S + q, NKW = ceil(S / 128), bit
+// 4 * blk + r  <->  key kw * 128 + 16 * blk + 4 * g + r (blk 0..7): the bits one forward lane
+// holds (query on the lane, keys 16 blk + 4 g + r in its accumulators) are one word.
+__host__ __device__ __forceinline__ int dmask_nkw(int S) { return (S + 127) >> 7; }
+__device__ __forceinline__ long dmask_word(int bh, int S, int kw, int g, int q) {
+    return ((long)(bh * dmask_nkw(S) + kw) * 4 + g) * S + q;
+}
+// keep bits of queries q0 .. q0+3 for one key (lane = key): the 4 words of (kw, g) of that key
+__device__ __forceinline__ uint4 dmask_words4(const uint32_t* __restrict__ dm, long w0, int q0, int S) {
+    if (((S | q0) & 3) == 0 && q0 + 3 < S) return *reinterpret_cast<const uint4*>(dm + w0);
+    return make_uint4(q0 < S ? dm[w0] : 0u, q0 + 1 < S ? dm[w0 + 1] : 0u, q0 + 2 < S ? dm[w0 + 2] : 0u,
+                      q0 + 3 < S ? dm[w0 + 3] : 0u);
+}
+
+// bit `bit` of each of the 4 words, packed into bits 0..3 (one register per 4 queries)
+__device__ __forceinline__ uint32_t dmask_pick4(uint4 w, int bit) {
+    return ((w.x >> bit) & 1u) | (((w.y >> bit) & 1u) << 1) | (((w.z >> bit) & 1u) << 2) | (((w.w >> bit) & 1u) << 3);
+}
+
 __device__ __forceinline__ bf16x8 load_frag_global(const bf16_t* rowp, int kk) {
     const int l = threadIdx.x & 63;
     return *reinterpret_cast<const bf16x8*>(rowp + kk * 32 + 8 * (l >> 4));
 }
 
 // ============================================================ forward
-__global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+// (256, 3): three waves per SIMD -- the compiler then allocates 144 VGPRs instead of 176 (two
+// waves per SIMD) without spilling; the tiled kernels wait on memory ~45-50 % of wave time,
+// which more resident waves hide (same for the two backward kernels below)
+__global__ __launch_bounds__(256, 3) void attn_fwd_k(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                   bf16_t* __restrict__ out, float* __restrict__ lse, int B, int S, int H,
-                                                  float scale, float p_drop, uint64_t seed) {
+                                                  float scale, float p_drop, uint64_t seed, uint32_t* __restrict__ dmask) {
     __shared__ __attribute__((aligned(16))) char smem[4 * TK * ROWB];   // K0 V0 K1 V1
+    // the tiles' additive key mask (scaled to log2), staged with K / V: an in-loop global load of
+    // it made the compiler wait out the K / V prefetch (vmcnt counts every load in order)
+    __shared__ __attribute__((aligned(16))) float s_mk[2][TK];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
     const long rs = 3L * H * D;                              // qkv row stride
@@ -184,19 +216,31 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
     const float* mrow = mask ? mask + (long)b * S : nullptr;
 
     const int nt = (S + TK - 1) / TK;
+    uint32_t kbits = 0;                                      // dropout keep bits of a 128-key word
     Stager sk, sv;
+    float nmk = 0.f;                                         // raw load; scaled / bounded at the store
+    bool mk_ok = false;
+    auto load_mk = [&](int t) __attribute__((always_inline)) {
+        const int k = t * TK + (int)threadIdx.x;
+        mk_ok = k < S;
+        if (mrow && threadIdx.x < TK) nmk = mrow[min(k, S - 1)];
+    };
     sk.load(kb, rs, 0, S);
     sv.load(vb, rs, 0, S);
+    load_mk(0);
     sk.store<false>(smem);
     sv.store<true>(smem + TK * ROWB);
+    if (mrow && threadIdx.x < TK) s_mk[0][threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         char* sK = smem + (t & 1) * 2 * TK * ROWB;
         char* sV = sK + TK * ROWB;
+        const float* sM = s_mk[t & 1];
         const bool more = t + 1 < nt;
         if (more) {
             sk.load(kb, rs, (t + 1) * TK, S);
             sv.load(vb, rs, (t + 1) * TK, S);
+            load_mk(t + 1);
         }
         // ---- S^T block: lane holds s[blk][r] = score(q = myq, k = t*64 + 16 blk + 4 g + r)
         f32x4 s[4];
@@ -214,12 +258,13 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
             const int k0 = t * TK + 16 * blk + 4 * g;
-            float mk[4] = {0.f, 0.f, 0.f, 0.f};
-            if (mrow) mask4(mrow, k0, S, mk);
+            float4 mk4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (mrow) mk4 = *reinterpret_cast<const float4*>(sM + 16 * blk + 4 * g);
+            const float mk[4] = {mk4.x, mk4.y, mk4.z, mk4.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float v = s[blk][r] * c2;
-                if (mrow) v += mk[r] * LOG2E;
+                if (mrow) v += mk[r];
                 if (tail && k0 + r >= S) v = -INFINITY;
                 s[blk][r] = v;
                 tmax = fmaxf(tmax, v);
@@ -240,9 +285,16 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
             for (int r = 0; r < 4; ++r) {
                 float pv = fast_exp2(s[blk][r] - msub);
                 psum += pv;
-                if (p_drop > 0.f) pv = keep[r] ? pv * inv_keep : 0.f;
+                if (p_drop > 0.f) {
+                    pv = keep[r] ? pv * inv_keep : 0.f;
+                    kbits |= (uint32_t)keep[r] << ((t & 1) * 16 + 4 * blk + r);
+                }
                 s[blk][r] = pv;
             }
+        }
+        if (p_drop > 0.f && ((t & 1) || t == nt - 1)) {      // a 128-key word is complete
+            if (qok) dmask[dmask_word(bh, S, t >> 1, g, myq)] = kbits;
+            kbits = 0;
         }
         lsum = lsum * alpha + psum;
 #pragma unroll
@@ -259,6 +311,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16_t* __restrict__ qkv
             char* nK = smem + ((t + 1) & 1) * 2 * TK * ROWB;
             sk.store<false>(nK);
             sv.store<true>(nK + TK * ROWB);
+            if (mrow && threadIdx.x < TK) s_mk[(t + 1) & 1][threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
         }
         __syncthreads();
     }
@@ -304,12 +357,16 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16_t* __restrict__ d
 
 // ============================================================ backward dK, dV
 // workgroup = 64 keys of one (b, h); wave w owns keys k0 + 16 w .. +15 (key on the lane).
-__global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
-                                                      int S, int H, float scale, float p_drop, uint64_t seed) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * TQ * ROWB];   // Q, dO tiles
+                                                      int S, int H, float scale, float p_drop,
+                                                      const uint32_t* __restrict__ dmask) {
+    // Q, dO tiles as row images (S, dP fragments) and transposed-read images (dK, dV fragments):
+    // the tr reads on a row image were 23 % bank-conflicted
+    __shared__ __attribute__((aligned(16))) char smem[4 * TQ * ROWB];
     __shared__ float s_lse[TQ], s_delta[TQ];
+    __shared__ __attribute__((aligned(16))) uint32_t s_dm[4 * TQ];      // this tile's keep words [g][q]
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -330,27 +387,51 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
     }
     const float mbias = (mask && kok) ? mask[(long)b * S + myk] : 0.f;
     const float c2 = scale * LOG2E;
-    const uint32_t thresh = drop_thresh16(p_drop);
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    // my key's keep bits: word (kw, gk) of each query (staged per tile in s_dm), bit kbit; the
+    // workgroup's 64 keys share kw
+    const int kq = kok ? myk : 0;
+    const int kw_blk = (blockIdx.x * TK) >> 7;
+    const uint32_t* dmw = s_dm + ((kq >> 2) & 3) * TQ;
+    const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
     f32x4 dv[4], dk[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
     char* sQ = smem;
     char* sO = smem + TQ * ROWB;
+    char* sQt = smem + 2 * TQ * ROWB;
+    char* sOt = smem + 3 * TQ * ROWB;
     const int nt = (S + TQ - 1) / TQ;
-    for (int t = 0; t < nt; ++t) {
-        Stager a, c;
+    // tile t+1's Q / dO rows, keep words, LSE and delta are loaded into registers while tile t
+    // computes (the single-buffered loop waited out every tile's loads)
+    Stager a, c;
+    uint32_t wd = 0;
+    float nlse = 0.f, ndel = 0.f;
+    auto fetch = [&](int t) __attribute__((always_inline)) {
         a.load(qb, rs, t * TQ, S);
         c.load(dob, (long)H * D, t * TQ, S);
+        const int q = t * TQ + (threadIdx.x & (TQ - 1));
+        if (p_drop > 0.f)            // keep word (g, q) of the tile, one per thread
+            wd = q < S ? dmask[dmask_word(bh, S, kw_blk, threadIdx.x >> 6, q)] : 0u;
+        if (threadIdx.x < TQ) {
+            nlse = q < S ? lse[(long)bh * S + q] : 0.f;
+            ndel = q < S ? delta[(long)bh * S + q] : 0.f;
+        }
+    };
+    fetch(0);
+    for (int t = 0; t < nt; ++t) {
         __syncthreads();             // previous tile fully consumed
         a.store<false>(sQ);
         c.store<false>(sO);
+        a.store<true>(sQt);
+        c.store<true>(sOt);
+        if (p_drop > 0.f) s_dm[threadIdx.x] = wd;
         if (threadIdx.x < TQ) {
-            const int q = t * TQ + threadIdx.x;
-            s_lse[threadIdx.x] = q < S ? lse[(long)bh * S + q] : 0.f;
-            s_delta[threadIdx.x] = q < S ? delta[(long)bh * S + q] : 0.f;
+            s_lse[threadIdx.x] = nlse;
+            s_delta[threadIdx.x] = ndel;
         }
         __syncthreads();
+        if (t + 1 < nt) fetch(t + 1);
         // S[q][k] and dP[q][k]: lane holds q = t*64 + 16 qb + 4 g + r, k = myk
         f32x4 sc[4], dp[4];
 #pragma unroll
@@ -365,7 +446,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
         }
         f32x4 pd[4], ds[4];
 #pragma unroll
-        for (int qbk = 0; qbk < 4; ++qbk)
+        for (int qbk = 0; qbk < 4; ++qbk) {
+            const int qa = t * TQ + 16 * qbk + 4 * g;
+            const uint32_t kb4 = p_drop > 0.f ? dmask_pick4(*reinterpret_cast<const uint4*>(dmw + (qa - t * TQ)), kbit)
+                                              : 0xfu;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ql = 16 * qbk + 4 * g + r;
@@ -374,16 +458,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
                 float dpv = dp[qbk][r];
                 float pdrop = pv;
                 if (p_drop > 0.f) {
-                    // lane = key, elements along queries: consecutive elements are S indices
-                    // apart, so each needs its own pair hash
-                    const uint64_t idx = ((uint64_t)bh * S + q) * S + myk;
-                    const bool keep = attn_keep_half(attn_hash(seed, idx >> 1), idx, thresh);
+                    const bool keep = (kb4 >> r) & 1u;
                     pdrop = keep ? pv * inv_keep : 0.f;
                     dpv = keep ? dpv * inv_keep : 0.f;
                 }
                 pd[qbk][r] = pdrop;
                 ds[qbk][r] = pv * (dpv - s_delta[ql]);
             }
+        }
         // dV^T[d][k] += dO^T[d][q] Pd[q][k];  dK^T[d][k] += Q^T[d][q] dS[q][k]
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -391,8 +473,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
             const bf16x8 sf = pack_acc(ds[2 * st], ds[2 * st + 1]);
 #pragma unroll
             for (int db = 0; db < 4; ++db) {
-                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sO, 32 * st, 16 * db), pf, dv[db], 0, 0, 0);
-                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sQ, 32 * st, 16 * db), sf, dk[db], 0, 0, 0);
+                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sOt, 32 * st, 16 * db), pf, dv[db], 0, 0, 0);
+                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sQt, 32 * st, 16 * db), sf, dk[db], 0, 0, 0);
             }
         }
     }
@@ -410,11 +492,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16_t* __restrict__
 
 // ============================================================ backward dQ
 // workgroup = 64 queries; wave owns 16 queries (query on the lane), loops over key tiles.
-__global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                      const float* __restrict__ lse, const float* __restrict__ delta,
                                                      const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
-                                                     int S, int H, float scale, float p_drop, uint64_t seed) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * TK * ROWB];   // K, V tiles
+                                                     int S, int H, float scale, float p_drop,
+                                                     const uint32_t* __restrict__ dmask) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * TK * ROWB];   // K, V tiles + K as a tr-read image
+    __shared__ __attribute__((aligned(16))) float s_mk[TK];            // the tile's additive key mask (log2)
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -434,24 +518,47 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
     const float my_lse = qok ? lse[(long)bh * S + myq] : 0.f;
     const float my_delta = qok ? delta[(long)bh * S + myq] : 0.f;
     const float c2 = scale * LOG2E;
-    const uint32_t thresh = drop_thresh16(p_drop);
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-    const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;
     const float* mrow = mask ? mask + (long)b * S : nullptr;
+    // this query's keep words, one per 128 keys, loaded up front (S <= 512 here: 4 words)
+    constexpr int MAXKW = 4;
+    uint32_t kwds[MAXKW] = {~0u, ~0u, ~0u, ~0u};
+    if (p_drop > 0.f && qok) {
+#pragma unroll
+        for (int i = 0; i < MAXKW; ++i)
+            if (i < dmask_nkw(S)) kwds[i] = dmask[dmask_word(bh, S, i, g, myq)];
+    }
     f32x4 dq[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
     char* sK = smem;
     char* sV = smem + TK * ROWB;
+    char* sKt = smem + 2 * TK * ROWB;
     const int nt = (S + TK - 1) / TK;
+    // tile t+1's K / V rows (and key mask) are loaded into registers while tile t computes
+    Stager a, c;
+    float nmk = 0.f;                                         // raw load; scaled / bounded at the store
+    bool mk_ok = false;
+    auto load_mk = [&](int t) __attribute__((always_inline)) {
+        const int k = t * TK + (int)threadIdx.x;
+        mk_ok = k < S;
+        if (mrow && threadIdx.x < TK) nmk = mrow[min(k, S - 1)];
+    };
+    a.load(kb, rs, 0, S);
+    c.load(vb, rs, 0, S);
+    load_mk(0);
     for (int t = 0; t < nt; ++t) {
-        Stager a, c;
-        a.load(kb, rs, t * TK, S);
-        c.load(vb, rs, t * TK, S);
         __syncthreads();
         a.store<false>(sK);
         c.store<false>(sV);
+        a.store<true>(sKt);
+        if (mrow && threadIdx.x < TK) s_mk[threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
         __syncthreads();
+        if (t + 1 < nt) {
+            a.load(kb, rs, (t + 1) * TK, S);
+            c.load(vb, rs, (t + 1) * TK, S);
+            load_mk(t + 1);
+        }
         // S^T[k][q], dP^T[k][q]: lane holds k = t*64 + 16 blk + 4 g + r, q = myq
         f32x4 sc[4], dp[4];
 #pragma unroll
@@ -466,19 +573,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
         }
         f32x4 ds[4];
         const float lse2 = my_lse * LOG2E;
+        // the forward's keep bits of my query for this tile's keys (one word per 128 keys)
+        uint32_t kbits = ~0u;
+        if (p_drop > 0.f && qok) {
+            const int kwi = t >> 1;
+            const uint32_t wv = kwi < MAXKW ? (kwi == 0 ? kwds[0] : kwi == 1 ? kwds[1] : kwi == 2 ? kwds[2] : kwds[3])
+                                            : dmask[dmask_word(bh, S, kwi, g, myq)];
+            kbits = wv >> ((t & 1) * 16);
+        }
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
             const int k0 = t * TK + 16 * blk + 4 * g;
-            float mk[4] = {0.f, 0.f, 0.f, 0.f};
-            if (mrow) mask4(mrow, k0, S, mk);
-            bool keep[4] = {true, true, true, true};
-            if (p_drop > 0.f) attn_keep4(seed, rowidx + k0, thresh, S & 1, keep);
+            float4 mk4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (mrow) mk4 = *reinterpret_cast<const float4*>(s_mk + 16 * blk + 4 * g);
+            const float mk[4] = {mk4.x, mk4.y, mk4.z, mk4.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const bool ok = qok && k0 + r < S;
-                const float pv = ok ? fast_exp2(sc[blk][r] * c2 + mk[r] * LOG2E - lse2) : 0.f;
+                const float pv = ok ? fast_exp2(sc[blk][r] * c2 + mk[r] - lse2) : 0.f;
                 float dpv = dp[blk][r];
-                if (p_drop > 0.f) dpv = keep[r] ? dpv * inv_keep : 0.f;
+                if (p_drop > 0.f) dpv = ((kbits >> (4 * blk + r)) & 1u) ? dpv * inv_keep : 0.f;
                 ds[blk][r] = pv * (dpv - my_delta);
             }
         }
@@ -488,7 +602,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16_t* __restrict__ 
             const bf16x8 sf = pack_acc(ds[2 * st], ds[2 * st + 1]);
 #pragma unroll
             for (int db = 0; db < 4; ++db)
-                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
+                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sKt, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
         }
     }
     if (!qok) return;
@@ -513,7 +627,8 @@ template <bool FULL, bool MASK, bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restrict__ qkv,
                                                             const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                             float* __restrict__ lse, int S, int H, float scale,
-                                                            float p_drop, uint64_t seed, int BH) {
+                                                            float p_drop, uint64_t seed, int BH,
+                                                            uint32_t* __restrict__ dmask) {
     // persistent: a workgroup walks (b, h) = blockIdx.x, + gridDim.x, ...; the next pair's K / V rows,
     // mask entry and Q fragments are loaded into registers while the current pair computes, and
     // staged into the other half of the double-buffered LDS images (the single-pair version
@@ -609,6 +724,7 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;
     float lsum = 0.f;
+    uint32_t kbits = 0;
 #pragma unroll
     for (int blk = 0; blk < 8; ++blk) {
         bool keep[4] = {true, true, true, true};
@@ -617,10 +733,14 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
         for (int r = 0; r < 4; ++r) {
             float pv = fast_exp2(s[blk][r] - msub);
             lsum += pv;
-            if (DROP) pv = keep[r] ? pv * inv_keep : 0.f;
+            if (DROP) {
+                pv = keep[r] ? pv * inv_keep : 0.f;
+                kbits |= (uint32_t)keep[r] << (4 * blk + r);
+            }
             s[blk][r] = pv;
         }
     }
+    if (DROP && qok) dmask[dmask_word(bh, S, 0, g, myq)] = kbits;   // for the backward
     lsum += __shfl_xor(lsum, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);
     // O^T[d][q] = V^T[d][k] P^T[k][q]
@@ -666,12 +786,13 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_short_k(const bf16_t* __restr
 // P and dP in both its dK/dV and its dQ kernel and reads Q/K/V/dO once per tile pair).
 // FULL: S == 128 (the query / key chunk loops unroll, no bounds checks); DROP: dropout on
 template <bool FULL, bool DROP>
-__global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restrict__ qkv,
                                                             const bf16_t* __restrict__ out,
                                                             const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
-                                                            int S, int H, float scale, float p_drop, uint64_t seed,
+                                                            int S, int H, float scale, float p_drop,
+                                                            const uint32_t* __restrict__ dmask,
                                                             float* __restrict__ colsum) {
     __shared__ __attribute__((aligned(16))) char smem[3 * FS * ROWB];   // Q, K, dO; then dS^T halves over Q, dO
     // colsum (nullable, [B][3 H D] fp32): this (b, h)'s column sums of dQ / dK / dV over the sequence --
@@ -680,6 +801,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
     __shared__ __attribute__((aligned(16))) float s_lse[FS];
     __shared__ __attribute__((aligned(16))) float s_delta[FS];
     __shared__ float s_mask[FS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_dm[DROP ? 4 * FS : 4];   // keep-bit words [g][q]
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -731,10 +853,13 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
         s_lse[tid] = tid < S ? lse[(long)bh * S + tid] * LOG2E : 0.f;
         s_mask[tid] = (mask && tid < S) ? mask[(long)b * S + tid] * LOG2E : 0.f;
     }
+    if (DROP) {   // the forward's dropout keep bits of this (b, h): word (g, q), one per thread
+        const int gq = tid >> 7, q = tid & (FS - 1);
+        s_dm[tid] = q < S ? dmask[dmask_word(bh, S, 0, gq, q)] : 0u;
+    }
     __syncthreads();
 
     const float c2 = scale * LOG2E;
-    const uint32_t thresh = drop_thresh16(p_drop);
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
 
     // ---- phase 1: lane = key
@@ -749,7 +874,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
             vf[kk] = load_frag_global(vr, kk);
         }
         const float mb2 = s_mask[kok ? myk : 0];
-        const uint64_t rowk = (uint64_t)bh * S * S + myk;     // score index of (q = 0, myk)
+        // my key's dropout keep bits: LDS words (gk, q), bit kbit
+        const int kq = kok ? myk : 0;
+        const uint32_t* dmw = s_dm + (DROP ? ((kq >> 2) & 3) * FS : 0);
+        const int kbit = (kq >> 4) * 4 + (kq & 3);
         f32x4 dv[4], dk[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
@@ -776,7 +904,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                 const int q0 = 32 * qc + 16 * j + 4 * g;
                 const f32x4 lse4 = *reinterpret_cast<const f32x4*>(s_lse + q0);     // one LDS read per 4 queries
                 const f32x4 del4 = *reinterpret_cast<const f32x4*>(s_delta + q0);
-                uint64_t idx = rowk + (uint64_t)q0 * S;                            // score index of (q0, myk)
+                // queries q0 .. q0+3: their keep bits for my key, packed into bits 0..3
+                const uint32_t kb4 = DROP ? dmask_pick4(*reinterpret_cast<const uint4*>(dmw + q0), kbit) : 0xfu;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int ql = q0 + r;
@@ -784,11 +913,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_k(const bf16_t* __restr
                     float dpv = dp[j][r];
                     float pdrop = pv;
                     if (DROP) {
-                        const bool keep = attn_keep_half(attn_hash(seed, idx >> 1), idx, thresh);
+                        const bool keep = (kb4 >> r) & 1u;
                         pdrop = keep ? pv * inv_keep : 0.f;
                         dpv = keep ? dpv * inv_keep : 0.f;
                     }
-                    idx += S;
                     pd[j][r] = pdrop;
                     ds[j][r] = pv * (dpv - del4[r]);
                 }
@@ -913,13 +1041,18 @@ bool fused_bwd_enabled() {
 }
 }  // namespace
 
+// dropout keep-bit words the forward writes and the backward reads (p_drop > 0)
+DDL_API long ddl_attn_dmask_words(int B, int S, int H) { return (long)B * H * dmask_nkw(S) * 4 * S; }
+
 // qkv [B, S, 3*H*64] bf16; mask: additive key bias [B, S] fp32 or null; out [B, S, H*64]; lse [B, H, S] fp32
+// dmask: ddl_attn_dmask_words uint32 (required when p_drop > 0): the dropout keep bits
 DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* lse, int B, int S, int H, float scale,
-                         float p_drop, uint64_t seed, hipStream_t st) {
+                         float p_drop, uint64_t seed, uint32_t* dmask, hipStream_t st) {
+    if (p_drop > 0.f && !dmask) return -5;
     if (S <= FS && fused_bwd_enabled()) {
         const bool full = S == FS, msk = mask != nullptr, drp = p_drop > 0.f;
         const int grid = std::min(B * H, 2 * num_cus());   // persistent: two workgroups per CU
-#define FWD_SHORT(F, M, D) attn_fwd_short_k<F, M, D><<<grid, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed, B * H)
+#define FWD_SHORT(F, M, D) attn_fwd_short_k<F, M, D><<<grid, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed, B * H, dmask)
         if (full) {
             if (msk) { if (drp) FWD_SHORT(true, true, true); else FWD_SHORT(true, true, false); }
             else { if (drp) FWD_SHORT(true, false, true); else FWD_SHORT(true, false, false); }
@@ -931,7 +1064,7 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
         DDL_RETURN_LAUNCH();
     }
     dim3 grid((S + TQ - 1) / TQ, B * H);
-    attn_fwd_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed);
+    attn_fwd_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed, dmask);
     DDL_RETURN_LAUNCH();
 }
 
@@ -939,11 +1072,12 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
 // colsum (nullable, [B][3 H 64] fp32): per-batch column sums of dqkv (the QKV bias gradient is their
 // column sum) -- single-workgroup path only (S <= 128): returns 1 when it was NOT written
 DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, const float* mask,
-                         float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop, uint64_t seed,
-                         float* colsum, hipStream_t st) {
+                         float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop,
+                         const uint32_t* dmask, float* colsum, hipStream_t st) {
+    if (p_drop > 0.f && !dmask) return -5;
     if (S <= FS && fused_bwd_enabled()) {   // the whole sequence fits one workgroup's LDS
 #define BWD_FUSED(F, DR) attn_bwd_fused_k<F, DR><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, \
-        (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, seed, colsum)
+        (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, dmask, colsum)
         if (S == FS) { if (p_drop > 0.f) BWD_FUSED(true, true); else BWD_FUSED(true, false); }
         else { if (p_drop > 0.f) BWD_FUSED(false, true); else BWD_FUSED(false, false); }
 #undef BWD_FUSED
@@ -953,9 +1087,9 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     attn_delta_k<<<(int)((rows * 8 + 255) / 256), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
     dim3 grid((S + TK - 1) / TK, B * H);
     attn_bwd_dkv_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B,
-                                         S, H, scale, p_drop, seed);
+                                         S, H, scale, p_drop, dmask);
     attn_bwd_dq_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B, S,
-                                        H, scale, p_drop, seed);
+                                        H, scale, p_drop, dmask);
     const int rc = (int)hipGetLastError();
     return rc ? rc : (colsum ? 1 : 0);
 }

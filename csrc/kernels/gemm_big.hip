@@ -675,10 +675,11 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
 // tile's loads instead of in a chip-wide burst between waves of blocks.
 // BNB: the BatchNorm-backward epilogue variant (its own instantiation, so the extra
 // registers it needs never weigh on the other epilogues)
-// EDGE = false: every tile is interior and the epilogue kind is one of the lean ones
-// (M, N multiples of 256 -- every BERT / ViT GEMM): the bounds-checked general epilogue
-// is not compiled in.  Its 64-bit per-site addresses were what spilled (35-72 VGPRs of
-// scratch in the persistent kernels); without it the NT kernel allocates spill-free.
+// EDGE = false (DDL_GEMM_LEAN=1): every tile is interior and the epilogue kind is one of the
+// lean ones (M, N multiples of 256): the bounds-checked general epilogue is not compiled in.
+// Its 64-bit per-site addresses are what spills (35-72 VGPRs of scratch in the persistent
+// kernels); without it the NT kernel allocates spill-free -- but runs slower (see
+// edge_split_enabled), so the spills are not on the interior tiles' critical path.
 template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false, bool EDGE = true>
 __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
@@ -1147,11 +1148,15 @@ bool direct_enabled() {
     return on;
 }
 
-// DDL_GEMM_LEAN=0 keeps the general-epilogue kernel for all-interior GEMMs too (A/B timing)
+// DDL_GEMM_LEAN=1 routes all-interior GEMMs to the variant without the general epilogue.
+// Off by default: spill-free as it is (the NT kernel), it measured 1.9 % SLOWER on BERT-base
+// same-box (8318-8333 vs 8473-8491 samples/s, 3 alternating runs each) -- the scratch the
+// general epilogue costs sits off the interior tiles' path, and the allocation the lean
+// variant gets in exchange schedules the main loop worse.
 bool edge_split_enabled() {
     static const bool on = [] {
         const char* e = getenv("DDL_GEMM_LEAN");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }

@@ -66,17 +66,14 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_partial_k(const T* __restrict_
     }
 }
 
+// channel c's statistics from its summed [sum | sumsq]: mean / invstd saved, running stats
+// updated, gamma / beta folded into (scale, shift)
 template <typename TP>
-__global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
-                                    const TP* __restrict__ gamma, const TP* __restrict__ beta,
-                                    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum,
-                                    float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                    float* __restrict__ scale, float* __restrict__ shift) {
-    __shared__ float red[1024];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
-    const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
-    if (threadIdx.x >= 64 || c >= C) return;
+__device__ __forceinline__ void bn_fwd_finish_channel(int c, double s, double q, long M, const TP* __restrict__ gamma,
+                                                      const TP* __restrict__ beta, float* __restrict__ running_mean,
+                                                      float* __restrict__ running_var, float momentum, float eps,
+                                                      float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                      float* __restrict__ scale, float* __restrict__ shift) {
     const double mean = s / (double)M;
     double var = q / (double)M - mean * mean;
     if (var < 0) var = 0;
@@ -92,6 +89,21 @@ __global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restr
     const float bb = beta ? to_f(beta[c]) : 0.f;
     scale[c] = g * invstd;
     shift[c] = bb - (float)mean * g * invstd;
+}
+
+template <typename TP>
+__global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+                                    const TP* __restrict__ gamma, const TP* __restrict__ beta,
+                                    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum,
+                                    float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
+    const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
+    if (threadIdx.x >= 64 || c >= C) return;
+    bn_fwd_finish_channel<TP>(c, s, q, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+                              save_invstd, scale, shift);
 }
 
 // eval mode: scale/shift from running statistics
@@ -299,15 +311,11 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
 }
 
 template <typename TP>
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
-                                  const TP* __restrict__ gamma, const float* __restrict__ invstd,
-                                  TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef,
-                                  int acc, const float* __restrict__ prow = nullptr) {
-    __shared__ float red[1024];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
-    const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
-    if (threadIdx.x >= 64 || c >= C) return;
+__device__ __forceinline__ void bn_bwd_finish_channel(int c, double s, double q, int C, long M,
+                                                      const TP* __restrict__ gamma, const float* __restrict__ invstd,
+                                                      TP* __restrict__ dgamma, TP* __restrict__ dbeta,
+                                                      float* __restrict__ coef, int acc,
+                                                      const float* __restrict__ prow) {
     // SyncBatchNorm: the coefficients need the group-summed row, but dgamma / dbeta are
     // this rank's partials (the data-parallel reducer sums them across ranks afterwards)
     const float ps = prow ? prow[c] : (float)s, pq = prow ? prow[C + c] : (float)q;
@@ -317,6 +325,19 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restric
     coef[c] = g * invstd[c];                 // k1
     coef[C + c] = (float)(s / (double)M);    // mean(dz)
     coef[2 * C + c] = (float)(q / (double)M);// mean(dz*xhat)
+}
+
+template <typename TP>
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ part, int nblk, int C, long M,
+                                  const TP* __restrict__ gamma, const float* __restrict__ invstd,
+                                  TP* __restrict__ dgamma, TP* __restrict__ dbeta, float* __restrict__ coef,
+                                  int acc, const float* __restrict__ prow = nullptr) {
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double s = colsum64(part, nblk, 2L * C, c, c < C, red);
+    const double q = colsum64(part, nblk, 2L * C, C + c, c < C, red);
+    if (threadIdx.x >= 64 || c >= C) return;
+    bn_bwd_finish_channel<TP>(c, s, q, C, M, gamma, invstd, dgamma, dbeta, coef, acc, prow);
 }
 
 template <typename T, bool RELU, bool DRES>
@@ -487,12 +508,17 @@ __global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T
 }
 
 // dx per row + dgamma/dbeta partials per block (ROWS_PER_BLK rows, 4 waves).
-template <typename T, int VPL>
+// ADD: dadd (the gradient of this LayerNorm's input from its other consumer -- a pre-LN
+// block's residual branch) is added to dx in the same pass, before the column sums, so dx is
+// the input's WHOLE gradient (no autograd add kernel, and the column sums are the producing
+// Linear's complete bias gradient)
+template <typename T, int VPL, bool ADD = false>
 __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                 const T* __restrict__ res, long res_rows, const T* __restrict__ gamma,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 T* __restrict__ dx, float* __restrict__ part, long rows, int H,
-                                                int rows_per_blk, int dxsum, Drop drop) {
+                                                int rows_per_blk, int dxsum, Drop drop,
+                                                const T* __restrict__ dadd = nullptr) {
     // part row per block: [dgamma(H) | dbeta(H) | (dxsum) sum of dx (H)] -- the last is the
     // bias gradient of the Linear that produced this LayerNorm's input
     __shared__ float s_acc[3][4][VPL * 256];
@@ -538,7 +564,15 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             }
         }
     };
-    auto finish_row = [&](long row, const float (&xv)[VPL][4], const float (&d)[VPL][4], const uint32_t (&kb)[VPL]) {
+    auto finish_row = [&](long row, const float (&xv)[VPL][4], const float (&d)[VPL][4], const RowRaw& R) {
+        const uint32_t (&kb)[VPL] = R.kb;
+        // the added gradient is loaded here, ahead of the row reductions, not a row pair ahead
+        // with the other operands (4 rows of it in flight cost the second wave per SIMD)
+        typename Raw4<T>::type ra[ADD ? VPL : 1];
+        if constexpr (ADD) {
+#pragma unroll
+            for (int k = 0; k < VPL; ++k) ra[k] = ld_raw4(dadd + row * H + 256 * k + 4 * lane);
+        }
         const float mu = mean[row], rs = rstd[row];
         float xh[VPL][4], gy[VPL][4];
         float s1 = 0.f, s2 = 0.f;
@@ -563,6 +597,12 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             if (drop.thresh) {
                 store4((T*)drop.dres + idx, o);      // residual gradient: unmasked
                 apply4(drop, kb[k], o);              // x gradient: through the dropout mask
+            }
+            if constexpr (ADD) {
+                float a[4];
+                cvt_raw4(ra[k], a);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] += a[j];
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) ds[k][j] += to_f(from_f<T>(o[j]));   // sum of the stored (rounded) dx
@@ -589,12 +629,12 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
         {
             float xv[VPL][4], d[VPL][4];
             prep_row(ra, xv, d);
-            finish_row(row, xv, d, ra.kb);
+            finish_row(row, xv, d, ra);
         }
         if (two) {
             float xv[VPL][4], d[VPL][4];
             prep_row(rb, xv, d);
-            finish_row(row + 4, xv, d, rb.kb);
+            finish_row(row + 4, xv, d, rb);
         }
         if constexpr (PIPE) {
             ra = rc;
@@ -811,6 +851,15 @@ DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float*
     DDL_RETURN_LAUNCH();
 }
 
+// backward coefficients (+ dgamma / dbeta) from nblk partial rows: collapse (if many) + finalize
+template <typename T>
+static void bwd_finalize(const float* part, int nblk, float* ws, int C, long M, const T* gamma, const float* invstd,
+                         T* dgamma, T* dbeta, float* coef, int acc, hipStream_t st) {
+    int nrows = nblk;
+    const float* fin = collapse_partials(part, nrows, 2 * C, st, ws);
+    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(fin, nrows, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
+}
+
 template <typename T>
 static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const float* mean, const float* invstd,
                             const T* gamma, long M, int C, int relu, float* part, T* dgamma, T* dbeta, float* coef,
@@ -821,9 +870,7 @@ static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const 
     rpb = (rpb + rpi - 1) / rpi * rpi;
     if (relu) bn_bwd_partial_k<T, true><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
-    int nrows = nblk;
-    const float* fin = collapse_partials(part, nrows, 2 * C, st);
-    bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(fin, nrows, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
+    bwd_finalize<T>(part, nblk, nullptr, C, M, gamma, invstd, dgamma, dbeta, coef, acc, st);
     if (rows_ok(C)) {
         const int gr = rows_grid(M, C);
         if (relu) {
@@ -996,9 +1043,8 @@ DDL_API int ddl_bn_bwd_pool(int dtype, const void* dy, const uint8_t* idx, const
 #define BBP(T) do {                                                                                                     \
         bn_bwd_pool_partial_k<T><<<nblk, 256, 0, st>>>((const T*)dy, idx, mask, (const T*)x, mean, invstd, N, H, W, C,  \
                                                        P, Q, part);                                                     \
-        const float* fin = collapse_partials(part, nrows, 2 * C, st);                                                   \
-        bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(fin, nrows, C, M, (const T*)gamma, invstd, (T*)dgamma,    \
-                                                             (T*)dbeta, coef, acc_params);                              \
+        bwd_finalize<T>(part, nrows, nullptr, C, M, (const T*)gamma, invstd, (T*)dgamma, (T*)dbeta, coef, acc_params,   \
+                        st);                                                                                            \
         bn_bwd_pool_apply_k<T><<<grid_for(M * (C / 8), 256, 8192), 256, 0, st>>>((const T*)dy, idx, mask, (const T*)x,   \
                                                                                 mean, invstd, coef, (T*)dx, N, H, W, C, \
                                                                                 P, Q);                                   \
@@ -1071,10 +1117,19 @@ DDL_API int ddl_ln_bwd_nblk(long rows) {
 template <typename T>
 static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows, const T* g, const float* mean,
                            const float* rstd, T* dx, float* part, T* dg, T* db, long rows, int H, int acc,
-                           float* dxsum, T* dxsink, Drop drop, hipStream_t st) {
+                           float* dxsum, T* dxsink, Drop drop, const T* dadd, hipStream_t st) {
     const int nblk = ddl_ln_bwd_nblk(rows);
     const int rpb = (int)((rows + nblk - 1) / nblk);
-    switch (H / 256) {
+#define LNB_ADD(V) ln_bwd_k<T, V, true><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop, dadd)
+    if (dadd) {
+        switch (H / 256) {
+            case 1: LNB_ADD(1); break;
+            case 2: LNB_ADD(2); break;
+            case 3: LNB_ADD(3); break;
+            case 4: LNB_ADD(4); break;
+            default: return -4;
+        }
+    } else switch (H / 256) {
         case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
@@ -1084,6 +1139,7 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
         case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         default: return -1;
     }
+#undef LNB_ADD
     int nrows = nblk;
     const float* fin = collapse_partials(part, nrows, (dxsum ? 3 : 2) * H, st);
     colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(fin, nrows, H, dg, db, acc, dxsum, dxsink);
@@ -1100,7 +1156,7 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
 DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res, long res_rows, const void* g,
                        const float* mean, const float* rstd, void* dx, float* part, void* dg, void* db, long rows, int H,
                        int acc_params, float* dxsum, unsigned long long drop_seed, float drop_p, void* dres,
-                       void* dxsink, hipStream_t st) {
+                       void* dxsink, const void* dadd, hipStream_t st) {
     if (!ddl_ln_supported(H)) return -1;
     if (res_rows <= 0) res_rows = rows;
     if (drop_p > 0.f && (!dres || res_rows != rows)) return -2;
@@ -1109,10 +1165,10 @@ DDL_API int ddl_ln_bwd(int dtype, const void* dy, const void* x, const void* res
     int rc = dtype == 1
                  ? ln_bwd_dispatch((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)res, res_rows, (const bf16_t*)g,
                                    mean, rstd, (bf16_t*)dx, part, (bf16_t*)dg, (bf16_t*)db, rows, H, acc_params, dxsum,
-                                   (bf16_t*)dxsink, drop, st)
+                                   (bf16_t*)dxsink, drop, (const bf16_t*)dadd, st)
                  : ln_bwd_dispatch((const float*)dy, (const float*)x, (const float*)res, res_rows, (const float*)g, mean,
                                    rstd, (float*)dx, part, (float*)dg, (float*)db, rows, H, acc_params, dxsum,
-                                   (float*)dxsink, drop, st);
+                                   (float*)dxsink, drop, (const float*)dadd, st);
     if (rc) return rc;
     DDL_RETURN_LAUNCH();
 }
@@ -1193,22 +1249,27 @@ DDL_API int ddl_bn_bwd_partials(int dtype, const void* dy, const void* mask, con
 // and the global row count M_total, the apply walks the local M rows; dgamma / dbeta come from
 // local_row (this rank's own [sum dz | sum dz*xhat], taken before the all-reduce) when given
 template <typename T>
+static void bn_bwd_apply_only(const T* dy, const uint8_t* mk, const T* x, const float* mean, const float* invstd,
+                              long M, int C, int relu, const float* coef, T* dx, T* dres, hipStream_t st) {
+    if (!rows_ok(C)) return;
+    const int gr = rows_grid(M, C);
+    if (relu) {
+        if (dres) bn_bwd_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+        else bn_bwd_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+    } else {
+        if (dres) bn_bwd_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+        else bn_bwd_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
+    }
+}
+
+template <typename T>
 static void bn_bwd_finish_t(const T* dy, const uint8_t* mk, const T* x, const float* mean, const float* invstd,
                             const T* gamma, long M, long M_total, int C, int relu, const float* row, int nrows,
                             T* dgamma, T* dbeta, float* coef, T* dx, T* dres, int acc, hipStream_t st,
                             const float* prow = nullptr) {
     bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(row, nrows, C, M_total, gamma, invstd, dgamma, dbeta, coef,
                                                          acc, prow);
-    if (rows_ok(C)) {
-        const int gr = rows_grid(M, C);
-        if (relu) {
-            if (dres) bn_bwd_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-            else bn_bwd_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-        } else {
-            if (dres) bn_bwd_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-            else bn_bwd_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-        }
-    }
+    bn_bwd_apply_only(dy, mk, x, mean, invstd, M, C, relu, coef, dx, dres, st);
 }
 
 DDL_API int ddl_bn_bwd_finish(int dtype, const void* dy, const void* mask, const void* x, const float* mean,
@@ -1238,8 +1299,14 @@ DDL_API int ddl_bn_bwd_from_partials(int dtype, const float* part, int nrows, fl
     if (!rows_ok(C) || dtype != 1) return -1;
     const long need = ddl_bn_partials_ws(nrows, C);
     if (need > 0 && (!ws || ws_elems < need)) return -2;
-    const float* fin = need > 0 ? collapse_partials(part, nrows, 2 * C, st, ws) : part;
-    bn_bwd_finish_t((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M, M, C, 0, fin,
+    if (need > 0) {
+        bwd_finalize<bf16_t>(part, nrows, ws, C, M, (const bf16_t*)gamma, invstd, (bf16_t*)dgamma, (bf16_t*)dbeta, coef,
+                             acc_params, st);
+        bn_bwd_apply_only((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, M, C, 0, coef, (bf16_t*)dx,
+                          (bf16_t*)dres, st);
+        DDL_RETURN_LAUNCH();
+    }
+    bn_bwd_finish_t((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, (const bf16_t*)gamma, M, M, C, 0, part,
                     nrows, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, (bf16_t*)dx, (bf16_t*)dres, acc_params, st);
     DDL_RETURN_LAUNCH();
 }

@@ -135,7 +135,7 @@ class StockBert(nn.Module):
 
 # ---------------------------------------------------------------- runner
 def run_stock(model: str, batch: int, steps: int, warmup: int, seq_len: int = 128, dropout: float = 0.1,
-              seed: int = 1234, bucket_mb: float = 25.0) -> Dict[str, Any]:
+              seed: int = 1234, bucket_mb: float = 25.0, pad_fraction: float = 0.0) -> Dict[str, Any]:
     """Train ``model`` ("resnet50" | "bert_base") with stock PyTorch + torch DDP on this
     rank's device; returns the same summary fields as ``training.loop.Trainer.run``."""
     from ..parallel import dist as ddist
@@ -157,13 +157,19 @@ def run_stock(model: str, batch: int, steps: int, warmup: int, seq_len: int = 12
         optimizer = "sgd"
     elif model == "bert_base":
         net = StockBert(p=dropout).to(dev)
+
+        def mask():
+            if pad_fraction <= 0:
+                return None
+            lens = torch.randint(int(seq_len * (1 - pad_fraction)), seq_len + 1, (batch,), generator=g, device=dev)
+            return (torch.arange(seq_len, device=dev)[None, :] < lens[:, None]).to(torch.int64)
         data = [(torch.randint(0, 30522, (batch, seq_len), generator=g, device=dev),
-                 torch.randint(0, 2, (batch,), generator=g, device=dev)) for _ in range(4)]
+                 torch.randint(0, 2, (batch,), generator=g, device=dev), mask()) for _ in range(4)]
         opt = torch.optim.AdamW(net.parameters(), lr=2e-5, weight_decay=0.01, eps=1e-6,
                                 **({"fused": True} if cuda else {}))
 
         def loss_fn(m, b):
-            return F.cross_entropy(m(b[0]), b[1])
+            return F.cross_entropy(m(b[0], b[2]), b[1])
         optimizer = "adamw"
     else:
         raise KeyError(model)

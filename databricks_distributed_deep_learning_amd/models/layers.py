@@ -103,9 +103,9 @@ class Linear(nn.Module):
                 bound = 1.0 / math.sqrt(fin)
                 nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x, grad_residual=None, fuse_dgelu: bool = False, residual=None):
+    def forward(self, x, grad_residual=None, fuse_dgelu: bool = False, residual=None, residual_grad_to=None):
         return ops.linear(x, self.weight, self.bias, self.act, grad_residual=grad_residual, fuse_dgelu=fuse_dgelu,
-                          residual=residual)
+                          residual=residual, residual_grad_to=residual_grad_to)
 
     def extra_repr(self):
         return f"{self.fin}, {self.fout}, bias={self.bias is not None}, act={self.act}"
@@ -166,10 +166,11 @@ class LayerNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(d))
         self.bias = nn.Parameter(torch.zeros(d))
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None, dropout: float = 0.0, residual_grad_to=None):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, dropout: float = 0.0, residual_grad_to=None,
+                grad_from=None):
         """``LayerNorm(dropout(x) + residual)``; ``dropout`` only applies in training."""
         return ops.layer_norm(x, self.weight, self.bias, self.eps, residual, dropout if self.training else 0.0,
-                              residual_grad_to=residual_grad_to)
+                              residual_grad_to=residual_grad_to, grad_from=grad_from)
 
 
 class Embedding(nn.Module):

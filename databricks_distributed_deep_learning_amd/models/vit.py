@@ -12,7 +12,11 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops.bridge import GradBridge
 from .layers import Dropout, LayerNorm, Linear
+
+# residual-stream gradient handed to the LayerNorm backwards (False: autograd sums it; tests)
+_LN_BRIDGE = True
 
 
 @dataclass
@@ -48,17 +52,22 @@ class ViTLayer(nn.Module):
             nn.init.zeros_(lin.bias)
 
     def forward(self, h):
-        y = self.layernorm_before(h)
+        b1 = GradBridge() if _LN_BRIDGE else None
+        y = self.layernorm_before(h, grad_from=b1)
         ctx = ops.attention(self.qkv(y), self.num_heads, None, self.attn_dropout, self.training)
         if self.dropout.p > 0.0 and self.training:
             h = h + self.dropout(self.attn_out(ctx))
             y = self.layernorm_after(h)
             return h + self.dropout(self.fc2(self.fc1(y), fuse_dgelu=True))
         # no hidden dropout (the ViT-B/16 recipe): both residual-stream adds ride the output
-        # GEMMs' epilogues; fc2's dgrad epilogue applies fc1's GELU backward
-        h = self.attn_out(ctx, residual=h)
-        y = self.layernorm_after(h)
-        return self.fc2(self.fc1(y), fuse_dgelu=True, residual=h)
+        # GEMMs' epilogues; fc2's dgrad epilogue applies fc1's GELU backward.  The residual
+        # stream's gradient reaches each LayerNorm backward through a bridge, which adds it
+        # to the LN input gradient in the same pass (no autograd add, and the column sums --
+        # the producing Linear's bias gradient -- come out of that pass too)
+        h = self.attn_out(ctx, residual=h, residual_grad_to=b1)
+        b2 = GradBridge() if _LN_BRIDGE else None
+        y = self.layernorm_after(h, grad_from=b2)
+        return self.fc2(self.fc1(y), fuse_dgelu=True, residual=h, residual_grad_to=b2)
 
 
 class ViTForImageClassification(nn.Module):

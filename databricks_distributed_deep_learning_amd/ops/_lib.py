@@ -137,7 +137,7 @@ _SIGS = {
     "ddl_ln_supported": [I],
     "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, U64, F, P],
     "ddl_ln_bwd_nblk": [L],
-    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P, U64, F, P, P, P],
+    "ddl_ln_bwd": [I, P, P, P, L, P, P, P, P, P, P, P, L, I, I, P, U64, F, P, P, P, P],
     # elementwise.hip
     "ddl_gelu_fwd": [I, P, P, L, P],
     "ddl_gelu_bwd": [I, P, P, P, L, P],

@@ -16,13 +16,17 @@ from ._lib import F as CF, I, L, P, U64
 from ._native_elementwise import new_seed
 
 _lib.register({
-    "ddl_attn_fwd": [P, P, P, P, I, I, I, CF, CF, U64, P],
-    "ddl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, CF, CF, U64, P, P],
+    "ddl_attn_fwd": [P, P, P, P, I, I, I, CF, CF, U64, P, P],
+    "ddl_attn_bwd": [P, P, P, P, P, P, P, I, I, I, CF, CF, P, P, P],
+    "ddl_attn_dmask_words": [I, I, I],
 })
 
 # the fused backward (S <= 128) also writes per-batch column sums of dQKV, from which the QKV
 # Linear takes its bias gradient instead of another pass over dQKV (DDL_ATTN_COLSUM=0: off)
 _COLSUM = os.environ.get("DDL_ATTN_COLSUM", "1") != "0"
+# measurement only (never a training setting): DDL_ATTN_NODROP_DEBUG=1 drops the attention-
+# probability dropout, to price its in-kernel mask generation in an A/B run
+_NODROP_DEBUG = os.environ.get("DDL_ATTN_NODROP_DEBUG", "0") == "1"
 
 
 class _Attention(torch.autograd.Function):
@@ -37,23 +41,30 @@ class _Attention(torch.autograd.Function):
         lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
         m = None if mask is None else mask.to(torch.float32).reshape(B, S).contiguous()
         seed = new_seed() if p_drop > 0 else 0
+        # dropout: the forward draws the keep decisions and stores them as bits (1 per score);
+        # the backward reads them instead of regenerating them
+        dmask = None
+        if p_drop > 0:
+            fn = _lib.fn("ddl_attn_dmask_words")
+            fn.restype = L
+            dmask = torch.empty(fn(B, S, H), dtype=torch.int32, device=qkv.device)
         _lib.call("ddl_attn_fwd", qkv.data_ptr(), _lib.p(m), out.data_ptr(), lse.data_ptr(), B, S, H, scale,
-                  float(p_drop), seed)
+                  float(p_drop), seed, _lib.p(dmask))
         ctx.meta = (B, S, H, scale, float(p_drop), seed)
-        ctx.save_for_backward(qkv, out, lse, m)
+        ctx.save_for_backward(qkv, out, lse, m, dmask)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, out, lse, m = ctx.saved_tensors
+        qkv, out, lse, m, dmask = ctx.saved_tensors
         B, S, H, scale, p_drop, seed = ctx.meta
         dout = dout.contiguous()
         delta = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
         dqkv = torch.empty_like(qkv)
         cs = torch.empty(B, 3 * H * 64, dtype=torch.float32, device=qkv.device) if _COLSUM and S <= 128 else None
         rc = _lib.fn("ddl_attn_bwd")(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _lib.p(m),
-                                     delta.data_ptr(), dqkv.data_ptr(), B, S, H, scale, p_drop, seed, _lib.p(cs),
-                                     _lib.stream())
+                                     delta.data_ptr(), dqkv.data_ptr(), B, S, H, scale, p_drop, _lib.p(dmask),
+                                     _lib.p(cs), _lib.stream())
         if rc not in (0, 1):
             raise RuntimeError(f"native kernel ddl_attn_bwd failed with HIP error {rc}")
         if cs is not None and rc == 0:
@@ -68,4 +79,4 @@ def attention(qkv, num_heads, mask, dropout_p):
     if qkv.dtype != torch.bfloat16 or three_hd != 3 * 64 * num_heads:
         from .attention import attention_reference
         return attention_reference(qkv, num_heads, mask, dropout_p, dropout_p > 0)
-    return _Attention.apply(qkv, num_heads, mask, float(dropout_p))
+    return _Attention.apply(qkv, num_heads, mask, 0.0 if _NODROP_DEBUG else float(dropout_p))

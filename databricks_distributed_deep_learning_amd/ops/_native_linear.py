@@ -54,9 +54,10 @@ def _transposed(param, w: torch.Tensor) -> torch.Tensor:
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, bridge=None, fuse_dgelu=False, residual=None):
+    def forward(ctx, x, w, b, act, bridge=None, fuse_dgelu=False, residual=None, res_bridge=None):
         ctx.w_param, ctx.b_param = w, b
         ctx.bridge = bridge
+        ctx.res_bridge = res_bridge if residual is not None else None
         # GELU chain (FFN): this layer's input is the output of a GELU Linear whose only
         # consumer is this layer -> the dgrad epilogue applies that layer's dGELU and
         # column-sums the result (its bias gradient); see ``_DgeluHandoff``
@@ -88,9 +89,11 @@ class _Linear(torch.autograd.Function):
         if z is not None:
             ctx.gelu_token = object()
             out._ddl_gelu_pre = (z, ctx.gelu_token)
-        elif b is not None and act is None and residual is None:
+        elif b is not None and act is None:
             # a LayerNorm consuming ``out`` may add the column sums of its input gradient
-            # (this bias's gradient) straight into the bias's arena slot
+            # (this bias's gradient) straight into the bias's arena slot (with a residual too:
+            # the residual does not change the bias gradient; if autograd sums another branch
+            # into ``out``'s gradient, the backward below corrects the sunk share)
             out._ddl_bias_param = b
         return out
 
@@ -99,8 +102,13 @@ class _Linear(torch.autograd.Function):
         x2, w, saved = ctx.saved_tensors
         M, K = x2.shape
         N = w.shape[0]
-        # the residual's gradient is dy itself (identity add in the epilogue)
+        # the residual's gradient is dy itself (identity add in the epilogue); handed to the
+        # LayerNorm that also consumes the residual when a bridge joins them
         dres = dy if ctx.has_res else None
+        if dres is not None and ctx.res_bridge is not None:
+            ctx.res_bridge.put(dres)
+            dres = None
+        ctx.res_bridge = None
         dy2 = dy.reshape(M, N)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
@@ -227,7 +235,7 @@ class _Linear(torch.autograd.Function):
             else:
                 db = torch.empty(N, dtype=w.dtype, device=w.device)
                 E.colsum(dz, db)
-        return dx, dw, db, None, None, None, dres
+        return dx, dw, db, None, None, None, dres, None
 
 
 def _colsum_rows(dy, act, N):
@@ -270,11 +278,12 @@ class _DgeluHandoff:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str],
-           bridge=None, fuse_dgelu: bool = False, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+           bridge=None, fuse_dgelu: bool = False, residual: Optional[torch.Tensor] = None,
+           residual_grad_to=None) -> torch.Tensor:
     if not _ok(x, w) or (b is not None and b.dtype != w.dtype) or \
             (residual is not None and residual.shape[-1] != w.shape[0]):
         from .bridge import join
         from .linear import linear_reference
         y = linear_reference(join(x, bridge), w, b, act)
         return y if residual is None else y + residual
-    return _Linear.apply(x, w, b, act, bridge, fuse_dgelu, residual)
+    return _Linear.apply(x, w, b, act, bridge, fuse_dgelu, residual, residual_grad_to)

@@ -360,9 +360,10 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum, e
 
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual, drop_p, bridge=None):
+    def forward(ctx, x, weight, bias, eps, residual, drop_p, bridge=None, grad_from=None):
         # the bias of the Linear that produced x
         ctx.bias_param = getattr(x, "_ddl_bias_param", None) if _LN_BIAS_SINK else None
+        ctx.grad_from = grad_from
         x = x.contiguous()
         H = x.shape[-1]
         rows = x.numel() // H
@@ -401,15 +402,35 @@ class _LayerNorm(torch.autograd.Function):
         if bsink is not None and (bsink.numel() != H or bsink.dtype != dg.dtype
                                   or getattr(ctx.bias_param, "_ddl_sunk", None) is not None):
             bsink = None
+        # x's gradient from its other consumer (a pre-LN residual branch, handed over by that
+        # Linear's backward): added in the same pass, so dx and its column sums are complete
+        add = ctx.grad_from.take() if ctx.grad_from is not None else None
+        ctx.grad_from = None
+        if add is not None:
+            add = add.reshape(x.shape)
+            if not add.is_contiguous() or add.dtype != x.dtype:
+                add = add.contiguous().to(x.dtype)
+            if H // 256 > 4:                 # no fused variant: sum afterwards (sinks off)
+                bsink, late = None, add
+                add = None
+            else:
+                late = None
+        else:
+            late = None
         call("ddl_ln_bwd", dcode(x), p(dy), p(x), p(res), ctx.res_rows, p(weight), p(stats[0]), p(stats[1]), p(dx),
-             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum), ctx.seed, ctx.drop_p, p(dres_buf), p(bsink))
+             p(part), p(dg), p(db), rows, H, int(direct), p(dxsum), ctx.seed, ctx.drop_p, p(dres_buf), p(bsink),
+             p(add))
+        if late is not None:
+            dx.add_(late)
+            dxsum = None
         if bsink is not None:
             ctx.bias_param._ddl_sunk = dxsum     # the Linear's backward only marks it ready
         ctx.bias_param = None
         # the column sums of dx ride along on the gradient tensor: the Linear whose output
         # fed this LayerNorm takes them as its bias gradient instead of re-reading dx
         # (the version guards against autograd accumulating another gradient into dx in place)
-        dx._ddl_colsum = (dxsum, dx._version)
+        if dxsum is not None:
+            dx._ddl_colsum = (dxsum, dx._version)
         if direct:
             grad_ready(ctx.params[0])
             grad_ready(ctx.params[1])
@@ -424,11 +445,11 @@ class _LayerNorm(torch.autograd.Function):
                     dres = None
             else:
                 dres = g.view(-1, ctx.res_rows, H).float().sum(0).to(dx.dtype).view(ctx.res_shape)
-        return dx, dg, db, None, dres, None, None
+        return dx, dg, db, None, dres, None, None, None
 
 
 def layer_norm(x, weight, bias, eps, residual: Optional[torch.Tensor] = None, dropout: float = 0.0,
-               residual_grad_to=None):
+               residual_grad_to=None, grad_from=None):
     from .norm import layer_norm_reference
     H = x.shape[-1]
     ok = bool(_lib.fn("ddl_ln_supported")(H)) and x.dtype in (torch.bfloat16, torch.float32)
@@ -445,7 +466,8 @@ def layer_norm(x, weight, bias, eps, residual: Optional[torch.Tensor] = None, dr
         if dropout > 0.0:
             from .activation import dropout as _dropout
             x = _dropout(x, dropout, True)
-        return layer_norm_reference(x, weight, bias, eps, residual)
+        from .bridge import join
+        return layer_norm_reference(join(x, grad_from), weight, bias, eps, residual)
     if weight.dtype != x.dtype:
         weight, bias = weight.to(x.dtype), bias.to(x.dtype)
-    return _LayerNorm.apply(x, weight, bias, eps, residual, float(dropout), residual_grad_to)
+    return _LayerNorm.apply(x, weight, bias, eps, residual, float(dropout), residual_grad_to, grad_from)

@@ -40,7 +40,7 @@ def linear_reference(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
            act: Optional[str] = None, grad_residual=None, fuse_dgelu: bool = False,
-           residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+           residual: Optional[torch.Tensor] = None, residual_grad_to=None) -> torch.Tensor:
     """``grad_residual``: a :class:`ops.bridge.GradBridge` whose pending gradient (a
     post-LN residual branch's) is added to this layer's input gradient inside the
     dgrad GEMM epilogue instead of by an autograd add kernel.
@@ -48,14 +48,17 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
     only consumer (an FFN) -- this layer's dgrad epilogue then applies that layer's
     dGELU and sums its bias gradient, so the GELU backward pass disappears.
     ``residual``: ``x W^T + b + residual`` (no activation) -- the pre-LN residual stream
-    add done in the GEMM epilogue instead of a separate elementwise pass."""
+    add done in the GEMM epilogue instead of a separate elementwise pass.
+    ``residual_grad_to``: a GradBridge that receives the residual's gradient (this
+    output's gradient) for the LayerNorm that also consumes ``residual``
+    (``layer_norm(grad_from=...)``), instead of autograd summing the two."""
     if act not in ACTS:
         raise ValueError(f"act must be one of {ACTS}")
     if residual is not None and act is not None:
         raise ValueError("linear(residual=...) is the identity-activation epilogue add")
     if _lib.use_native(x):
         from . import _native_linear
-        return _native_linear.linear(x, w, b, act, grad_residual, fuse_dgelu, residual)
+        return _native_linear.linear(x, w, b, act, grad_residual, fuse_dgelu, residual, residual_grad_to)
     from .bridge import join
     y = linear_reference(join(x, grad_residual), w, b, act)
     return y if residual is None else y + residual

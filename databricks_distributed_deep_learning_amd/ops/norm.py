@@ -93,7 +93,7 @@ def layer_norm_reference(x, weight, bias, eps: float = 1e-12, residual: Optional
 
 
 def layer_norm(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Tensor] = None,
-               dropout: float = 0.0, residual_grad_to=None):
+               dropout: float = 0.0, residual_grad_to=None, grad_from=None):
     """``LayerNorm(dropout(x) + residual)`` over the last axis; fp32 statistics.
 
     ``dropout`` (training-time probability on ``x``; post-LN transformers apply it to
@@ -101,13 +101,17 @@ def layer_norm(x, weight, bias, eps: float = 1e-12, residual: Optional[torch.Ten
     the HIP path: the mask is a counter hash regenerated in the backward, which also
     emits the masked gradient's column sums for the producing Linear's bias.
     ``residual_grad_to``: a :class:`ops.bridge.GradBridge` that receives the residual's
-    gradient (for the Linear that also consumes ``residual``) instead of autograd."""
+    gradient (for the Linear that also consumes ``residual``) instead of autograd.
+    ``grad_from``: a GradBridge holding the gradient of ``x`` from its other consumer (a
+    pre-LN block's residual branch, ``linear(residual=x, residual_grad_to=...)``); the
+    backward adds it to this LayerNorm's input gradient in the same pass."""
     if _lib.use_native(x):
         from . import _native_norm
-        return _native_norm.layer_norm(x, weight, bias, eps, residual, dropout, residual_grad_to)
+        return _native_norm.layer_norm(x, weight, bias, eps, residual, dropout, residual_grad_to, grad_from)
     if dropout > 0.0:
         x = F.dropout(x, dropout, True)
-    return layer_norm_reference(x, weight, bias, eps, residual)
+    from .bridge import join
+    return layer_norm_reference(join(x, grad_from), weight, bias, eps, residual)
 
 
 def batch_norm_add_bn(x, weight, bias, running_mean, running_var, momentum, eps, x2, weight2, bias2,

@@ -1,6 +1,6 @@
 """Per-GEMM device time of one training step, grouped by call signature (GPU diagnostics).
 
-    python scripts/debug/gemm_trace.py [resnet50|bert_base] [--batch N]
+    python scripts/debug/gemm_trace.py [resnet50|bert_base|vit_b16|bert_large] [--batch N]
 
 Runs warm-up steps (GEMM tuning), then one traced step with HIP events around every
 native GEMM launch, and prints the signatures sorted by time: which convolution /
@@ -26,9 +26,15 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
-    preset = "resnet50_ddp" if a.model.startswith("resnet") else "bert_base_ddp"
-    cfg = get_preset(preset, batch_size=a.batch or (256 if preset.startswith("resnet") else 128))
-    cfg = cfg.replace(model=a.model, steps=1, warmup_steps=2, log_every=0)
+    if a.model == "vit_b16":
+        cfg = get_preset("vit_b16", **({"batch_size": a.batch} if a.batch else {}))
+    elif a.model == "bert_large":
+        cfg = get_preset("bert_large_lamb", batch_size=a.batch or 32, grad_accum=1)
+    else:
+        preset = "resnet50_ddp" if a.model.startswith("resnet") else "bert_base_ddp"
+        cfg = get_preset(preset, batch_size=a.batch or (256 if preset.startswith("resnet") else 128))
+        cfg = cfg.replace(model=a.model)
+    cfg = cfg.replace(steps=1, warmup_steps=2, log_every=0)
     tr = Trainer(cfg)
     tr.run()                       # warm-up + tuning
     torch.cuda.synchronize()

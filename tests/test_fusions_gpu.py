@@ -189,3 +189,64 @@ def test_stem_bn_relu_maxpool(shape, fused_bwd, monkeypatch):
         assert ((u - v).norm() / v.norm().clamp_min(1e-12)).item() < 1e-2, n
     torch.testing.assert_close(res[0][4], res[1][4])
     torch.testing.assert_close(res[0][5], res[1][5])
+
+
+@pytest.mark.parametrize("nblk,C", [(300, 64), (3000, 512), (1057, 2048)])
+def test_bn_finalize_from_many_partial_rows(nblk, C):
+    """Many GEMM-epilogue partial rows (collapsed 32:1, then finalized) -> BatchNorm
+    forward statistics and backward coefficients, against fp64 sums of the same rows."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops._lib import call, p
+    torch.manual_seed(5)
+    M = nblk * 128
+    part = torch.rand(nblk, 2 * C, device=dev) * 4.0
+    part[:, C:] += part[:, :C] ** 2 / 16        # second moments >= mean^2 on average
+    ws = torch.empty(-(-nblk // 32) * 2 * C, device=dev)
+    gamma = (torch.rand(C, device=dev) + 0.5).bfloat16()
+    beta = torch.randn(C, device=dev).bfloat16()
+    s, q = part.double().sum(0)[:C], part.double().sum(0)[C:]
+    for rep in range(3):
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        st = torch.empty(4, C, device=dev)
+        call("ddl_bn_fwd_from_partials", 1, p(part), nblk, M, C, p(gamma), p(beta), p(rm), p(rv), 0.1, 1e-5,
+             p(st[0]), p(st[1]), p(st[2]), p(st[3]), p(ws), ws.numel())
+        mean = s / M
+        var = (q / M - mean * mean).clamp_min(0)
+        torch.testing.assert_close(st[0].double(), mean, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(st[1].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(rm.double(), 0.1 * mean, rtol=1e-5, atol=1e-6)
+    # backward: coefficients (k1, mean dz, mean dz*xhat) and dgamma / dbeta from the same rows
+    x = torch.randn(M, C, device=dev).bfloat16()
+    dz = torch.randn(M, C, device=dev).bfloat16()
+    istd = torch.rand(C, device=dev) + 0.5
+    mu = torch.randn(C, device=dev) * 0.1
+    coef = torch.empty(3 * C, device=dev)
+    dg, db = torch.empty(C, device=dev).bfloat16(), torch.empty(C, device=dev).bfloat16()
+    dx = torch.empty_like(x)
+    call("ddl_bn_bwd_from_partials", 1, p(part), nblk, p(ws), ws.numel(), p(dz), p(x), p(mu), p(istd), p(gamma), M, C,
+         p(dg), p(db), p(coef), p(dx), None, 0)
+    torch.testing.assert_close(coef[C:2 * C].double(), s / M, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(coef[2 * C:].double(), q / M, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(db.double(), s.to(torch.bfloat16).double(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dg.double(), q.to(torch.bfloat16).double(), rtol=1e-2, atol=1e-2)
+    k1 = gamma.float() * istd
+    ref = k1 * (dz.float() - coef[C:2 * C] - (x.float() - mu) * istd * coef[2 * C:])
+    assert ((dx.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
+@pytest.mark.parametrize("nrows,width,n,acc", [(100, 1536, 768, 1), (777, 64, 64, 0), (2000, 6144, 3072, 1)])
+def test_rows_sum_sink_many_rows(nrows, width, n, acc):
+    """Column sums of many partial rows straight into a bf16 gradient slot (a Linear's bias),
+    against fp64."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops._lib import call, p
+    torch.manual_seed(2)
+    part = torch.randn(nrows, width, device=dev)
+    ws = torch.empty(-(-nrows // 32) * width, device=dev)
+    sink = torch.randn(n, device=dev).bfloat16()
+    before = sink.double().clone()
+    for _ in range(2):
+        out = sink.clone()
+        call("ddl_rows_sum_sink", 1, p(part), nrows, width, n, p(out), acc, p(ws))
+        ref = part.double().sum(0)[:n] + (before if acc else 0)
+        torch.testing.assert_close(out.double(), ref.to(torch.bfloat16).double(), rtol=2e-2, atol=2e-2)

@@ -133,12 +133,12 @@ def test_layernorm_fused_dropout(dtype, H):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H", [768, 1024])
 @pytest.mark.parametrize("res", [None, "full", "bcast"])
-def test_layernorm(dtype, H, res):
+@pytest.mark.parametrize("B,S", [(3, 37), (64, 197)])   # 64 x 197 rows: > 64 partial rows (merged finish)
+def test_layernorm(dtype, H, res, B, S):
     dev = gpu_device()
     _native_lib_loaded()
     from databricks_distributed_deep_learning_amd.ops import norm
     torch.manual_seed(1)
-    B, S = 3, 37
     x = torch.randn(B, S, H, device=dev).to(dtype)
     g = (torch.rand(H, device=dev) + 0.5).to(dtype)
     b = (torch.randn(H, device=dev) * 0.1).to(dtype)

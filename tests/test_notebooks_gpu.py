@@ -21,6 +21,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_resnet_notebook_gpu_branch():
     gpu_device()
     env = dict(os.environ, DDL_NOTEBOOK_SMOKE="gpu", PYTHONPATH=ROOT)
+    # a fresh notebook process: no rendezvous variables left over from this pytest process
+    for k in ("MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "notebooks/cv/resnet_distributed_training.py")],
                        env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
