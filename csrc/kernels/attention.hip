@@ -361,7 +361,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
                                                       int S, int H, float scale, float p_drop,
-                                                      const uint32_t* __restrict__ dmask) {
+                                                      const uint32_t* __restrict__ dmask,
+                                                      float* __restrict__ colsum) {
     // Q, dO tiles as row images (S, dP fragments) and transposed-read images (dK, dV fragments):
     // the tr reads on a row image were 23 % bank-conflicted
     __shared__ __attribute__((aligned(16))) char smem[4 * TQ * ROWB];
@@ -478,6 +479,26 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
             }
         }
     }
+    if (colsum) {
+        // the QKV bias gradient's share of this wave's 16 keys: column sums of their dK, dV
+        // rows, row (b * tiles + tile) * 4 + wave of colsum [B * tiles * 4][3 H D] (keys past S
+        // contribute zero).  Per wave, no barrier: a workgroup-wide reduction held every wave
+        // until the slowest finished (+10 us per launch at ViT's 6144 workgroups)
+        float* crow = colsum + (((long)b * gridDim.x + blockIdx.x) * 4 + w) * rs + h * D + 4 * g;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            float sk[4], sv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                sk[r] = row16_sum(kok ? dk[db][r] * scale : 0.f);     // over the DPP row = 16 keys
+                sv[r] = row16_sum(kok ? dv[db][r] : 0.f);
+            }
+            if ((lane & 15) == 0) {
+                *reinterpret_cast<float4*>(crow + H * D + 16 * db) = make_float4(sk[0], sk[1], sk[2], sk[3]);
+                *reinterpret_cast<float4*>(crow + 2 * H * D + 16 * db) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+            }
+        }
+    }
     if (!kok) return;
     bf16_t* dkr = dqkv + ((long)b * S + myk) * rs + H * D + h * D;
     bf16_t* dvr = dkr + H * D;
@@ -496,7 +517,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
                                                      const float* __restrict__ lse, const float* __restrict__ delta,
                                                      const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
                                                      int S, int H, float scale, float p_drop,
-                                                     const uint32_t* __restrict__ dmask) {
+                                                     const uint32_t* __restrict__ dmask,
+                                                     float* __restrict__ colsum) {
     __shared__ __attribute__((aligned(16))) char smem[3 * TK * ROWB];   // K, V tiles + K as a tr-read image
     __shared__ __attribute__((aligned(16))) float s_mk[TK];            // the tile's additive key mask (log2)
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -603,6 +625,19 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
 #pragma unroll
             for (int db = 0; db < 4; ++db)
                 dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sKt, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
+        }
+    }
+    if (colsum) {
+        // column sums of this wave's 16 dQ rows (the same colsum row as the dKV kernel's wave
+        // over these positions' keys)
+        float* crow = colsum + (((long)b * gridDim.x + blockIdx.x) * 4 + w) * rs + h * D + 4 * g;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            float sq[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sq[r] = row16_sum(qok ? dq[db][r] * scale : 0.f);
+            if ((lane & 15) == 0)
+                *reinterpret_cast<float4*>(crow + 16 * db) = make_float4(sq[0], sq[1], sq[2], sq[3]);
         }
     }
     if (!qok) return;
@@ -1069,8 +1104,9 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
 }
 
 // dqkv [B, S, 3*H*64] bf16 (fully written); delta scratch [B, H, S] fp32
-// colsum (nullable, [B][3 H 64] fp32): per-batch column sums of dqkv (the QKV bias gradient is their
-// column sum) -- single-workgroup path only (S <= 128): returns 1 when it was NOT written
+// colsum (nullable, [B * 4 ceil(S / 64)][3 H 64] fp32): column sums of dqkv per batch (single-
+// workgroup path: rows 0..B-1, returns 0) or per batch and 16-row group (tiled path: every row,
+// returns 2) -- the QKV bias gradient is the column sum of the written rows
 DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, const float* mask,
                          float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop,
                          const uint32_t* dmask, float* colsum, hipStream_t st) {
@@ -1086,10 +1122,11 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     const long rows = (long)B * S * H;
     attn_delta_k<<<(int)((rows * 8 + 255) / 256), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
     dim3 grid((S + TK - 1) / TK, B * H);
+    static_assert(TQ == TK, "the dKV and dQ tiles share the colsum rows");
     attn_bwd_dkv_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B,
-                                         S, H, scale, p_drop, dmask);
+                                         S, H, scale, p_drop, dmask, colsum);
     attn_bwd_dq_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B, S,
-                                        H, scale, p_drop, dmask);
+                                        H, scale, p_drop, dmask, colsum);
     const int rc = (int)hipGetLastError();
-    return rc ? rc : (colsum ? 1 : 0);
+    return rc ? rc : (colsum ? 2 : 0);
 }

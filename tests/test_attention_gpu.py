@@ -99,11 +99,13 @@ def test_attention_dropout_mask_parity(S):
     assert (qkv.grad.float() - q32.grad).abs().max().item() < 3e-2 * q32.grad.abs().max().item() + 1e-2
 
 
-@pytest.mark.parametrize("S,sink", [(128, False), (128, True), (100, True), (197, False)])
+@pytest.mark.parametrize("S,sink", [(128, False), (128, True), (100, True), (197, False), (197, True),
+                                    (300, True)])
 def test_qkv_bias_gradient_from_attention_column_sums(S, sink):
-    """The fused attention backward (S <= 128) writes per-batch column sums of dQKV; the QKV
+    """The attention backward writes column sums of dQKV -- per batch (fused kernel, S <= 128)
+    or per batch and 64-row tile (dKV / dQ kernels, S = 197 / 300, ragged last tile); the QKV
     Linear takes its bias gradient from them (into the DataParallel slot, or a fresh tensor)
-    instead of another pass over dQKV.  S = 197 takes the two-kernel path and the plain sum."""
+    instead of another pass over dQKV."""
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd import ops
     torch.manual_seed(2)
