@@ -211,31 +211,33 @@ def agree_across_ranks(group=None) -> int:
     collective on the host group -- call it between steps, never inside backward),
     sums them over the ranks that tuned the signature and sets the argmin everywhere.
     All ranks compute the same answer from the same gathered data.  Returns how many
-    choices changed on this rank (a caller re-runs a warm-up step when > 0: a changed
-    plan may route later GEMMs through signatures not tuned yet)."""
+    signatures had a rank whose choice changed -- the SAME number on every rank, so a
+    caller that re-runs a warm-up step when it is > 0 (a changed plan may route later
+    GEMMs through signatures not tuned yet) does so on every rank or on none (a per-rank
+    count let one rank run an extra step alone: a collective deadlock)."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return 0
-    mine = {k: {f"{kind}:{s}": t for (kind, s), t in v.items()} for k, v in _timings.items()}
+    mine = {"timings": {k: {f"{kind}:{s}": t for (kind, s), t in v.items()} for k, v in _timings.items()},
+            "tuned": {k: f"{v[0]}:{v[1]}" for k, v in _tuned.items()}}
     gathered = [None] * dist.get_world_size(group)
     dist.all_gather_object(gathered, mine, group=group)
     keys = set()
     for g in gathered:
-        keys.update(g.keys())
+        keys.update(g["timings"].keys())
     changed = 0
     for key in sorted(keys):
         tot: dict = {}
         for g in gathered:
-            for c, t in g.get(key, {}).items():
+            for c, t in g["timings"].get(key, {}).items():
                 tot.setdefault(c, []).append(t)
         n = max(len(v) for v in tot.values())
         # only candidates every tuning rank timed compete (the same list on each rank)
         best = min((sum(v), c) for c, v in tot.items() if len(v) == n)[1]
-        kind, s = best.split(":")
-        choice = (kind, int(s))
-        if _tuned.get(key) != choice:
+        if any(g["tuned"].get(key, best) != best for g in gathered):
             changed += 1
-        _tuned[key] = choice
+        kind, s = best.split(":")
+        _tuned[key] = (kind, int(s))
     _save_cache()
     return changed
 

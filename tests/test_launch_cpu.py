@@ -57,15 +57,19 @@ def _agree_all():
     import torch.distributed as dist
     out = _agree()
     got = [None] * dist.get_world_size()
-    dist.all_gather_object(got, out["tuned"])
+    dist.all_gather_object(got, (out["tuned"], out["changed"]))
     return got
 
 
 def test_ranks_agree_on_gemm_plans():
-    plans = Distributor(num_processes=2, use_gpu=False).run(_agree_all)
+    res = Distributor(num_processes=2, use_gpu=False).run(_agree_all)
+    plans = [r[0] for r in res]
     assert plans[0] == plans[1], plans
     assert plans[0]["k1"] == ("small", 1)          # 1.5 + 1.0  vs  0.8 + 1.2 -> small (2.0 < 2.5)
     assert plans[0]["k2"] == ("small", 1)          # 1.0 + 2.0 = 3.0 < 4.0
+    # rank 0 already ran "small" on both, rank 1 "big" / "narrow": both ranks must report the
+    # same count (a caller re-runs a warm-up step on every rank or on none)
+    assert res[0][1] == res[1][1] == 2, res
 
 
 def _hvd_passes(pause):
