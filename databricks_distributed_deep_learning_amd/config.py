@@ -66,6 +66,7 @@ class TrainConfig:
     resume: bool = False
     fault_rank: int = -1             # test-only fault injection (rank that raises)
     fault_step: int = -1
+    check_replicas_every: int = 0    # debug: every N steps assert DP replicas hold identical params
     data: str = "synthetic"          # synthetic (Petastorm/Delta replacement)
     synthetic_pool: int = 4          # distinct device-resident batches cycled
     pad_fraction: float = 0.0        # NLP: random right-padding up to this fraction (attention-mask path)

@@ -67,6 +67,10 @@ class Bucket:
     eager_done: bool = False     # set_eager callback already issued on the side stream
 
 
+class ReplicaDivergence(RuntimeError):
+    """Data-parallel replicas no longer hold identical parameters (see ``check_replicas``)."""
+
+
 class DataParallel(nn.Module):
     """Wrap ``module`` for data-parallel training.
 
@@ -379,6 +383,36 @@ class DataParallel(nn.Module):
                 self._acc32.add_(self.arena.grad)
                 self.arena.grad.zero_()
                 self._acc_active = True
+
+    def replica_fingerprint(self) -> torch.Tensor:
+        """fp64 [sum, position-weighted sum] of this rank's parameter arena (2 numbers per
+        check; weighted so a permutation or a swapped bucket does not cancel out)."""
+        flat = self.arena.flat
+        n = flat.numel()
+        w = torch.arange(1, n + 1, device=flat.device, dtype=torch.float64).remainder_(4093.0).add_(1.0)
+        x = flat.detach().double()
+        return torch.stack([x.sum(), (x * w).sum()])
+
+    def check_replicas(self, rtol: float = 0.0) -> None:
+        """Debug / race check: data-parallel replicas must hold IDENTICAL parameters
+        after every optimizer step (same all-reduced gradient, same update).  A missing stream
+        dependency -- an optimizer reading a bucket before its all-reduce landed, an eager update
+        racing a backward read -- shows up as replicas drifting apart.  All ranks call this at
+        the same step; every rank raises ``ReplicaDivergence`` when fingerprints differ."""
+        if self.world == 1:
+            return
+        self.wait_params()
+        fp = self.replica_fingerprint()
+        lo, hi = fp.clone(), fp.clone()
+        if not fp.is_cuda or dist.get_backend(self.pg) == "gloo":
+            lo, hi = lo.cpu(), hi.cpu()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.pg)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.pg)
+        spread = (hi - lo).abs().cpu()
+        scale = torch.maximum(hi.abs(), lo.abs()).cpu()
+        if bool((spread > rtol * scale).any()):
+            raise ReplicaDivergence(f"rank {ddist.rank()}: parameter replicas differ across ranks "
+                                    f"(fingerprint min {lo.tolist()} max {hi.tolist()})")
 
     def finish(self, on_ready: Optional[Callable[[torch.Tensor, int, int], None]] = None) -> torch.Tensor:
         """Wait for all buckets; return the flat reduced gradient (SUM over ranks).

@@ -245,6 +245,10 @@ class Trainer:
                 self.logger.log({"step": self.step, "loss": gl, "lr": self.opt.lr,
                                  **self.phases.summary(reset=True), **memory_stats(self.device)})
                 timer.start()
+            if c.check_replicas_every and self.step % c.check_replicas_every == 0:
+                t_seg += timer.stop()             # (outside the timed region, like log points)
+                self.ddp.check_replicas()
+                timer.start()
             if c.checkpoint_every and c.checkpoint_dir and self.step % c.checkpoint_every == 0:
                 t_pause = timer.stop()
                 t_seg += t_pause

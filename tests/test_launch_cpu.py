@@ -167,3 +167,35 @@ def test_resume_is_bit_identical(tmp_path):
     out = Distributor(num_processes=2, use_gpu=False, timeout_s=600).run(_resume_bitwise, str(tmp_path))
     assert out["err"] == 0.0, out
     assert {"fwd_ms", "bwd_ms"} <= set(out["phases"]), out
+
+
+def _replicas(corrupt):
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.parallel import ReplicaDivergence
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    cfg = get_preset("resnet18_gloo", batch_size=2, image_size=32, steps=3, warmup_steps=0, num_classes=10,
+                     log_every=0, check_replicas_every=1)
+    t = Trainer(cfg)
+    t.run()                                  # identical replicas: the per-step checks pass
+    if not corrupt:
+        return "ok"
+    if dist.get_rank() == 1:                 # a replica drifts (what a missing stream dependency does)
+        with torch.no_grad():
+            t.ddp.arena.flat[123] += 1e-3
+    try:
+        t.ddp.check_replicas()
+    except ReplicaDivergence as e:
+        return f"caught: {e}"
+    return "missed"
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_replica_divergence_check(corrupt):
+    """DataParallel.check_replicas (Trainer check_replicas_every): identical replicas pass every
+    step; a parameter that differs on one rank raises ReplicaDivergence on every rank."""
+    out = Distributor(num_processes=2, use_gpu=False, timeout_s=300).run(_replicas, corrupt)
+    if corrupt:
+        assert out.startswith("caught: rank 0"), out
+    else:
+        assert out == "ok"

@@ -5,7 +5,9 @@
   for its bucket's all-reduce handle) == the post-backward step, parameters AND optimizer
   state, at world size 2 -- the multi-rank ordering a missing stream dependency breaks;
 * ZeRO-1 on reduce-scatter (local gradient shards, sharded native optimizer kernels,
-  per-bucket all-gathers waited by forward pre-hooks) == replicated data parallelism.
+  per-bucket all-gathers waited by forward pre-hooks) == replicated data parallelism;
+* every arm checks after every step that both ranks hold identical parameters
+  (``DataParallel.check_replicas``).
 """
 import os
 
@@ -31,7 +33,8 @@ def _rank_main(rank, world, port, q, what):
             (dict(zero_optimizer=True), dict(zero_optimizer=False))
         for arm in arms:
             cfg = get_preset("bert_base_ddp", batch_size=4, seq_len=64, steps=3, warmup_steps=0, log_every=0,
-                             backend="gloo", optimizer="adamw", lr=1e-3, bucket_mb=8.0, first_bucket_mb=2.0, **arm)
+                             backend="gloo", optimizer="adamw", lr=1e-3, bucket_mb=8.0, first_bucket_mb=2.0,
+                             check_replicas_every=1, **arm)   # replicas identical after every step
             t = Trainer(cfg)
             if what == "eager":
                 assert t.eager_optimizer == arm["eager_optimizer"]
