@@ -1054,6 +1054,422 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
         }
     }
 }
+
+// ============================================================ forward, 128 < S <= 256
+// ViT-B/16 (S = 197) and BERT at seq 256: one workgroup (8 waves) per (b, h) with K and V of
+// the whole sequence in LDS (64 KB: two workgroups per CU, so one stages while the other
+// computes); wave w owns query blocks w and w + 8, each with all 16 key blocks' scores in
+// registers (64 accumulator VGPRs), so the softmax is exact in one pass as in the S <= 128
+// kernel.  The tiled forward re-staged K / V once per 64 queries and rescaled its running
+// output per 64-key tile.  Both query blocks' Q fragments are loaded in the prologue, under
+// the K / V staging.
+constexpr int FM = 256;        // longest sequence of the medium kernels
+
+template <bool MASK, bool DROP>
+__global__ __launch_bounds__(512, 2) void attn_fwd_med_k(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+                                                          bf16_t* __restrict__ out, float* __restrict__ lse, int S, int H,
+                                                          float scale, float p_drop, uint64_t seed,
+                                                          uint32_t* __restrict__ dmask) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * FM * ROWB + FM * 4];   // K rows, V^T image, mask
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const long rs = 3L * H * D;
+    const bf16_t* qb = qkv + (long)b * S * rs + h * D;
+    const bf16_t* kb = qb + H * D;
+    const bf16_t* vb = qb + 2 * H * D;
+    char* sK = smem;
+    char* sV = smem + FM * ROWB;
+    float* sM = reinterpret_cast<float*>(smem + 2 * FM * ROWB);
+    const int nblk = (S + 15) >> 4;          // key blocks = query blocks (> 8: S > 128)
+    uint4 k4[4], v4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (tid >> 3) + 64 * i, c = tid & 7;
+        const int rr = r < S ? r : 0;
+        k4[i] = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
+        v4[i] = *reinterpret_cast<const uint4*>(vb + (long)rr * rs + c * 8);
+    }
+    float nm = 0.f;
+    if (MASK && tid < FM) nm = tid < S ? mask[(long)b * S + tid] : 0.f;
+    bf16x8 qf[2][2];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+        const int q = 16 * (w + 8 * qi) + (lane & 15);
+        const bf16_t* qr = qb + (long)(q < S ? q : 0) * rs;
+        qf[qi][0] = load_frag_global(qr, 0);
+        qf[qi][1] = load_frag_global(qr, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (tid >> 3) + 64 * i, c = tid & 7;
+        const bool ok = r < S;
+        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = zero_unless(ok, k4[i]);
+        *reinterpret_cast<uint4*>(sV + lds_off<true>(r, c)) = zero_unless(ok, v4[i]);
+    }
+    if (MASK && tid < FM) sM[tid] = nm * LOG2E;
+    __syncthreads();
+    const float c2 = scale * LOG2E;
+    const uint32_t thresh = drop_thresh16(p_drop);
+    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+        const int qblk = w + 8 * qi;
+        if (qblk < nblk) {                       // uniform per wave
+        const int myq = 16 * qblk + (lane & 15);
+        const bool qok = myq < S;
+        // S^T blocks: lane holds s[blk][r] = score(q = myq, k = 16 blk + 4 g + r); blocks past
+        // the last key block stay 0 and are never exponentiated (P = 0 there)
+        f32x4 s[16];
+#pragma unroll
+        for (int blk = 0; blk < 16; ++blk) {
+            s[blk] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (blk < nblk) {
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+                    s[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sK, 16 * blk, kk), qf[qi][kk],
+                                                                      s[blk], 0, 0, 0);
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int blk = 0; blk < 16; ++blk) {
+            if (blk >= nblk) continue;
+            const int k0 = 16 * blk + 4 * g;
+            float4 mk = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (MASK) mk = *reinterpret_cast<const float4*>(sM + k0);
+            const float mka[4] = {mk.x, mk.y, mk.z, mk.w};
+            const bool edge = 16 * blk + 16 > S;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = MASK ? s[blk][r] * c2 + mka[r] : s[blk][r] * c2;
+                if (edge && k0 + r >= S) v = -INFINITY;
+                s[blk][r] = v;
+                mx = fmaxf(mx, v);
+            }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float msub = mx == -INFINITY ? 0.f : mx;
+        const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;
+        float lsum = 0.f;
+        uint32_t kbits[2] = {0u, 0u};            // keep bits of keys 0..127 / 128..255
+#pragma unroll
+        for (int blk = 0; blk < 16; ++blk) {
+            if (blk >= nblk) continue;
+            bool keep[4] = {true, true, true, true};
+            if (DROP) attn_keep4(seed, rowidx + 16 * blk + 4 * g, thresh, S & 1, keep);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float pv = fast_exp2(s[blk][r] - msub);
+                lsum += pv;
+                if (DROP) {
+                    pv = keep[r] ? pv * inv_keep : 0.f;
+                    kbits[blk >> 3] |= (uint32_t)keep[r] << (4 * (blk & 7) + r);
+                }
+                s[blk][r] = pv;
+            }
+        }
+        if (DROP && qok) {
+            dmask[dmask_word(bh, S, 0, g, myq)] = kbits[0];
+            dmask[dmask_word(bh, S, 1, g, myq)] = kbits[1];
+        }
+        lsum += __shfl_xor(lsum, 16, 64);
+        lsum += __shfl_xor(lsum, 32, 64);
+        // O^T[d][q] = V^T[d][k] P^T[k][q], 32 keys per step
+        f32x4 o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+            if (2 * st >= nblk) continue;
+            const bf16x8 pf = pack_acc(s[2 * st], s[2 * st + 1]);
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+                o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sV, 32 * st, 16 * db), pf, o[db], 0, 0, 0);
+        }
+        if (qok) {
+            const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+            bf16_t* orow = out + ((long)b * S + myq) * H * D + h * D;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                float v[4] = {o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv};
+                store4(orow + 16 * db + 4 * g, v);
+            }
+            if (g == 0) lse[(long)bh * S + myq] = (mx + log2f(lsum)) / LOG2E;
+        }
+        }
+    }
+}
+
+// ============================================================ fused backward, 128 < S <= 256
+// The S <= 128 fused backward scaled to 256 rows: Q, K, dO row images (96 KB: one workgroup
+// per CU), delta / LSE / mask / dropout words in LDS, then
+//   phase 1 (lane = key): wave w owns key blocks w and w + 8 in turn -- S, dP over all queries
+//           in 32-query chunks, P, dS -> dK, dV complete in registers and stored; both blocks'
+//           dS columns stay in registers as bf16 (2 x 32 VGPRs);
+//   phase 2 (lane = query), in two halves of 128 queries: the half's dS^T columns go to LDS as
+//           two [256 keys][64 queries] row images over the Q and dO images (64 KB), then
+//           dQ = dS K for query blocks w (first half) and w + 8 (second half).
+// Replaces the delta pass + dK/dV kernel + dQ kernel of the tiled path, which re-derived P and
+// dP in both kernels and re-read Q / K / V / dO once per 64 x 64 tile pair.
+template <bool DROP>
+__global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restrict__ qkv,
+                                                          const bf16_t* __restrict__ out,
+                                                          const bf16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
+                                                          int S, int H, float scale, float p_drop,
+                                                          const uint32_t* __restrict__ dmask,
+                                                          float* __restrict__ colsum) {
+    // one LDS object, carved by hand: Q, K, dO images | col sums [8][3][D] | LSE | delta | mask | keep words
+    constexpr int IMG = FM * ROWB;
+    constexpr int OFF_CS = 3 * IMG;
+    constexpr int OFF_LSE = OFF_CS + 8 * 3 * D * 4;
+    constexpr int OFF_DEL = OFF_LSE + FM * 4;
+    constexpr int OFF_MSK = OFF_DEL + FM * 4;
+    constexpr int OFF_DM = OFF_MSK + FM * 4;
+    __shared__ __attribute__((aligned(16))) char smem[OFF_DM + (DROP ? 2 * 4 * FM * 4 : 16)];
+    float* s_cs = reinterpret_cast<float*>(smem + OFF_CS);     // [w][part][d]
+    float* s_lse = reinterpret_cast<float*>(smem + OFF_LSE);
+    float* s_delta = reinterpret_cast<float*>(smem + OFF_DEL);
+    float* s_mask = reinterpret_cast<float*>(smem + OFF_MSK);
+    uint32_t* s_dm = reinterpret_cast<uint32_t*>(smem + OFF_DM);   // keep-bit words [kw][g][q]
+    const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+    const long rs = 3L * H * D;
+    const long ors = (long)H * D;
+    const bf16_t* qb = qkv + (long)b * S * rs + h * D;
+    const bf16_t* kb = qb + H * D;
+    const bf16_t* vb = qb + 2 * H * D;
+    const bf16_t* dob = dout + (long)b * S * ors + h * D;
+    const bf16_t* ob = out + (long)b * S * ors + h * D;
+    char* sQ = smem;
+    char* sK = sQ + IMG;
+    char* sO = sK + IMG;
+    char* sT0 = sQ;                 // dS^T[:, half + 0:64]   (phase 2)
+    char* sT1 = sO;                 // dS^T[:, half + 64:128] (phase 2)
+    const int nblk = (S + 15) >> 4;
+    const int nch = (S + 31) >> 5;  // 32-row chunks
+
+    // ---- prologue: my key blocks' V fragments (B operand of dP^T), then the row images
+    bf16x8 vf[2][2];
+#pragma unroll
+    for (int ki = 0; ki < 2; ++ki) {
+        const int k = 16 * (w + 8 * ki) + (lane & 15);
+        const bf16_t* vr = vb + (long)(k < S ? k : 0) * rs;
+        vf[ki][0] = load_frag_global(vr, 0);
+        vf[ki][1] = load_frag_global(vr, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (tid >> 3) + 64 * i, c = tid & 7;
+        const bool ok = r < S;
+        const int rr = ok ? r : 0;
+        const uint4 q4 = *reinterpret_cast<const uint4*>(qb + (long)rr * rs + c * 8);
+        const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
+        const uint4 o4 = *reinterpret_cast<const uint4*>(dob + (long)rr * ors + c * 8);
+        *reinterpret_cast<uint4*>(sQ + lds_off<false>(r, c)) = zero_unless(ok, q4);
+        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = zero_unless(ok, k4);
+        *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = zero_unless(ok, o4);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        // delta[q] = sum_d dO[q][d] O[q][d]: 4 threads per query, 16 d each
+        const int q = (tid >> 2) + 128 * j, part = tid & 3;
+        float a = 0.f;
+        if (q < S) {
+            float x[8], y[8];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                load8(dob + (long)q * ors + part * 16 + hh * 8, x);
+                load8(ob + (long)q * ors + part * 16 + hh * 8, y);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a += x[e] * y[e];
+            }
+        }
+        a += __shfl_xor(a, 1);
+        a += __shfl_xor(a, 2);
+        if (part == 0) s_delta[q] = a;
+    }
+    if (tid < FM) {
+        s_lse[tid] = tid < S ? lse[(long)bh * S + tid] * LOG2E : 0.f;
+        s_mask[tid] = (mask && tid < S) ? mask[(long)b * S + tid] * LOG2E : 0.f;
+    }
+    if (DROP) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = tid + 512 * i, kw = idx >> 10, gq = (idx >> 8) & 3, q = idx & (FM - 1);
+            s_dm[idx] = q < S ? dmask[dmask_word(bh, S, kw, gq, q)] : 0u;
+        }
+    }
+    __syncthreads();
+
+    const float c2 = scale * LOG2E;
+    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    uint2 dsk[2][16];               // my keys' dS columns, bf16, blocks of 4 queries: [key block][query block]
+
+    // ---- phase 1: lane = key
+#pragma unroll
+    for (int ki = 0; ki < 2; ++ki) {
+        const int kblk = w + 8 * ki;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dsk[ki][c] = make_uint2(0u, 0u);
+        if (kblk < nblk) {              // uniform per wave (S > 128: every wave has block w)
+            const int myk = 16 * kblk + (lane & 15);
+            const bool kok = myk < S;
+            bf16x8 kf[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) kf[kk] = frag_rows<false>(sK, 16 * kblk, kk);
+            const float mb2 = s_mask[kok ? myk : 0];
+            const int kq = kok ? myk : 0;
+            const uint32_t* dmw = s_dm + (DROP ? (kq >> 7) * 4 * FM + ((kq >> 2) & 3) * FM : 0);
+            const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
+            f32x4 dv[4], dk[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
+#pragma unroll
+            for (int qc = 0; qc < 8; ++qc) {
+                if (qc >= nch) break;
+                f32x4 sc[2], dp[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    sc[j] = (f32x4){0, 0, 0, 0};
+                    dp[j] = (f32x4){0, 0, 0, 0};
+#pragma unroll
+                    for (int kk = 0; kk < 2; ++kk) {
+                        sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sQ, 32 * qc + 16 * j, kk),
+                                                                        kf[kk], sc[j], 0, 0, 0);
+                        dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sO, 32 * qc + 16 * j, kk),
+                                                                        vf[ki][kk], dp[j], 0, 0, 0);
+                    }
+                }
+                f32x4 pd[2], ds[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int q0 = 32 * qc + 16 * j + 4 * g;
+                    const f32x4 lse4 = *reinterpret_cast<const f32x4*>(s_lse + q0);
+                    const f32x4 del4 = *reinterpret_cast<const f32x4*>(s_delta + q0);
+                    const uint32_t kb4 = DROP ? dmask_pick4(*reinterpret_cast<const uint4*>(dmw + q0), kbit) : 0xfu;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int ql = q0 + r;
+                        const float pv = (ql < S && kok) ? fast_exp2(sc[j][r] * c2 + (mb2 - lse4[r])) : 0.f;
+                        float dpv = dp[j][r];
+                        float pdrop = pv;
+                        if (DROP) {
+                            const bool keep = (kb4 >> r) & 1u;
+                            pdrop = keep ? pv * inv_keep : 0.f;
+                            dpv = keep ? dpv * inv_keep : 0.f;
+                        }
+                        pd[j][r] = pdrop;
+                        ds[j][r] = pv * (dpv - del4[r]);
+                    }
+                    dsk[ki][2 * qc + j] = make_uint2(pack2bf(ds[j][0], ds[j][1]), pack2bf(ds[j][2], ds[j][3]));
+                }
+                const bf16x8 pf = pack_acc(pd[0], pd[1]);
+                const bf16x8 sf = pack_acc(ds[0], ds[1]);
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sO, 32 * qc, 16 * db), pf, dv[db],
+                                                                     0, 0, 0);
+                    dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sQ, 32 * qc, 16 * db), sf, dk[db],
+                                                                     0, 0, 0);
+                }
+            }
+            if (kok) {
+                bf16_t* dkr = dqkv + ((long)b * S + myk) * rs + H * D + h * D;
+                bf16_t* dvr = dkr + H * D;
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    float a4[4] = {dk[db][0] * scale, dk[db][1] * scale, dk[db][2] * scale, dk[db][3] * scale};
+                    float b4[4] = {dv[db][0], dv[db][1], dv[db][2], dv[db][3]};
+                    store4(dkr + 16 * db + 4 * g, a4);
+                    store4(dvr + 16 * db + 4 * g, b4);
+                }
+            }
+            if (colsum) {   // keys past S hold zero gradients
+#pragma unroll
+                for (int db = 0; db < 4; ++db)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float sk = row16_sum(dk[db][e] * scale), sv = row16_sum(dv[db][e]);
+                        if ((lane & 15) == 0) {
+                            float* c1 = s_cs + (w * 3 + 1) * D + 16 * db + 4 * g + e;
+                            float* c2p = s_cs + (w * 3 + 2) * D + 16 * db + 4 * g + e;
+                            *c1 = ki ? *c1 + sk : sk;
+                            *c2p = ki ? *c2p + sv : sv;
+                        }
+                    }
+            }
+        }
+    }
+
+    // ---- phase 2, two halves of 128 queries: dQ^T[d][q] = K^T[d][k] dS^T[k][q] over all keys
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        __syncthreads();            // phase 1 / the previous half is done with the images it overwrites
+#pragma unroll
+        for (int ki = 0; ki < 2; ++ki) {
+            const int myk = 16 * (w + 8 * ki) + (lane & 15);   // rows of absent blocks / keys get zeros
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int q0 = 16 * c + 4 * g;
+                char* img = q0 < 64 ? sT0 : sT1;
+                const int qq = q0 & 63;
+                *reinterpret_cast<uint2*>(img + lds_off<false>(myk, qq >> 3) + (qq & 7) * 2) = dsk[ki][8 * half + c];
+            }
+        }
+        __syncthreads();
+        const int qblk = 8 * half + w;
+        if (qblk < nblk) {
+            const int myq = 16 * qblk + (lane & 15);
+            const char* img = w < 4 ? sT0 : sT1;
+            const int cb = (16 * w) & 63;
+            f32x4 dq[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                if (st >= nch) break;
+                const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
+#pragma unroll
+                for (int db = 0; db < 4; ++db)
+                    dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 16 * db), sf, dq[db],
+                                                                     0, 0, 0);
+            }
+            if (myq < S) {
+                bf16_t* dqr = dqkv + ((long)b * S + myq) * rs + h * D;
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    float a4[4] = {dq[db][0] * scale, dq[db][1] * scale, dq[db][2] * scale, dq[db][3] * scale};
+                    store4(dqr + 16 * db + 4 * g, a4);
+                }
+            }
+            if (colsum) {   // queries past S hold zero gradients
+#pragma unroll
+                for (int db = 0; db < 4; ++db)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float sq = row16_sum(dq[db][e] * scale);
+                        if ((lane & 15) == 0) {
+                            float* c0 = s_cs + (w * 3 + 0) * D + 16 * db + 4 * g + e;
+                            *c0 = half ? *c0 + sq : sq;
+                        }
+                    }
+            }
+        }
+    }
+    if (colsum) {
+        __syncthreads();
+        if (tid < 3 * D) {
+            const int part = tid / D, d = tid - part * D;
+            float acc = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < 8; ++ww) acc += s_cs[(ww * 3 + part) * D + d];
+            colsum[(long)b * 3 * H * D + part * H * D + h * D + d] = acc;
+        }
+    }
+}
 }  // namespace
 
 namespace {
@@ -1071,6 +1487,14 @@ bool fused_bwd_enabled() {
     static const bool on = [] {
         const char* e = getenv("DDL_ATTN_FUSED_BWD");
         return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// DDL_ATTN_MED=0: 128 < S <= 256 takes the tiled forward and two-kernel backward (A/B timing)
+bool med_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_ATTN_MED");
+        return fused_bwd_enabled() && !(e && e[0] == '0');
     }();
     return on;
 }
@@ -1098,6 +1522,13 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
 #undef FWD_SHORT
         DDL_RETURN_LAUNCH();
     }
+    if (S <= FM && med_enabled()) {
+#define FWD_MED(M, D) attn_fwd_med_k<M, D><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, S, H, scale, p_drop, seed, dmask)
+        if (mask) { if (p_drop > 0.f) FWD_MED(true, true); else FWD_MED(true, false); }
+        else { if (p_drop > 0.f) FWD_MED(false, true); else FWD_MED(false, false); }
+#undef FWD_MED
+        DDL_RETURN_LAUNCH();
+    }
     dim3 grid((S + TQ - 1) / TQ, B * H);
     attn_fwd_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed, dmask);
     DDL_RETURN_LAUNCH();
@@ -1117,6 +1548,13 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
         if (S == FS) { if (p_drop > 0.f) BWD_FUSED(true, true); else BWD_FUSED(true, false); }
         else { if (p_drop > 0.f) BWD_FUSED(false, true); else BWD_FUSED(false, false); }
 #undef BWD_FUSED
+        DDL_RETURN_LAUNCH();
+    }
+    if (S <= FM && med_enabled()) {   // 96 KB of row images: one workgroup per CU
+#define BWD_MED(DR) attn_bwd_med_k<DR><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, \
+        (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, dmask, colsum)
+        if (p_drop > 0.f) BWD_MED(true); else BWD_MED(false);
+#undef BWD_MED
         DDL_RETURN_LAUNCH();
     }
     const long rows = (long)B * S * H;

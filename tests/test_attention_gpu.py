@@ -50,7 +50,8 @@ def ref_attention(qkv, H, mask=None, keep=None, p=0.0):
     return (pr @ v).permute(0, 2, 1, 3).reshape(B, S, H * D)
 
 
-@pytest.mark.parametrize("B,S,H", [(2, 128, 12), (3, 197, 2), (1, 64, 4), (2, 100, 3), (1, 512, 2)])
+@pytest.mark.parametrize("B,S,H", [(2, 128, 12), (3, 197, 2), (2, 256, 3), (1, 129, 2), (1, 64, 4), (2, 100, 3),
+                                   (1, 257, 2), (1, 512, 2)])
 @pytest.mark.parametrize("masked", [False, True])
 def test_attention_fwd_bwd(B, S, H, masked):
     dev = gpu_device()
@@ -73,7 +74,7 @@ def test_attention_fwd_bwd(B, S, H, masked):
     assert gerr < 3e-2 * q32.grad.abs().max().item() + 1e-2, gerr
 
 
-@pytest.mark.parametrize("S", [96, 97])          # odd S: pairs of score indices straddle rows
+@pytest.mark.parametrize("S", [96, 97, 197, 256])   # odd S: pairs of score indices straddle rows; > 128: medium kernels
 def test_attention_dropout_mask_parity(S):
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd.ops import _native_attention as NA
