@@ -1202,29 +1202,34 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_med_k(const bf16_t* __restric
 }
 
 // ============================================================ fused backward, 128 < S <= 256
-// The S <= 128 fused backward scaled to 256 rows: Q, K, dO row images (96 KB: one workgroup
-// per CU), delta / LSE / mask / dropout words in LDS, then
-//   phase 1 (lane = key): wave w owns key blocks w and w + 8 in turn -- S, dP over all queries
-//           in 32-query chunks, P, dS -> dK, dV complete in registers and stored; both blocks'
-//           dS columns stay in registers as bf16 (2 x 32 VGPRs);
+// The S <= 128 fused backward scaled to 256 rows, with 16 waves (1024 threads: four per SIMD
+// to cover the LDS and MFMA latencies of the one workgroup a CU holds): Q, K, dO row images
+// (96 KB), delta / LSE / mask / dropout words in LDS, then
+//   phase 1 (lane = key): wave w owns key block w -- S, dP over all queries in 32-query
+//           chunks, P, dS -> dK, dV complete in registers and stored; the lane's dS column
+//           stays in registers as bf16 (32 VGPRs);
 //   phase 2 (lane = query), in two halves of 128 queries: the half's dS^T columns go to LDS as
 //           two [256 keys][64 queries] row images over the Q and dO images (64 KB), then
-//           dQ = dS K for query blocks w (first half) and w + 8 (second half).
+//           dQ = dS K, wave w computing query block (w & 7) of the half, head dims
+//           32 (w >> 3) .. +31.
 // Replaces the delta pass + dK/dV kernel + dQ kernel of the tiled path, which re-derived P and
 // dP in both kernels and re-read Q / K / V / dO once per 64 x 64 tile pair.
+constexpr int MW = 16;         // waves per workgroup of the medium backward
+
 template <bool DROP>
-__global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restrict__ qkv,
-                                                          const bf16_t* __restrict__ out,
-                                                          const bf16_t* __restrict__ dout,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
-                                                          int S, int H, float scale, float p_drop,
-                                                          const uint32_t* __restrict__ dmask,
-                                                          float* __restrict__ colsum) {
-    // one LDS object, carved by hand: Q, K, dO images | col sums [8][3][D] | LSE | delta | mask | keep words
+__global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __restrict__ qkv,
+                                                              const bf16_t* __restrict__ out,
+                                                              const bf16_t* __restrict__ dout,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
+                                                              int S, int H, float scale, float p_drop,
+                                                              const uint32_t* __restrict__ dmask,
+                                                              float* __restrict__ colsum) {
+    // one LDS object, carved by hand: Q, K, dO images | col sums [MW][3][D] | LSE | delta | mask | keep words
+    constexpr int NT = 64 * MW;
     constexpr int IMG = FM * ROWB;
     constexpr int OFF_CS = 3 * IMG;
-    constexpr int OFF_LSE = OFF_CS + 8 * 3 * D * 4;
+    constexpr int OFF_LSE = OFF_CS + MW * 3 * D * 4;
     constexpr int OFF_DEL = OFF_LSE + FM * 4;
     constexpr int OFF_MSK = OFF_DEL + FM * 4;
     constexpr int OFF_DM = OFF_MSK + FM * 4;
@@ -1250,19 +1255,19 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
     char* sT1 = sO;                 // dS^T[:, half + 64:128] (phase 2)
     const int nblk = (S + 15) >> 4;
     const int nch = (S + 31) >> 5;  // 32-row chunks
+    const int myk = 16 * w + (lane & 15);
+    const bool kok = myk < S;
 
-    // ---- prologue: my key blocks' V fragments (B operand of dP^T), then the row images
-    bf16x8 vf[2][2];
-#pragma unroll
-    for (int ki = 0; ki < 2; ++ki) {
-        const int k = 16 * (w + 8 * ki) + (lane & 15);
-        const bf16_t* vr = vb + (long)(k < S ? k : 0) * rs;
-        vf[ki][0] = load_frag_global(vr, 0);
-        vf[ki][1] = load_frag_global(vr, 1);
+    // ---- prologue: my key block's V fragments (B operand of dP^T), then the row images
+    bf16x8 vf[2];
+    {
+        const bf16_t* vr = vb + (long)(kok ? myk : 0) * rs;
+        vf[0] = load_frag_global(vr, 0);
+        vf[1] = load_frag_global(vr, 1);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = (tid >> 3) + 64 * i, c = tid & 7;
+    for (int i = 0; i < 2; ++i) {
+        const int r = (tid >> 3) + (NT / 8) * i, c = tid & 7;
         const bool ok = r < S;
         const int rr = ok ? r : 0;
         const uint4 q4 = *reinterpret_cast<const uint4*>(qb + (long)rr * rs + c * 8);
@@ -1272,10 +1277,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
         *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = zero_unless(ok, k4);
         *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = zero_unless(ok, o4);
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    {
         // delta[q] = sum_d dO[q][d] O[q][d]: 4 threads per query, 16 d each
-        const int q = (tid >> 2) + 128 * j, part = tid & 3;
+        const int q = tid >> 2, part = tid & 3;
         float a = 0.f;
         if (q < S) {
             float x[8], y[8];
@@ -1297,8 +1301,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
     }
     if (DROP) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = tid + 512 * i, kw = idx >> 10, gq = (idx >> 8) & 3, q = idx & (FM - 1);
+        for (int i = 0; i < 2; ++i) {
+            const int idx = tid + NT * i, kw = idx >> 10, gq = (idx >> 8) & 3, q = idx & (FM - 1);
             s_dm[idx] = q < S ? dmask[dmask_word(bh, S, kw, gq, q)] : 0u;
         }
     }
@@ -1306,30 +1310,25 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
 
     const float c2 = scale * LOG2E;
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-    uint2 dsk[2][16];               // my keys' dS columns, bf16, blocks of 4 queries: [key block][query block]
+    uint2 dsk[16];                  // my key's dS column, bf16, blocks of 4 queries per query block
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dsk[c] = make_uint2(0u, 0u);
 
     // ---- phase 1: lane = key
+    if (w < nblk) {                 // uniform per wave
+        bf16x8 kf[2];
 #pragma unroll
-    for (int ki = 0; ki < 2; ++ki) {
-        const int kblk = w + 8 * ki;
+        for (int kk = 0; kk < 2; ++kk) kf[kk] = frag_rows<false>(sK, 16 * w, kk);
+        const float mb2 = s_mask[kok ? myk : 0];
+        const int kq = kok ? myk : 0;
+        const uint32_t* dmw = s_dm + (DROP ? (kq >> 7) * 4 * FM + ((kq >> 2) & 3) * FM : 0);
+        const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
+        f32x4 dv[4], dk[4];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) dsk[ki][c] = make_uint2(0u, 0u);
-        if (kblk < nblk) {              // uniform per wave (S > 128: every wave has block w)
-            const int myk = 16 * kblk + (lane & 15);
-            const bool kok = myk < S;
-            bf16x8 kf[2];
+        for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) kf[kk] = frag_rows<false>(sK, 16 * kblk, kk);
-            const float mb2 = s_mask[kok ? myk : 0];
-            const int kq = kok ? myk : 0;
-            const uint32_t* dmw = s_dm + (DROP ? (kq >> 7) * 4 * FM + ((kq >> 2) & 3) * FM : 0);
-            const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
-            f32x4 dv[4], dk[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
-#pragma unroll
-            for (int qc = 0; qc < 8; ++qc) {
-                if (qc >= nch) break;
+        for (int qc = 0; qc < 8; ++qc) {
+            if (qc < nch) {
                 f32x4 sc[2], dp[2];
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -1340,7 +1339,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
                         sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sQ, 32 * qc + 16 * j, kk),
                                                                         kf[kk], sc[j], 0, 0, 0);
                         dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sO, 32 * qc + 16 * j, kk),
-                                                                        vf[ki][kk], dp[j], 0, 0, 0);
+                                                                        vf[kk], dp[j], 0, 0, 0);
                     }
                 }
                 f32x4 pd[2], ds[2];
@@ -1364,7 +1363,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
                         pd[j][r] = pdrop;
                         ds[j][r] = pv * (dpv - del4[r]);
                     }
-                    dsk[ki][2 * qc + j] = make_uint2(pack2bf(ds[j][0], ds[j][1]), pack2bf(ds[j][2], ds[j][3]));
+                    dsk[2 * qc + j] = make_uint2(pack2bf(ds[j][0], ds[j][1]), pack2bf(ds[j][2], ds[j][3]));
                 }
                 const bf16x8 pf = pack_acc(pd[0], pd[1]);
                 const bf16x8 sf = pack_acc(ds[0], ds[1]);
@@ -1376,83 +1375,82 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
                                                                      0, 0, 0);
                 }
             }
-            if (kok) {
-                bf16_t* dkr = dqkv + ((long)b * S + myk) * rs + H * D + h * D;
-                bf16_t* dvr = dkr + H * D;
+        }
+        if (kok) {
+            bf16_t* dkr = dqkv + ((long)b * S + myk) * rs + H * D + h * D;
+            bf16_t* dvr = dkr + H * D;
 #pragma unroll
-                for (int db = 0; db < 4; ++db) {
-                    float a4[4] = {dk[db][0] * scale, dk[db][1] * scale, dk[db][2] * scale, dk[db][3] * scale};
-                    float b4[4] = {dv[db][0], dv[db][1], dv[db][2], dv[db][3]};
-                    store4(dkr + 16 * db + 4 * g, a4);
-                    store4(dvr + 16 * db + 4 * g, b4);
-                }
-            }
-            if (colsum) {   // keys past S hold zero gradients
-#pragma unroll
-                for (int db = 0; db < 4; ++db)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float sk = row16_sum(dk[db][e] * scale), sv = row16_sum(dv[db][e]);
-                        if ((lane & 15) == 0) {
-                            float* c1 = s_cs + (w * 3 + 1) * D + 16 * db + 4 * g + e;
-                            float* c2p = s_cs + (w * 3 + 2) * D + 16 * db + 4 * g + e;
-                            *c1 = ki ? *c1 + sk : sk;
-                            *c2p = ki ? *c2p + sv : sv;
-                        }
-                    }
+            for (int db = 0; db < 4; ++db) {
+                float a4[4] = {dk[db][0] * scale, dk[db][1] * scale, dk[db][2] * scale, dk[db][3] * scale};
+                float b4[4] = {dv[db][0], dv[db][1], dv[db][2], dv[db][3]};
+                store4(dkr + 16 * db + 4 * g, a4);
+                store4(dvr + 16 * db + 4 * g, b4);
             }
         }
+        if (colsum) {   // keys past S hold zero gradients
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float sk = row16_sum(dk[db][e] * scale), sv = row16_sum(dv[db][e]);
+                    if ((lane & 15) == 0) {
+                        s_cs[(w * 3 + 1) * D + 16 * db + 4 * g + e] = sk;
+                        s_cs[(w * 3 + 2) * D + 16 * db + 4 * g + e] = sv;
+                    }
+                }
+        }
+    } else if (colsum && lane < D) {   // no key block: zero dK / dV column sums
+        s_cs[(w * 3 + 1) * D + lane] = 0.f;
+        s_cs[(w * 3 + 2) * D + lane] = 0.f;
     }
 
     // ---- phase 2, two halves of 128 queries: dQ^T[d][q] = K^T[d][k] dS^T[k][q] over all keys
+    const int qsub = w & 7, dh = w >> 3;        // query block within the half, head-dim half
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
         __syncthreads();            // phase 1 / the previous half is done with the images it overwrites
 #pragma unroll
-        for (int ki = 0; ki < 2; ++ki) {
-            const int myk = 16 * (w + 8 * ki) + (lane & 15);   // rows of absent blocks / keys get zeros
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const int q0 = 16 * c + 4 * g;
-                char* img = q0 < 64 ? sT0 : sT1;
-                const int qq = q0 & 63;
-                *reinterpret_cast<uint2*>(img + lds_off<false>(myk, qq >> 3) + (qq & 7) * 2) = dsk[ki][8 * half + c];
-            }
+        for (int c = 0; c < 8; ++c) {   // rows of absent key blocks / keys past S get zeros
+            const int q0 = 16 * c + 4 * g;
+            char* img = q0 < 64 ? sT0 : sT1;
+            const int qq = q0 & 63;
+            *reinterpret_cast<uint2*>(img + lds_off<false>(myk, qq >> 3) + (qq & 7) * 2) = dsk[8 * half + c];
         }
         __syncthreads();
-        const int qblk = 8 * half + w;
+        const int qblk = 8 * half + qsub;
         if (qblk < nblk) {
             const int myq = 16 * qblk + (lane & 15);
-            const char* img = w < 4 ? sT0 : sT1;
-            const int cb = (16 * w) & 63;
-            f32x4 dq[4];
+            const char* img = qsub < 4 ? sT0 : sT1;
+            const int cb = (16 * qsub) & 63;
+            f32x4 dq[2];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
+            for (int i = 0; i < 2; ++i) dq[i] = (f32x4){0, 0, 0, 0};
 #pragma unroll
             for (int st = 0; st < 8; ++st) {
-                if (st >= nch) break;
-                const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
+                if (st < nch) {
+                    const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
 #pragma unroll
-                for (int db = 0; db < 4; ++db)
-                    dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 16 * db), sf, dq[db],
-                                                                     0, 0, 0);
-            }
-            if (myq < S) {
-                bf16_t* dqr = dqkv + ((long)b * S + myq) * rs + h * D;
-#pragma unroll
-                for (int db = 0; db < 4; ++db) {
-                    float a4[4] = {dq[db][0] * scale, dq[db][1] * scale, dq[db][2] * scale, dq[db][3] * scale};
-                    store4(dqr + 16 * db + 4 * g, a4);
+                    for (int i = 0; i < 2; ++i)
+                        dq[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 32 * dh + 16 * i),
+                                                                        sf, dq[i], 0, 0, 0);
                 }
             }
-            if (colsum) {   // queries past S hold zero gradients
+            if (myq < S) {
+                bf16_t* dqr = dqkv + ((long)b * S + myq) * rs + h * D + 32 * dh;
 #pragma unroll
-                for (int db = 0; db < 4; ++db)
+                for (int i = 0; i < 2; ++i) {
+                    float a4[4] = {dq[i][0] * scale, dq[i][1] * scale, dq[i][2] * scale, dq[i][3] * scale};
+                    store4(dqr + 16 * i + 4 * g, a4);
+                }
+            }
+            if (colsum) {   // queries past S hold zero gradients; wave w sums head dims 32 dh .. +31
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const float sq = row16_sum(dq[db][e] * scale);
+                        const float sq = row16_sum(dq[i][e] * scale);
                         if ((lane & 15) == 0) {
-                            float* c0 = s_cs + (w * 3 + 0) * D + 16 * db + 4 * g + e;
+                            float* c0 = s_cs + (w * 3 + 0) * D + 32 * dh + 16 * i + 4 * g + e;
                             *c0 = half ? *c0 + sq : sq;
                         }
                     }
@@ -1464,8 +1462,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_med_k(const bf16_t* __restric
         if (tid < 3 * D) {
             const int part = tid / D, d = tid - part * D;
             float acc = 0.f;
+            if (part == 0) {        // dQ: waves 8 (d >> 5) .. +7 hold head dim d
 #pragma unroll
-            for (int ww = 0; ww < 8; ++ww) acc += s_cs[(ww * 3 + part) * D + d];
+                for (int ww = 0; ww < 8; ++ww) acc += s_cs[((8 * (d >> 5) + ww) * 3) * D + d];
+            } else {
+#pragma unroll
+                for (int ww = 0; ww < MW; ++ww) acc += s_cs[(ww * 3 + part) * D + d];
+            }
             colsum[(long)b * 3 * H * D + part * H * D + h * D + d] = acc;
         }
     }
@@ -1551,7 +1554,7 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
         DDL_RETURN_LAUNCH();
     }
     if (S <= FM && med_enabled()) {   // 96 KB of row images: one workgroup per CU
-#define BWD_MED(DR) attn_bwd_med_k<DR><<<B * H, 512, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, \
+#define BWD_MED(DR) attn_bwd_med_k<DR><<<B * H, 64 * MW, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)out, \
         (const bf16_t*)dout, lse, mask, (bf16_t*)dqkv, S, H, scale, p_drop, dmask, colsum)
         if (p_drop > 0.f) BWD_MED(true); else BWD_MED(false);
 #undef BWD_MED
