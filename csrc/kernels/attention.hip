@@ -44,7 +44,11 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 
 // Row image swizzle (128-B rows; ds_read_b128 fragment reads conflict free).
 __device__ __forceinline__ int swz_row(int r, int c) { return c ^ ((r >> 1) & 7); }
-// V / transposed-read image: 8 consecutive rows x 2 chunks conflict free for tr reads.
+// V / transposed-read image: 8 consecutive rows x 2 chunks conflict free for tr reads.  It is
+// conflict free for frag_rows' ds_read_b128 groups too (16-row fragments: the 8 even and the 8
+// odd rows of a lane group land on 8 distinct 16-B slots), so images read BOTH ways (Q, dO, K
+// and the dS^T images of the fused backward kernels) use it; the row swizzle above put pairs of
+// rows on the same slots for the tr reads (2-way conflicts: ~32 % extra LDS cycles).
 __device__ __forceinline__ int swz_tr(int r, int c) { return c ^ (2 * ((r >> 1) & 3)); }
 
 template <bool TR>
@@ -862,9 +866,9 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
         const uint4 q4 = *reinterpret_cast<const uint4*>(qb + (long)rr * rs + c * 8);
         const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
         const uint4 o4 = *reinterpret_cast<const uint4*>(dob + (long)rr * ors + c * 8);
-        *reinterpret_cast<uint4*>(sQ + lds_off<false>(r, c)) = zero_unless(ok, q4);
-        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = zero_unless(ok, k4);
-        *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = zero_unless(ok, o4);
+        *reinterpret_cast<uint4*>(sQ + lds_off<true>(r, c)) = zero_unless(ok, q4);
+        *reinterpret_cast<uint4*>(sK + lds_off<true>(r, c)) = zero_unless(ok, k4);
+        *reinterpret_cast<uint4*>(sO + lds_off<true>(r, c)) = zero_unless(ok, o4);
     }
     {
         // delta[q] = sum_d dO[q][d] O[q][d]: 4 threads per query, 16 d each
@@ -905,7 +909,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
         const bf16_t* vr = vb + (long)(kok ? myk : 0) * rs;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            kf[kk] = frag_rows<false>(sK, 16 * w, kk);   // B operand: my key's row, d = 32kk + 8g ..
+            kf[kk] = frag_rows<true>(sK, 16 * w, kk);   // B operand: my key's row, d = 32kk + 8g ..
             vf[kk] = load_frag_global(vr, kk);
         }
         const float mb2 = s_mask[kok ? myk : 0];
@@ -927,9 +931,9 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
                 dp[j] = (f32x4){0, 0, 0, 0};
 #pragma unroll
                 for (int kk = 0; kk < 2; ++kk) {
-                    sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sQ, 32 * qc + 16 * j, kk), kf[kk],
+                    sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sQ, 32 * qc + 16 * j, kk), kf[kk],
                                                                     sc[j], 0, 0, 0);
-                    dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sO, 32 * qc + 16 * j, kk), vf[kk],
+                    dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sO, 32 * qc + 16 * j, kk), vf[kk],
                                                                     dp[j], 0, 0, 0);
                 }
             }
@@ -963,8 +967,8 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
             const bf16x8 sf = pack_acc(ds[0], ds[1]);
 #pragma unroll
             for (int db = 0; db < 4; ++db) {
-                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sO, 32 * qc, 16 * db), pf, dv[db], 0, 0, 0);
-                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sQ, 32 * qc, 16 * db), sf, dk[db], 0, 0, 0);
+                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sO, 32 * qc, 16 * db), pf, dv[db], 0, 0, 0);
+                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sQ, 32 * qc, 16 * db), sf, dk[db], 0, 0, 0);
             }
         }
         // query chunks past S: their dS^T columns read as zeros in phase 2
@@ -1003,7 +1007,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
             const int q0 = 16 * c + 4 * g;             // block c = (qc, j) = (c / 2, c % 2)
             char* img = q0 < 64 ? sT0 : sT1;
             const int qq = q0 & 63;
-            *reinterpret_cast<uint2*>(img + lds_off<false>(myk, qq >> 3) + (qq & 7) * 2) = dsk[c];
+            *reinterpret_cast<uint2*>(img + lds_off<true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[c];
         }
     }
     __syncthreads();
@@ -1020,10 +1024,10 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
             if (!FULL && st >= nkc) break;
-            const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
+            const bf16x8 sf = frag_tr<true>(img, 32 * st, cb);
 #pragma unroll
             for (int db = 0; db < 4; ++db)
-                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
+                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sK, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
         }
         if (myq < S) {
             bf16_t* dqr = dqkv + ((long)b * S + myq) * rs + h * D;
@@ -1273,9 +1277,9 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
         const uint4 q4 = *reinterpret_cast<const uint4*>(qb + (long)rr * rs + c * 8);
         const uint4 k4 = *reinterpret_cast<const uint4*>(kb + (long)rr * rs + c * 8);
         const uint4 o4 = *reinterpret_cast<const uint4*>(dob + (long)rr * ors + c * 8);
-        *reinterpret_cast<uint4*>(sQ + lds_off<false>(r, c)) = zero_unless(ok, q4);
-        *reinterpret_cast<uint4*>(sK + lds_off<false>(r, c)) = zero_unless(ok, k4);
-        *reinterpret_cast<uint4*>(sO + lds_off<false>(r, c)) = zero_unless(ok, o4);
+        *reinterpret_cast<uint4*>(sQ + lds_off<true>(r, c)) = zero_unless(ok, q4);
+        *reinterpret_cast<uint4*>(sK + lds_off<true>(r, c)) = zero_unless(ok, k4);
+        *reinterpret_cast<uint4*>(sO + lds_off<true>(r, c)) = zero_unless(ok, o4);
     }
     {
         // delta[q] = sum_d dO[q][d] O[q][d]: 4 threads per query, 16 d each
@@ -1318,7 +1322,7 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
     if (w < nblk) {                 // uniform per wave
         bf16x8 kf[2];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) kf[kk] = frag_rows<false>(sK, 16 * w, kk);
+        for (int kk = 0; kk < 2; ++kk) kf[kk] = frag_rows<true>(sK, 16 * w, kk);
         const float mb2 = s_mask[kok ? myk : 0];
         const int kq = kok ? myk : 0;
         const uint32_t* dmw = s_dm + (DROP ? (kq >> 7) * 4 * FM + ((kq >> 2) & 3) * FM : 0);
@@ -1336,9 +1340,9 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
                     dp[j] = (f32x4){0, 0, 0, 0};
 #pragma unroll
                     for (int kk = 0; kk < 2; ++kk) {
-                        sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sQ, 32 * qc + 16 * j, kk),
+                        sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sQ, 32 * qc + 16 * j, kk),
                                                                         kf[kk], sc[j], 0, 0, 0);
-                        dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sO, 32 * qc + 16 * j, kk),
+                        dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sO, 32 * qc + 16 * j, kk),
                                                                         vf[kk], dp[j], 0, 0, 0);
                     }
                 }
@@ -1369,9 +1373,9 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
                 const bf16x8 sf = pack_acc(ds[0], ds[1]);
 #pragma unroll
                 for (int db = 0; db < 4; ++db) {
-                    dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sO, 32 * qc, 16 * db), pf, dv[db],
+                    dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sO, 32 * qc, 16 * db), pf, dv[db],
                                                                      0, 0, 0);
-                    dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sQ, 32 * qc, 16 * db), sf, dk[db],
+                    dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sQ, 32 * qc, 16 * db), sf, dk[db],
                                                                      0, 0, 0);
                 }
             }
@@ -1414,7 +1418,7 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
             const int q0 = 16 * c + 4 * g;
             char* img = q0 < 64 ? sT0 : sT1;
             const int qq = q0 & 63;
-            *reinterpret_cast<uint2*>(img + lds_off<false>(myk, qq >> 3) + (qq & 7) * 2) = dsk[8 * half + c];
+            *reinterpret_cast<uint2*>(img + lds_off<true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[8 * half + c];
         }
         __syncthreads();
         const int qblk = 8 * half + qsub;
@@ -1428,10 +1432,10 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
 #pragma unroll
             for (int st = 0; st < 8; ++st) {
                 if (st < nch) {
-                    const bf16x8 sf = frag_tr<false>(img, 32 * st, cb);
+                    const bf16x8 sf = frag_tr<true>(img, 32 * st, cb);
 #pragma unroll
                     for (int i = 0; i < 2; ++i)
-                        dq[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<false>(sK, 32 * st, 32 * dh + 16 * i),
+                        dq[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sK, 32 * st, 32 * dh + 16 * i),
                                                                         sf, dq[i], 0, 0, 0);
                 }
             }
