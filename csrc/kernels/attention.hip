@@ -367,9 +367,10 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
                                                       int S, int H, float scale, float p_drop,
                                                       const uint32_t* __restrict__ dmask,
                                                       float* __restrict__ colsum) {
-    // Q, dO tiles as row images (S, dP fragments) and transposed-read images (dK, dV fragments):
-    // the tr reads on a row image were 23 % bank-conflicted
-    __shared__ __attribute__((aligned(16))) char smem[4 * TQ * ROWB];
+    // Q, dO tiles as ONE image each on the transposed-read swizzle, read both as rows (S, dP
+    // fragments) and transposed (dK, dV fragments) without bank conflicts (the row swizzle had
+    // 23 % conflicted tr reads; a second, transposed copy of each tile doubled the staging)
+    __shared__ __attribute__((aligned(16))) char smem[2 * TQ * ROWB];
     __shared__ float s_lse[TQ], s_delta[TQ];
     __shared__ __attribute__((aligned(16))) uint32_t s_dm[4 * TQ];      // this tile's keep words [g][q]
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -404,8 +405,6 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
     for (int i = 0; i < 4; ++i) { dv[i] = (f32x4){0, 0, 0, 0}; dk[i] = (f32x4){0, 0, 0, 0}; }
     char* sQ = smem;
     char* sO = smem + TQ * ROWB;
-    char* sQt = smem + 2 * TQ * ROWB;
-    char* sOt = smem + 3 * TQ * ROWB;
     const int nt = (S + TQ - 1) / TQ;
     // tile t+1's Q / dO rows, keep words, LSE and delta are loaded into registers while tile t
     // computes (the single-buffered loop waited out every tile's loads)
@@ -426,10 +425,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
     fetch(0);
     for (int t = 0; t < nt; ++t) {
         __syncthreads();             // previous tile fully consumed
-        a.store<false>(sQ);
-        c.store<false>(sO);
-        a.store<true>(sQt);
-        c.store<true>(sOt);
+        a.store<true>(sQ);
+        c.store<true>(sO);
         if (p_drop > 0.f) s_dm[threadIdx.x] = wd;
         if (threadIdx.x < TQ) {
             s_lse[threadIdx.x] = nlse;
@@ -445,8 +442,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
             dp[qbk] = (f32x4){0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                sc[qbk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sQ, 16 * qbk, kk), kf[kk], sc[qbk], 0, 0, 0);
-                dp[qbk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sO, 16 * qbk, kk), vf[kk], dp[qbk], 0, 0, 0);
+                sc[qbk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sQ, 16 * qbk, kk), kf[kk], sc[qbk], 0, 0, 0);
+                dp[qbk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sO, 16 * qbk, kk), vf[kk], dp[qbk], 0, 0, 0);
             }
         }
         f32x4 pd[4], ds[4];
@@ -478,8 +475,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
             const bf16x8 sf = pack_acc(ds[2 * st], ds[2 * st + 1]);
 #pragma unroll
             for (int db = 0; db < 4; ++db) {
-                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sOt, 32 * st, 16 * db), pf, dv[db], 0, 0, 0);
-                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sQt, 32 * st, 16 * db), sf, dk[db], 0, 0, 0);
+                dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sO, 32 * st, 16 * db), pf, dv[db], 0, 0, 0);
+                dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sQ, 32 * st, 16 * db), sf, dk[db], 0, 0, 0);
             }
         }
     }
@@ -523,7 +520,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
                                                      int S, int H, float scale, float p_drop,
                                                      const uint32_t* __restrict__ dmask,
                                                      float* __restrict__ colsum) {
-    __shared__ __attribute__((aligned(16))) char smem[3 * TK * ROWB];   // K, V tiles + K as a tr-read image
+    __shared__ __attribute__((aligned(16))) char smem[2 * TK * ROWB];   // K (tr swizzle: read both ways), V tiles
     __shared__ __attribute__((aligned(16))) float s_mk[TK];            // the tile's additive key mask (log2)
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
@@ -559,7 +556,6 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
     for (int i = 0; i < 4; ++i) dq[i] = (f32x4){0, 0, 0, 0};
     char* sK = smem;
     char* sV = smem + TK * ROWB;
-    char* sKt = smem + 2 * TK * ROWB;
     const int nt = (S + TK - 1) / TK;
     // tile t+1's K / V rows (and key mask) are loaded into registers while tile t computes
     Stager a, c;
@@ -575,9 +571,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
     load_mk(0);
     for (int t = 0; t < nt; ++t) {
         __syncthreads();
-        a.store<false>(sK);
+        a.store<true>(sK);
         c.store<false>(sV);
-        a.store<true>(sKt);
         if (mrow && threadIdx.x < TK) s_mk[threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
         __syncthreads();
         if (t + 1 < nt) {
@@ -593,7 +588,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
             dp[blk] = (f32x4){0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
-                sc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sK, 16 * blk, kk), qf[kk], sc[blk], 0, 0, 0);
+                sc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<true>(sK, 16 * blk, kk), qf[kk], sc[blk], 0, 0, 0);
                 dp[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<false>(sV, 16 * blk, kk), of[kk], dp[blk], 0, 0, 0);
             }
         }
@@ -628,7 +623,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
             const bf16x8 sf = pack_acc(ds[2 * st], ds[2 * st + 1]);
 #pragma unroll
             for (int db = 0; db < 4; ++db)
-                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sKt, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
+                dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sK, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
         }
     }
     if (colsum) {
