@@ -240,12 +240,26 @@ def set_wgrad_stream(enabled: bool) -> None:
     _WGRAD_STREAM = bool(enabled)
 
 
+def fork_event():
+    """The point of the compute stream a side-stream wgrad may start from: recorded BEFORE the
+    layer's dgrad is launched (its operands -- the incoming gradient and the saved input --
+    are ready there), so the two GEMMs run concurrently.  Ordered after the dgrad instead
+    (``side_stream`` without ``after``), the side stream waited the dgrad out and the "overlap"
+    was a serialisation plus two stream hops per layer.  None when the side stream is off."""
+    if not _WGRAD_STREAM or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+        return None
+    ev = torch.cuda.Event()
+    ev.record()
+    return ev
+
+
 @_contextlib.contextmanager
-def side_stream(*tensors: torch.Tensor):
+def side_stream(*tensors: torch.Tensor, after=None):
     """Run the block on this device's side stream (when enabled and not capturing), then
-    make the compute stream wait for it.  ``tensors`` are the block's inputs allocated on
-    the compute stream: recorded on the side stream so the caching allocator does not
-    hand their memory out again before the side stream is done with it."""
+    make the compute stream wait for it.  ``after``: the ``fork_event`` the side stream starts
+    from (default: everything the compute stream issued so far).  ``tensors`` are the block's
+    inputs allocated on the compute stream: recorded on the side stream so the caching
+    allocator does not hand their memory out again before the side stream is done with it."""
     if not _WGRAD_STREAM or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
         yield
         return
@@ -254,7 +268,10 @@ def side_stream(*tensors: torch.Tensor):
     s = _side.get(dev)
     if s is None:
         s = _side[dev] = torch.cuda.Stream(device=dev)
-    s.wait_stream(compute)
+    if after is not None:
+        s.wait_event(after)
+    else:
+        s.wait_stream(compute)
     with torch.cuda.stream(s):
         yield
     for t in tensors:

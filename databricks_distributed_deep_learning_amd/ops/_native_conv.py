@@ -456,6 +456,7 @@ class _Conv(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
         dx = dw = None
+        fork = _lib.fork_event() if ctx.needs_input_grad[1] else None   # wgrad may start here
         if ctx.needs_input_grad[0]:
             res = ctx.bridge.take() if ctx.bridge is not None else None
             if res is not None:
@@ -468,7 +469,7 @@ class _Conv(torch.autograd.Function):
             sink = grad_sink(ctx.w_param)
             # concurrent with the dgrad just issued (DDL_WGRAD_STREAM, _lib.side_stream)
             if sink is not None and sink.shape == w.shape:
-                with _lib.side_stream(dy, x):
+                with _lib.side_stream(dy, x, after=fork):
                     _wgrad(dy, x, w.shape, ctx.stride, ctx.pad, out=sink)
                 grad_ready(ctx.w_param)
             else:

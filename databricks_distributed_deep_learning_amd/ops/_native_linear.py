@@ -147,6 +147,9 @@ class _Linear(torch.autograd.Function):
             dz = dy2 * (saved > 0)
         else:
             dz = dy2
+        # DDL_WGRAD_STREAM: the wgrad below starts from HERE on the side stream, concurrent
+        # with the dgrad (whose grid leaves CUs idle at N = 768: 192 tiles on 256 CUs)
+        fork = _lib.fork_event() if ctx.needs_input_grad[1] else None
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
@@ -186,7 +189,7 @@ class _Linear(torch.autograd.Function):
             if sink is None:
                 dw = torch.empty(N, K, dtype=w.dtype, device=w.device)
             # concurrent with the dgrad just issued (DDL_WGRAD_STREAM, _lib.side_stream)
-            with _lib.side_stream(dz, x2):
+            with _lib.side_stream(dz, x2, after=fork):
                 if sink is not None:       # accumulate straight into the reducer's gradient arena
                     gemm(MODE_TN, dz, N, x2, K, sink, K, N, K, M, accumulate=True)
                 else:
