@@ -101,8 +101,46 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
     return max(1, min(2 * NUM_CU // tiles, nk // 8))
 
 
+_HYBRID = os.environ.get("DDL_GEMM_HYBRID", "1") != "0"   # tuner candidate (A/B: 0 = never)
+
+
+def hybrid_rows(M: int, N: int, K: int):
+    """Row split of a 256x256-tile GEMM whose tile grid ends in a partial round, or None.
+
+    ViT-B/16's N = 768 GEMMs (M = 25216 tokens) have 99 x 3 = 297 tiles: the persistent grid
+    runs 256 of them, then 41 CUs run a second tile each while 215 idle -- two full rounds for
+    1.16 rounds of work.  The rows are split instead: rows [0, M1) -- whole rounds of tiles --
+    run unsplit, and the remaining rows run split-K over the whole chip (their fp32 partials
+    reduced with the epilogue), so the tail takes 1/s of a round plus the reduction.  Returns
+    (M1, largest useful split); the tuner times the splits against the plain launch."""
+    tn = -(-N // 256)
+    tm = -(-M // 256)
+    tiles = tm * tn
+    if tiles <= NUM_CU or K % BK:
+        return None
+    tm1 = (tiles // NUM_CU) * NUM_CU // tn
+    rem = (tm - tm1) * tn
+    smax = min(NUM_CU // max(rem, 1), -(-K // BK) // 4)
+    if tm1 <= 0 or rem <= 0 or smax < 2:
+        return None
+    return tm1 * 256, smax
+
+
+def _at(t, off: int):
+    """A one-element view of ``t`` starting ``off`` elements further (only its pointer is used)."""
+    return None if t is None else t.as_strided((1,), (1,), t.storage_offset() + off)
+
+
 def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr,
             row_remap, residual, accumulate, colstats=None, bnb=None) -> None:
+    if kind == "hybrid":
+        # rows [0, M1): whole rounds of unsplit tiles; rows [M1, M): split-K s over the chip
+        M1 = hybrid_rows(M, N, K)[0]
+        _launch("big", 1, mode, A, lda, B, ldb, C, ldc, M1, N, K, bias, act, aux, conv_arr, False, residual,
+                accumulate)
+        _launch("big", s, mode, _at(A, M1 * lda), lda, B, ldb, _at(C, M1 * ldc), ldc, M - M1, N, K, bias, act,
+                _at(aux, M1 * ldc), conv_arr, False, _at(residual, M1 * ldc), accumulate)
+        return
     if kind.startswith("t"):
         # weight-gradient GEMMs computed transposed (operands swapped, C^T stored): a
         # 64-wide output-channel side lands on the tile's N extent (128x64 tiles)
@@ -150,6 +188,10 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
     if mode in (MODE_TN, MODE_CONVW) and plain and (M <= 192 or M % 128 == 64):
         ts = pick_splits(N, 2 * M, K)     # transposed: N' = M (output channels) on 64-wide tiles
         out += [("tnarrow", s) for s in sorted({1, max(1, ts // 2), ts})]
+    if _HYBRID and mode in (MODE_NT, MODE_NN) and not row_remap and _big_allowed(mode, K, lda, ldb):
+        hy = hybrid_rows(M, N, K)
+        if hy is not None:                # a partial last round of 256x256 tiles
+            out += [("hybrid", s) for s in sorted({2, max(2, hy[1] // 2), hy[1]})]
     return out
 
 
@@ -306,7 +348,13 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
     if kernel is not None:
         if kernel == "big" and not _big_allowed(mode, K, lda, ldb):
             kernel = "small"              # no 256x256 variant for these
-        if kernel == "big":
+        hy = hybrid_rows(M, N, K) if kernel == "hybrid" and mode in (MODE_NT, MODE_NN) and not row_remap \
+            and colstats is None and _big_allowed(mode, K, lda, ldb) else None
+        if kernel == "hybrid":
+            kernel = "big" if hy is None else kernel     # no partial round: the plain launch
+        if hy is not None:
+            choice = ("hybrid", max(2, splits or hy[1]))
+        elif kernel == "big":
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
         elif kernel == "narrow":
             choice = ("narrow", 1 if row_remap else pick_splits(M, 2 * N, K, splits))
@@ -356,7 +404,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          residual: Optional[torch.Tensor] = None, accumulate: bool = False,
          kernel: Optional[str] = None, colstats: Optional[torch.Tensor] = None, bnb=None):
     """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
-    "narrow" (128x64) or "tnarrow" (weight gradient computed transposed on 128x64 tiles).
+    "narrow" (128x64), "tnarrow" (weight gradient computed transposed on 128x64 tiles) or
+    "hybrid" (256x256 tiles, the rows past the last whole round split-K: ``hybrid_rows``).
 
     ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm
     statistics partials of the bf16 output; the function then returns the number of

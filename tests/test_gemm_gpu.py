@@ -433,3 +433,51 @@ def test_layernorm_sinks_linear_bias_gradient(second_consumer):
     dp.finish()
     assert getattr(mod.lin.bias, "_ddl_sunk", None) is None
     assert _rel_err(mod.lin.bias.grad, want) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(25216, 768, 768), (16384, 2304, 768), (23000, 768, 1536)])
+@pytest.mark.parametrize("epi", ["plain", "bias_res", "gelu", "dgelu"])
+def test_hybrid_row_split_gemm(M, N, K, epi):
+    """256x256-tile GEMMs whose grid ends in a partial round (ViT: 297 tiles on 256 CUs) run
+    their last rows split-K (kernel "hybrid", _native_gemm.hybrid_rows): same result as the
+    single launch, with the bias / residual / GELU (+ pre-activation) / dGELU epilogues applied
+    to both row ranges (the split part's by the reduce kernel)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    hy = NG.hybrid_rows(M, N, K)
+    assert hy is not None and 0 < hy[0] < M
+    torch.manual_seed(11)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    pre = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    for mode in (NG.MODE_NT, NG.MODE_NN):
+        wop = w if mode == NG.MODE_NT else w.t().contiguous()     # NN: B[k][n]
+        ldb = K if mode == NG.MODE_NT else N
+        ref = a.float() @ w.float().t()
+        outs = {}
+        for kern in ("big", "hybrid"):
+            c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            kw = {}
+            if epi == "bias_res":
+                kw = dict(bias=b, residual=res)
+            elif epi == "gelu":
+                kw = dict(bias=b, act="gelu", aux=torch.empty_like(c))
+            elif epi == "dgelu":
+                kw = dict(act="dgelu", aux=pre)
+            NG.gemm(mode, a, K, wop, ldb, c, N, M, N, K, kernel=kern, **kw)
+            outs[kern] = (c, kw.get("aux"))
+        if epi == "plain":
+            exp = ref
+        elif epi == "bias_res":
+            exp = ref + b.float() + res.float()
+        elif epi == "gelu":
+            exp = torch.nn.functional.gelu(ref + b.float())
+            assert _rel_err(outs["hybrid"][1], ref + b.float()) < 1e-2
+        else:
+            z = pre.float()
+            cdf = 0.5 * (1 + torch.erf(z / 2 ** 0.5))
+            exp = ref * (cdf + z * torch.exp(-0.5 * z * z) / (2 * torch.pi) ** 0.5)
+        assert _rel_err(outs["hybrid"][0], exp) < 1e-2
+        assert _rel_err(outs["hybrid"][0], outs["big"][0].float()) < 1e-2
