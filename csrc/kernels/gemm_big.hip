@@ -461,7 +461,15 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
 // With colstats (EK_BF16 / EK_GEN) the BatchNorm statistics of the bf16 output --
 // what BN will read -- are summed per lane over its 8 rows, then over the 16
 // lanes holding the same columns; one partial row per (tile, wave row).
-template <int EK>
+// Column of an accumulator block: quadrant qn, 16-column block j of wave column wn.  A 192-wide
+// N tile (N192) keeps quadrant 0 as is (128 columns, 32 per wave) and gives each wave ONE 16-column
+// block of quadrant 1 (64 columns): acc[.][1][.][1] is not used.
+template <bool N192>
+__device__ __forceinline__ int col_base(int n0, int qn, int wn, int j) {
+    return n0 + qn * 128 + ((N192 && qn) ? wn * 16 : wn * 32 + j * 16);
+}
+
+template <int EK, bool N192 = false>
 __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
                                            int wm, int wn, int lane, int split) {
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
@@ -476,14 +484,16 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
         for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                bpre[qn][j] = *reinterpret_cast<const uint2*>((const bf16_t*)p.bias + n0 + qn * 128 + wn * 32 +
-                                                              j * 16 + g4);
+                bpre[qn][j] = (N192 && qn && j) ? make_uint2(0u, 0u)
+                                                : *reinterpret_cast<const uint2*>((const bf16_t*)p.bias +
+                                                                                  col_base<N192>(n0, qn, wn, j) + g4);
     }
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int n = n0 + qn * 128 + wn * 32 + j * 16 + g4;
+            if (N192 && qn && j) continue;
+            const int n = col_base<N192>(n0, qn, wn, j) + g4;
             float bv[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
             if ((EK == EK_BF16 || EK == EK_GELU) && p.bias) {
                 const uint2 b2 = bpre[qn][j];
@@ -561,7 +571,7 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
             // consecutive columns of one row (half the store instructions; 8-byte stores kept
             // the epilogue store-issue bound).  Row-block i values wait in (plo, phi) / (zlo, zhi).
             uint32_t plo = 0, phi = 0, zlo = 0, zhi = 0;
-            const int wcol = n0 + qn * 128 + wn * 32 + j * 16 + (lane >> 5) * 8;   // (g >> 1) * 8
+            const int wcol = col_base<N192>(n0, qn, wn, j) + (lane >> 5) * 8;   // (g >> 1) * 8
             auto store_pair = [&](void* base, uint32_t lo0, uint32_t hi0, uint32_t lo1, uint32_t hi1, int m1) {
                 const auto x = __builtin_amdgcn_permlane16_swap(lo0, lo1, false, false);
                 const auto y = __builtin_amdgcn_permlane16_swap(hi0, hi1, false, false);
@@ -680,8 +690,16 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
 // Its 64-bit per-site addresses are what spills (35-72 VGPRs of scratch in the persistent
 // kernels); without it the NT kernel allocates spill-free -- but runs slower (see
 // edge_split_enabled), so the spills are not on the interior tiles' critical path.
-template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false, bool EDGE = true>
+// N192: 256 x 192 tiles (register epilogue only): BERT's N = 768 / 2304 GEMMs have 192 / 576
+// tiles of 256 x 256 on 256 CUs (one 75 %-full round / 2.25 rounds); 192-wide tiles make that
+// 256 / 768 -- whole rounds.  The B operand is still staged as two 128-row halves (the rows
+// past the tile's 192 are read but never multiplied: the weight panel is L2-resident), so the
+// 8-phase schedule and its DMA counts are unchanged; quadrant qn = 1 runs one 16-column block
+// per wave (8 MFMAs instead of 16 per phase).
+template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false, bool EDGE = true, bool N192 = false>
 __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
+    static_assert(!N192 || (DIRECT && !BNB), "192-wide tiles: register epilogue only");
+    constexpr int TBN = N192 ? 192 : TB;
     // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
     // makes the compiler's LDS-DMA alias tracking wait vmcnt(0) before fragment reads)
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF + 16];
@@ -702,7 +720,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         tm = first_m + wl % gsz;
         tn = wl / gsz;
         m0 = tm * TB;
-        n0 = tn * TB;
+        n0 = tn * TBN;
     };
     // Tile order.  Static: block b walks tiles b, b + gridDim.x, ... (same XCD range).
     // Dynamic (p.sched, gridDim.x % 8 == 0): the first tile is static, every further one
@@ -764,9 +782,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     auto readB = [&](int buf, int qn, bf16x8 (&fb)[2][2]) {
         const char* hb = smem + half_off(buf, 1, qn);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j) {
+            if (N192 && qn && j) continue;
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag<LB>(hb, wn * 32 + j * 16, kk);
+            for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag<LB>(hb, (N192 && qn) ? wn * 16 : wn * 32 + j * 16, kk);
+        }
     };
     auto mma = [&](int qm, int qn, bf16x8 (&fb)[2][2]) {
         __builtin_amdgcn_s_setprio(1);
@@ -776,7 +796,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[qm][qn][i][j] =
+                    if (!(N192 && qn && j)) acc[qm][qn][i][j] =
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[qm][qn][i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
@@ -901,7 +921,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                                              : vt + (int)gridDim.x;
             const bool next = vn < nwg;
             const int m0c = m0, n0c = n0, tm_c = tm;
-            const bool interior = !EDGE || (m0c + TB <= p.M && n0c + TB <= p.N);
+            const bool interior = !EDGE || (m0c + TB <= p.M && n0c + TBN <= p.N);
             // Store-behind: when this tile's epilogue issues a KNOWN number of vector-memory
             // ops (lean bf16 variant: one 8-byte store per site, +8 statistics stores), the
             // WHOLE next prologue (E and O halves) is issued first and only the E loads are
@@ -911,7 +931,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // load -> compute -> store-drain per tile.
             // (a residual's loads retire in order behind the next prologue's, so the counts
             // below stay upper bounds)
-            const bool behind = next && nK > 0 && interior &&
+            // (not with 192-wide tiles: the store counts its vmcnt waits assume are the 256-wide ones)
+            const bool behind = !N192 && next && nK > 0 && interior &&
                 ((p.ek == EK_BF16 && (!p.bias || (p.behind_mask & BEHIND_BIAS)) &&
                   (!p.res || (p.behind_mask & BEHIND_RES))) ||
                  (p.ek == EK_GELU && (p.behind_mask & BEHIND_GELU)));
@@ -933,15 +954,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             if (BNB)   // checked on every tile: a lean interior twin spills (measured slower)
                 epi_direct<EK_BNBC>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_BF16)
-                epi_direct<EK_BF16>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_BF16, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_F32)
-                epi_direct<EK_F32>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_F32, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_GELU)
-                epi_direct<EK_GELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_GELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_DGELU)
-                epi_direct<EK_DGELU>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_DGELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if constexpr (EDGE)
-                epi_direct<EK_GEN>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_GEN, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             if (!next) {
                 if constexpr (DYN) break;    // the ticket slot's exit bookkeeping below the loop
                 return;
@@ -1206,10 +1227,11 @@ int behind_mask() {
 }
 
 template <int LA, int LB>
-int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st) {
+int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st, bool n192 = false) {
     p.behind_mask = behind_mask();
+    const int tbn = n192 ? 192 : TB;
     p.tiles_m = (p.M + TB - 1) / TB;
-    p.tiles_n = (p.N + TB - 1) / TB;
+    p.tiles_n = (p.N + tbn - 1) / tbn;
     const int nk = (p.K + BK - 1) / BK;
     if (splits < 1) splits = 1;
     if (splits > nk) splits = nk > 0 ? nk : 1;
@@ -1265,6 +1287,14 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
             }
         }
         if (p.act == ACT_BNB) return -8;
+        if (n192) {
+            if constexpr (LA == KC && (LB == KC || LB == KO)) {   // Linear fwd / dgrad operand layouts
+                if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, true, false, true, true>), grid, dim3(NTH), 0, st, kp);
+                else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true, false, true, true>), grid, dim3(NTH), 0, st, kp);
+            } else {
+                return -9;
+            }
+        } else {
         // all tiles interior with a lean epilogue kind: the variant without the general epilogue
         const bool lean = p.M % TB == 0 && p.N % TB == 0 && p.ek != EK_GEN && edge_split_enabled();
         if (lean) {
@@ -1275,7 +1305,9 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
         } else {
             hipLaunchKernelGGL((gemm_big_k<LA, LB, false, true>), grid, dim3(NTH), 0, st, kp);
         }
+        }
     } else {
+        if (n192) return -9;    // 192-wide tiles: register epilogue only
         if (ktail) hipLaunchKernelGGL((gemm_big_k<LA, LB, true, false>), grid, dim3(NTH), 0, st, kp);
         else hipLaunchKernelGGL((gemm_big_k<LA, LB, false, false>), grid, dim3(NTH), 0, st, kp);
     }
@@ -1290,7 +1322,7 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
 }  // namespace
 
 // mode: 0 = A KC, B KC (NT)   1 = A KC, B KO (NN)   2 = A KO, B KO (TN)
-//       3 = A CONV, B KC      4 = A KO, B CONVW
+//       3 = A CONV, B KC      4 = A KO, B CONVW      | 32: 256 x 192 tiles (modes 0 / 1)
 // Requirements: K % 8 == 0, leading dims % 8 == 0 (16-B chunks), zero points at >= 16 zero bytes.
 DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, const void* bias, int bias_bf16, int act, void* aux, int out_f32, int splits,
@@ -1316,9 +1348,13 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
         return -6;
     }
     if (conv) fill_conv(p.cd, conv);
+    // mode flag 32: 256 x 192 tiles (N192 in gemm_big_k; NT / NN, register epilogue, no BN backward)
+    const bool n192 = (mode & 32) != 0;
+    mode &= ~32;
+    if (n192 && (act == ACT_BNB || (mode != 0 && mode != 1))) return -9;
     switch (mode) {
-        case 0: return launch_big<KC, KC>(p, workspace, ws_elems, splits, st);
-        case 1: return launch_big<KC, KO>(p, workspace, ws_elems, splits, st);
+        case 0: return launch_big<KC, KC>(p, workspace, ws_elems, splits, st, n192);
+        case 1: return launch_big<KC, KO>(p, workspace, ws_elems, splits, st, n192);
         case 2: return launch_big<KO, KO>(p, workspace, ws_elems, splits, st);
         case 3: return launch_big<CONV, KC>(p, workspace, ws_elems, splits, st);
         default: return -1;   // conv wgrad (CONVW) stays on the 128x128 kernel (gemm.hip)

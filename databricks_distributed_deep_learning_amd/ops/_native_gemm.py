@@ -20,6 +20,7 @@ _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
 MODE_CONVW_A = 5      # conv wgrad with the im2col operand on the M side (computes dW^T)
 TRANS_OUT = 16        # flag: the kernel stores C^T
+N192 = 32             # flag (256x256 kernel): 256 x 192 tiles
 ACT = {None: 0, "gelu": 1, "relu": 2, "tanh": 3, "dgelu": 4, "bnb": 5}
 BM = BN = 128
 BK = 64
@@ -102,6 +103,8 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
 
 
 _HYBRID = os.environ.get("DDL_GEMM_HYBRID", "1") != "0"   # tuner candidate (A/B: 0 = never)
+_BIG192 = os.environ.get("DDL_GEMM_192", "1") != "0"       # tuner candidate "big192" (A/B: 0 = never)
+_DIRECT = os.environ.get("DDL_GEMM_DIRECT", "1") != "0"    # gemm_big.hip register epilogue (big192 needs it)
 
 
 def hybrid_rows(M: int, N: int, K: int):
@@ -157,7 +160,9 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
     cs = _lib.p(colstats)
     if bnb is not None:   # ACT_BNB side arguments (mask, mean, invstd), consumed by this launch
         _lib.fn("ddl_gemm_bnb")(_lib.p(bnb[0]), _lib.p(bnb[1]), _lib.p(bnb[2]))
-    if kind == "big":
+    if kind in ("big", "big192"):
+        if kind == "big192":
+            args = (mode | N192,) + args[1:]
         rc = _lib.fn("ddl_gemm_big2")(*args, _zero_page(C.device).data_ptr(), cs, _lib.stream())
     elif kind == "narrow":
         rc = _lib.fn("ddl_gemm_n64")(*args, cs, _lib.stream())
@@ -188,6 +193,11 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
     if mode in (MODE_TN, MODE_CONVW) and plain and (M <= 192 or M % 128 == 64):
         ts = pick_splits(N, 2 * M, K)     # transposed: N' = M (output channels) on 64-wide tiles
         out += [("tnarrow", s) for s in sorted({1, max(1, ts // 2), ts})]
+    if mode in (MODE_NT, MODE_NN) and not row_remap and _big_allowed(mode, K, lda, ldb) and N % 192 == 0 \
+            and _DIRECT:
+        # 256 x 192 tiles: whole rounds where 256-wide ones leave a partial one (N = 768: 192 -> 256 tiles
+        # at M = 16384); register epilogue only (the caller drops it for the BatchNorm-backward epilogue)
+        out += [("big192", 1)] if _BIG192 else []
     if _HYBRID and mode in (MODE_NT, MODE_NN) and not row_remap and _big_allowed(mode, K, lda, ldb):
         hy = hybrid_rows(M, N, K)
         if hy is not None:                # a partial last round of 256x256 tiles
@@ -299,6 +309,8 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
           colstats=None, bnb=None):
     plain = bias is None and act is None and residual is None and aux is None and not row_remap
     cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain)
+    if act not in (None, "relu", "gelu", "dgelu") or (act == "dgelu" and aux is None):
+        cands = [c for c in cands if c[0] != "big192"]     # LDS-staged epilogue: 256-wide tiles only
     cs_s = None
     if colstats is not None:   # statistics epilogue: whole-K tiles only
         cands = [c for c in cands if c[1] == 1 and not c[0].startswith("t")]
@@ -345,6 +357,10 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
             kernel, colstats, bnb=None):
     """(kernel kind, splits) for one GEMM call: forced, explicit, tuned (cached) or heuristic."""
     kernel = kernel or _forced
+    if kernel == "big192" and not (mode in (MODE_NT, MODE_NN) and not row_remap and _DIRECT and
+                                   _big_allowed(mode, K, lda, ldb) and act in (None, "relu", "gelu", "dgelu")
+                                   and not (act == "dgelu" and aux is None)):
+        kernel = "big"                    # 192-wide tiles: NT / NN with a register epilogue only
     if kernel is not None:
         if kernel == "big" and not _big_allowed(mode, K, lda, ldb):
             kernel = "small"              # no 256x256 variant for these
@@ -352,7 +368,9 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
             and colstats is None and _big_allowed(mode, K, lda, ldb) else None
         if kernel == "hybrid":
             kernel = "big" if hy is None else kernel     # no partial round: the plain launch
-        if hy is not None:
+        if kernel == "big192":
+            choice = ("big192", 1)
+        elif hy is not None:
             choice = ("hybrid", max(2, splits or hy[1]))
         elif kernel == "big":
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
@@ -382,7 +400,7 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
     else:
         choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
     if colstats is not None and (choice[1] != 1 or choice[0].startswith("t")):
-        choice = ("big" if choice[0] == "big" else "small", 1)
+        choice = (choice[0] if choice[0] in ("big", "big192") else "small", 1)
     return choice
 
 
@@ -404,7 +422,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          residual: Optional[torch.Tensor] = None, accumulate: bool = False,
          kernel: Optional[str] = None, colstats: Optional[torch.Tensor] = None, bnb=None):
     """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
-    "narrow" (128x64), "tnarrow" (weight gradient computed transposed on 128x64 tiles) or
+    "narrow" (128x64), "tnarrow" (weight gradient computed transposed on 128x64 tiles), "big192"
+    (256x192 tiles of the 256x256 kernel: NT / NN, register epilogue) or
     "hybrid" (256x256 tiles, the rows past the last whole round split-K: ``hybrid_rows``).
 
     ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm
@@ -431,7 +450,7 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
                         residual is not None, colstats is not None, accumulate), choice, e0, e1))
     if colstats is not None:
         # one partial row per 128 output rows (256x256 tiles: one per wave row)
-        return 2 * -(-M // 256) if choice[0] == "big" else -(-M // 128)
+        return 2 * -(-M // 256) if choice[0] in ("big", "big192") else -(-M // 128)
     return C
 
 

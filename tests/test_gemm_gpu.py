@@ -481,3 +481,52 @@ def test_hybrid_row_split_gemm(M, N, K, epi):
             exp = ref * (cdf + z * torch.exp(-0.5 * z * z) / (2 * torch.pi) ** 0.5)
         assert _rel_err(outs["hybrid"][0], exp) < 1e-2
         assert _rel_err(outs["hybrid"][0], outs["big"][0].float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (1000, 576, 200), (4096, 2304, 3072)])
+@pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "relu", "gelu", "dgelu_stats"])
+def test_big192_tiles(M, N, K, epi):
+    """256 x 192 tiles of the 256x256 kernel (kernel "big192": BERT's N = 768 GEMMs become 256
+    tiles instead of 192 on 256 CUs): NT and NN against the fp32 reference for every register
+    epilogue, edge tiles (M % 256, K % 64) included, and the dGELU column sums (bias gradient)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    torch.manual_seed(12)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    pre = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    for mode in (NG.MODE_NT, NG.MODE_NN):
+        wop = w if mode == NG.MODE_NT else w.t().contiguous()
+        ldb = K if mode == NG.MODE_NT else N
+        ref = a.float() @ w.float().t()
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        kw = {}
+        if epi == "bias":
+            kw = dict(bias=b)
+        elif epi == "bias_res":
+            kw = dict(bias=b, residual=res)
+        elif epi == "relu":
+            kw = dict(bias=b, act="relu")
+        elif epi == "gelu":
+            kw = dict(bias=b, act="gelu", aux=torch.empty_like(c))
+        elif epi == "dgelu_stats":
+            kw = dict(act="dgelu", aux=pre, colstats=torch.zeros(NG.stats_rows_max(M) * 2 * N, device=dev))
+        rows = NG.gemm(mode, a, K, wop, ldb, c, N, M, N, K, kernel="big192", **kw)
+        exp = ref
+        if epi in ("bias", "bias_res", "relu", "gelu"):
+            exp = exp + b.float()
+        if epi == "bias_res":
+            exp = exp + res.float()
+        if epi == "relu":
+            exp = exp.clamp_min(0)
+        if epi == "gelu":
+            assert _rel_err(kw["aux"], exp) < 1e-2
+            exp = torch.nn.functional.gelu(exp)
+        if epi == "dgelu_stats":
+            z = pre.float()
+            exp = exp * (0.5 * (1 + torch.erf(z / 2 ** 0.5)) + z * torch.exp(-0.5 * z * z) / (2 * torch.pi) ** 0.5)
+            sums = kw["colstats"].view(-1, 2, N)[:rows, 0].sum(0)
+            assert _rel_err(sums, c.float().sum(0)) < 1e-3
+        assert _rel_err(c, exp) < 1e-2, (mode, epi)
