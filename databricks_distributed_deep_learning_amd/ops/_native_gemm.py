@@ -103,7 +103,11 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
 
 
 _HYBRID = os.environ.get("DDL_GEMM_HYBRID", "1") != "0"   # tuner candidate (A/B: 0 = never)
-_BIG192 = os.environ.get("DDL_GEMM_192", "1") != "0"       # tuner candidate "big192" (A/B: 0 = never)
+# tuner candidate "big192" (256 x 192 tiles), off by default: never the tuner's pick on BERT-base's
+# shapes (same-box A/B neutral, ViT -0.5 %): its quadrant-1 phases run 8 MFMAs per wave instead of 16
+# with the same barrier / fragment-read / DMA-issue cost, so a tile costs about as much as a 256-wide
+# one and the whole-round grid buys nothing.  DDL_GEMM_192=1 offers it (forcing: kernel="big192").
+_BIG192 = os.environ.get("DDL_GEMM_192", "0") == "1"
 _DIRECT = os.environ.get("DDL_GEMM_DIRECT", "1") != "0"    # gemm_big.hip register epilogue (big192 needs it)
 
 
