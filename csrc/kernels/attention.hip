@@ -30,8 +30,14 @@
 namespace {
 
 constexpr int D = 64;          // head dim
-constexpr int TQ = 64;         // queries per workgroup
+constexpr int TQ = 64;         // query rows per staged tile
 constexpr int TK = 64;         // keys per tile
+// waves per workgroup of the tiled (S > 256) kernels, 16 rows each; a staged tile is shared by all
+// of them.  Forward: 8 (each K / V tile staged once per 128 queries: fwd 63 -> 57 us at BERT-large's
+// shape); backward: 4 (at 8 the dK/dV and dQ kernels' 130-160 VGPRs leave one 8-wave workgroup
+// per CU instead of three 4-wave ones, and fwd+bwd went 178 -> 200 us)
+constexpr int TWF = 8, TWB = 4;
+constexpr int TROWS_F = 16 * TWF, TROWS_B = 16 * TWB;
 constexpr int ROWB = 128;      // bytes per LDS row (64 bf16)
 constexpr int FS = 128;        // longest sequence of the one-workgroup-per-(b, h) kernels
 constexpr float LOG2E = 1.4426950408889634f;
@@ -96,19 +102,21 @@ __device__ __forceinline__ uint4 zero_unless(bool ok, uint4 v) {
     return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
 }
 
-// stage a [64 rows][64] bf16 tile (rows >= nrows -> 0) with 256 threads: 2 chunks each.
+// stage a [64 rows][64] bf16 tile (rows >= nrows -> 0) with NT threads: 512 / NT chunks each.
 // load() keeps the RAW loaded chunks and only records which rows are past the end; the zero
 // select happens in store(): a select right after the load made the compiler wait for the
 // load there (s_waitcnt vmcnt(0) straight behind the prefetch), so a tile "prefetched" under
 // the previous tile's compute was in fact waited for before that compute started
+template <int NT = 256>
 struct Stager {
-    uint4 v[2];
-    bool ok[2];
+    static constexpr int PER = 512 / NT;
+    uint4 v[PER];
+    bool ok[PER];
     __device__ __forceinline__ void load(const bf16_t* base, long row_stride, int row0, int nrows) {
         const int t = threadIdx.x;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int r = (t >> 3) + 32 * i, c = t & 7;
+        for (int i = 0; i < PER; ++i) {
+            const int r = (t >> 3) + (NT / 8) * i, c = t & 7;
             ok[i] = row0 + r < nrows;
             v[i] = *reinterpret_cast<const uint4*>(base + (long)(ok[i] ? row0 + r : 0) * row_stride + c * 8);
         }
@@ -117,8 +125,8 @@ struct Stager {
     __device__ __forceinline__ void store(char* lds) {
         const int t = threadIdx.x;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int r = (t >> 3) + 32 * i, c = t & 7;
+        for (int i = 0; i < PER; ++i) {
+            const int r = (t >> 3) + (NT / 8) * i, c = t & 7;
             *reinterpret_cast<uint4*>(lds + lds_off<TR>(r, c)) = zero_unless(ok[i], v[i]);
         }
     }
@@ -183,10 +191,10 @@ __device__ __forceinline__ bf16x8 load_frag_global(const bf16_t* rowp, int kk) {
 }
 
 // ============================================================ forward
-// (256, 3): three waves per SIMD -- the compiler then allocates 144 VGPRs instead of 176 (two
-// waves per SIMD) without spilling; the tiled kernels wait on memory ~45-50 % of wave time,
-// which more resident waves hide (same for the two backward kernels below)
-__global__ __launch_bounds__(256, 3) void attn_fwd_k(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+// 8 waves (128 queries) per workgroup: each K / V tile is staged once for 128 queries (it was
+// once per 64 with 4 waves: half the staging per query); (512, 1) leaves the compiler its
+// register budget, LDS allows two workgroups per CU
+__global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                   bf16_t* __restrict__ out, float* __restrict__ lse, int B, int S, int H,
                                                   float scale, float p_drop, uint64_t seed, uint32_t* __restrict__ dmask) {
     __shared__ __attribute__((aligned(16))) char smem[4 * TK * ROWB];   // K0 V0 K1 V1
@@ -199,7 +207,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_k(const bf16_t* __restrict__ 
     const bf16_t* qb = qkv + (long)b * S * rs + h * D;
     const bf16_t* kb = qb + H * D;
     const bf16_t* vb = qb + 2 * H * D;
-    const int q0 = blockIdx.x * TQ + w * 16;
+    const int q0 = blockIdx.x * TROWS_F + w * 16;
     const int myq = q0 + (lane & 15);
     const bool qok = myq < S;
     // Q fragments (B operand of S^T = K Q^T): lane holds Q[myq][32kk + 8g + 0..7]
@@ -221,7 +229,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_k(const bf16_t* __restrict__ 
 
     const int nt = (S + TK - 1) / TK;
     uint32_t kbits = 0;                                      // dropout keep bits of a 128-key word
-    Stager sk, sv;
+    Stager<64 * TWF> sk, sv;
     float nmk = 0.f;                                         // raw load; scaled / bounded at the store
     bool mk_ok = false;
     auto load_mk = [&](int t) __attribute__((always_inline)) {
@@ -360,8 +368,11 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16_t* __restrict__ d
 }
 
 // ============================================================ backward dK, dV
-// workgroup = 64 keys of one (b, h); wave w owns keys k0 + 16 w .. +15 (key on the lane).
-__global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+// workgroup = 16 TWB keys of one (b, h); wave w owns keys k0 + 16 w .. +15 (key on the lane).
+// (256, 3): three waves per SIMD -- the compiler then allocates ~160 VGPRs instead of 176 (two
+// waves per SIMD) without spilling; the tiled kernels wait on memory ~45-50 % of wave time,
+// which more resident waves hide (same for the dQ kernel below)
+__global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
                                                       int S, int H, float scale, float p_drop,
@@ -380,7 +391,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
     const bf16_t* kb = qb + H * D;
     const bf16_t* vb = qb + 2 * H * D;
     const bf16_t* dob = dout + (long)b * S * H * D + h * D;
-    const int k0 = blockIdx.x * TK + w * 16;
+    const int k0 = blockIdx.x * TROWS_B + w * 16;
     const int myk = k0 + (lane & 15);
     const bool kok = myk < S;
     // K and V rows of my key as B operands (lane: row myk, d = 32kk + 8g + ..)
@@ -395,9 +406,10 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
     const float c2 = scale * LOG2E;
     const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     // my key's keep bits: word (kw, gk) of each query (staged per tile in s_dm), bit kbit; the
-    // workgroup's 64 keys share kw
+    // workgroup's keys share kw
+    static_assert(TROWS_B <= 128 && 128 % TROWS_B == 0, "a workgroup's keys in one 128-key keep word");
     const int kq = kok ? myk : 0;
-    const int kw_blk = (blockIdx.x * TK) >> 7;
+    const int kw_blk = (blockIdx.x * TROWS_B) >> 7;
     const uint32_t* dmw = s_dm + ((kq >> 2) & 3) * TQ;
     const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
     f32x4 dv[4], dk[4];
@@ -408,14 +420,14 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
     const int nt = (S + TQ - 1) / TQ;
     // tile t+1's Q / dO rows, keep words, LSE and delta are loaded into registers while tile t
     // computes (the single-buffered loop waited out every tile's loads)
-    Stager a, c;
+    Stager<64 * TWB> a, c;
     uint32_t wd = 0;
     float nlse = 0.f, ndel = 0.f;
     auto fetch = [&](int t) __attribute__((always_inline)) {
         a.load(qb, rs, t * TQ, S);
         c.load(dob, (long)H * D, t * TQ, S);
         const int q = t * TQ + (threadIdx.x & (TQ - 1));
-        if (p_drop > 0.f)            // keep word (g, q) of the tile, one per thread
+        if (p_drop > 0.f && threadIdx.x < 4 * TQ)   // keep word (g, q) of the tile, one per thread
             wd = q < S ? dmask[dmask_word(bh, S, kw_blk, threadIdx.x >> 6, q)] : 0u;
         if (threadIdx.x < TQ) {
             nlse = q < S ? lse[(long)bh * S + q] : 0.f;
@@ -427,7 +439,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
         __syncthreads();             // previous tile fully consumed
         a.store<true>(sQ);
         c.store<true>(sO);
-        if (p_drop > 0.f) s_dm[threadIdx.x] = wd;
+        if (p_drop > 0.f && threadIdx.x < 4 * TQ) s_dm[threadIdx.x] = wd;
         if (threadIdx.x < TQ) {
             s_lse[threadIdx.x] = nlse;
             s_delta[threadIdx.x] = ndel;
@@ -485,7 +497,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
         // rows, row (b * tiles + tile) * 4 + wave of colsum [B * tiles * 4][3 H D] (keys past S
         // contribute zero).  Per wave, no barrier: a workgroup-wide reduction held every wave
         // until the slowest finished (+10 us per launch at ViT's 6144 workgroups)
-        float* crow = colsum + (((long)b * gridDim.x + blockIdx.x) * 4 + w) * rs + h * D + 4 * g;
+        float* crow = colsum + (((long)b * gridDim.x + blockIdx.x) * TWB + w) * rs + h * D + 4 * g;
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
             float sk[4], sv[4];
@@ -513,8 +525,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkv_k(const bf16_t* __restric
 }
 
 // ============================================================ backward dQ
-// workgroup = 64 queries; wave owns 16 queries (query on the lane), loops over key tiles.
-__global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+// workgroup = 16 TWB queries; wave owns 16 queries (query on the lane), loops over key tiles.
+__global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                      const float* __restrict__ lse, const float* __restrict__ delta,
                                                      const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
                                                      int S, int H, float scale, float p_drop,
@@ -529,7 +541,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
     const bf16_t* kb = qb + H * D;
     const bf16_t* vb = qb + 2 * H * D;
     const bf16_t* dob = dout + (long)b * S * H * D + h * D;
-    const int myq = blockIdx.x * TQ + w * 16 + (lane & 15);
+    const int myq = blockIdx.x * TROWS_B + w * 16 + (lane & 15);
     const bool qok = myq < S;
     bf16x8 qf[2], of[2];
     {
@@ -558,7 +570,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
     char* sV = smem + TK * ROWB;
     const int nt = (S + TK - 1) / TK;
     // tile t+1's K / V rows (and key mask) are loaded into registers while tile t computes
-    Stager a, c;
+    Stager<64 * TWB> a, c;
     float nmk = 0.f;                                         // raw load; scaled / bounded at the store
     bool mk_ok = false;
     auto load_mk = [&](int t) __attribute__((always_inline)) {
@@ -629,7 +641,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_k(const bf16_t* __restrict
     if (colsum) {
         // column sums of this wave's 16 dQ rows (the same colsum row as the dKV kernel's wave
         // over these positions' keys)
-        float* crow = colsum + (((long)b * gridDim.x + blockIdx.x) * 4 + w) * rs + h * D + 4 * g;
+        float* crow = colsum + (((long)b * gridDim.x + blockIdx.x) * TWB + w) * rs + h * D + 4 * g;
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
             float sq[4];
@@ -1531,14 +1543,14 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
 #undef FWD_MED
         DDL_RETURN_LAUNCH();
     }
-    dim3 grid((S + TQ - 1) / TQ, B * H);
-    attn_fwd_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed, dmask);
+    dim3 grid((S + TROWS_F - 1) / TROWS_F, B * H);
+    attn_fwd_k<<<grid, 64 * TWF, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed, dmask);
     DDL_RETURN_LAUNCH();
 }
 
 // dqkv [B, S, 3*H*64] bf16 (fully written); delta scratch [B, H, S] fp32
 // colsum (nullable, [B * 4 ceil(S / 64)][3 H 64] fp32): column sums of dqkv per batch (single-
-// workgroup path: rows 0..B-1, returns 0) or per batch and 16-row group (tiled path: every row,
+// workgroup paths: rows 0..B-1, returns 0) or per batch and 16-row group (tiled path: every row,
 // returns 2) -- the QKV bias gradient is the column sum of the written rows
 DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, const float* mask,
                          float* delta, void* dqkv, int B, int S, int H, float scale, float p_drop,
@@ -1561,11 +1573,10 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     }
     const long rows = (long)B * S * H;
     attn_delta_k<<<(int)((rows * 8 + 255) / 256), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
-    dim3 grid((S + TK - 1) / TK, B * H);
-    static_assert(TQ == TK, "the dKV and dQ tiles share the colsum rows");
-    attn_bwd_dkv_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B,
+    dim3 grid((S + TROWS_B - 1) / TROWS_B, B * H);    // the dKV and dQ workgroups share the colsum rows
+    attn_bwd_dkv_k<<<grid, 64 * TWB, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B,
                                          S, H, scale, p_drop, dmask, colsum);
-    attn_bwd_dq_k<<<grid, 256, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B, S,
+    attn_bwd_dq_k<<<grid, 64 * TWB, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B, S,
                                         H, scale, p_drop, dmask, colsum);
     const int rc = (int)hipGetLastError();
     return rc ? rc : (colsum ? 2 : 0);

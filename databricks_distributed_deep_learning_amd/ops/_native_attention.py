@@ -61,8 +61,10 @@ class _Attention(torch.autograd.Function):
         dout = dout.contiguous()
         delta = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
         dqkv = torch.empty_like(qkv)
-        # QKV bias gradient rows: per batch (single-workgroup kernel) or per batch and 16-row group
-        cs = torch.empty(B * 4 * -(-S // 64), 3 * H * 64, dtype=torch.float32, device=qkv.device) if _COLSUM else None
+        # QKV bias gradient rows: per batch (single-workgroup kernels) or per batch and 16-row group
+        # (tiled backward kernels: 64-row workgroups of 4 waves)
+        tiled_rows = B * 4 * -(-S // 64)
+        cs = torch.empty(tiled_rows, 3 * H * 64, dtype=torch.float32, device=qkv.device) if _COLSUM else None
         rc = _lib.fn("ddl_attn_bwd")(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr(), _lib.p(m),
                                      delta.data_ptr(), dqkv.data_ptr(), B, S, H, scale, p_drop, _lib.p(dmask),
                                      _lib.p(cs), _lib.stream())
@@ -71,7 +73,7 @@ class _Attention(torch.autograd.Function):
         if cs is not None:
             # rides on the gradient: the producing Linear's bias gradient = column sums of these rows
             # (the version guards against autograd accumulating another gradient into dqkv)
-            dqkv._ddl_colsum_rows = (cs if rc == 2 else cs[:B], dqkv._version)
+            dqkv._ddl_colsum_rows = (cs[:tiled_rows] if rc == 2 else cs[:B], dqkv._version)
         return dqkv, None, None, None
 
 
