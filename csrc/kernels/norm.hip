@@ -14,6 +14,8 @@
 // per row and per-block dgamma/dbeta partials reduced by a second kernel.
 #include "ddl_common.h"
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 namespace {
 
@@ -256,11 +258,50 @@ __global__ __launch_bounds__(256) void bn_apply2_rows_k(const T* __restrict__ x,
     }
 }
 
-// blocks for the row-major passes: ~8 blocks of 256 threads per CU, each thread
-// looping over rows
-static int rows_grid(long M, int C) {
+// blocks for the row-major passes: ONE resident round -- as many blocks of 256 threads as the
+// CUs hold at once for THIS kernel (its occupancy), each thread looping over rows.  A fixed 2048
+// (8 per CU) left a second round wherever registers allow fewer: at 68 VGPRs (7 waves per SIMD)
+// 1792 blocks ran, then 256 more, one per CU, ran alone to finish the pass.
+// DDL_BN_ROWS_GRID=0 restores the fixed 2048 (A/B timing).
+static int cu_count() {
+    static const int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
+static bool rows_grid_fit() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_BN_ROWS_GRID");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+static int rows_grid(long M, int C, const void* kernel = nullptr) {
     const long rpb = 256 / (C / 8);
-    return (int)std::max<long>(1, std::min<long>(2048, (M + rpb - 1) / rpb));
+    const long need = (M + rpb - 1) / rpb;
+    long cap = 2048;
+    if (kernel && rows_grid_fit()) {
+        static std::mutex mu;
+        static std::unordered_map<const void*, int> per_cu;
+        int nb = 0;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto it = per_cu.find(kernel);
+            if (it == per_cu.end()) {
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess) nb = 8;
+                nb = std::min(8, std::max(1, nb));
+                per_cu.emplace(kernel, nb);
+            } else {
+                nb = it->second;
+            }
+        }
+        cap = (long)nb * cu_count();
+    }
+    return (int)std::max<long>(1, std::min<long>(cap, need));
 }
 static bool rows_ok(int C) { return C % 8 == 0 && 256 % (C / 8) == 0; }
 
@@ -804,14 +845,9 @@ static void bn_apply_dispatch(const T* x, const T* res, const float* sc, const f
                               int C, int relu, hipStream_t st) {
     if (rows_ok(C) && n % C == 0) {
         const long M = n / C;
-        const int gr = rows_grid(M, C);
-        if (res) {
-            if (relu) bn_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
-            else bn_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
-        } else {
-            if (relu) bn_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
-            else bn_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(x, res, sc, sh, y, mask, M, C);
-        }
+        auto k = res ? (relu ? bn_apply_rows_k<T, true, true> : bn_apply_rows_k<T, true, false>)
+                     : (relu ? bn_apply_rows_k<T, false, true> : bn_apply_rows_k<T, false, false>);
+        hipLaunchKernelGGL(k, dim3(rows_grid(M, C, (const void*)k)), dim3(256), 0, st, x, res, sc, sh, y, mask, M, C);
         return;
     }
     const long n8 = n / 8;
@@ -832,10 +868,10 @@ DDL_API int ddl_bn_apply2(int dtype, const void* x, const void* x2, const float*
                           hipStream_t st) {
     if (n % 8 || !rows_ok(C) || n % C) return -1;
     const long M = n / C;
-    const int gr = rows_grid(M, C);
     uint8_t* mk = (uint8_t*)mask;
-#define BA2(T) do { if (relu) bn_apply2_rows_k<T, true><<<gr, 256, 0, st>>>((const T*)x, (const T*)x2, scale, shift, scale2, shift2, (T*)y, mk, M, C); \
-                    else bn_apply2_rows_k<T, false><<<gr, 256, 0, st>>>((const T*)x, (const T*)x2, scale, shift, scale2, shift2, (T*)y, mk, M, C); } while (0)
+#define BA2(T) do { auto k = relu ? bn_apply2_rows_k<T, true> : bn_apply2_rows_k<T, false>; \
+                    hipLaunchKernelGGL(k, dim3(rows_grid(M, C, (const void*)k)), dim3(256), 0, st, (const T*)x, (const T*)x2, \
+                                       scale, shift, scale2, shift2, (T*)y, mk, M, C); } while (0)
     if (dtype == 1) BA2(bf16_t);
     else BA2(float);
 #undef BA2
@@ -872,14 +908,10 @@ static void bn_bwd_dispatch(const T* dy, const uint8_t* yout, const T* x, const 
     else bn_bwd_partial_k<T, false><<<nblk, BN_NT, 0, st>>>(dy, yout, x, mean, invstd, M, C, (int)rpb, part);
     bwd_finalize<T>(part, nblk, nullptr, C, M, gamma, invstd, dgamma, dbeta, coef, acc, st);
     if (rows_ok(C)) {
-        const int gr = rows_grid(M, C);
-        if (relu) {
-            if (dres) bn_bwd_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
-            else bn_bwd_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
-        } else {
-            if (dres) bn_bwd_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
-            else bn_bwd_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(dy, yout, x, mean, invstd, coef, dx, dres, M, C);
-        }
+        auto k = relu ? (dres ? bn_bwd_apply_rows_k<T, true, true> : bn_bwd_apply_rows_k<T, true, false>)
+                      : (dres ? bn_bwd_apply_rows_k<T, false, true> : bn_bwd_apply_rows_k<T, false, false>);
+        hipLaunchKernelGGL(k, dim3(rows_grid(M, C, (const void*)k)), dim3(256), 0, st, dy, yout, x, mean, invstd, coef,
+                           dx, dres, M, C);
         return;
     }
     const long n8 = M * C / 8;
@@ -1252,14 +1284,10 @@ template <typename T>
 static void bn_bwd_apply_only(const T* dy, const uint8_t* mk, const T* x, const float* mean, const float* invstd,
                               long M, int C, int relu, const float* coef, T* dx, T* dres, hipStream_t st) {
     if (!rows_ok(C)) return;
-    const int gr = rows_grid(M, C);
-    if (relu) {
-        if (dres) bn_bwd_apply_rows_k<T, true, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-        else bn_bwd_apply_rows_k<T, true, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-    } else {
-        if (dres) bn_bwd_apply_rows_k<T, false, true><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-        else bn_bwd_apply_rows_k<T, false, false><<<gr, 256, 0, st>>>(dy, mk, x, mean, invstd, coef, dx, dres, M, C);
-    }
+    auto k = relu ? (dres ? bn_bwd_apply_rows_k<T, true, true> : bn_bwd_apply_rows_k<T, true, false>)
+                  : (dres ? bn_bwd_apply_rows_k<T, false, true> : bn_bwd_apply_rows_k<T, false, false>);
+    hipLaunchKernelGGL(k, dim3(rows_grid(M, C, (const void*)k)), dim3(256), 0, st, dy, mk, x, mean, invstd, coef, dx,
+                       dres, M, C);
 }
 
 template <typename T>
