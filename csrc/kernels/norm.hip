@@ -1141,9 +1141,17 @@ static int ln_env(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && atoi(v) > 0 ? atoi(v) : dflt;
 }
+// Blocks of ~32 rows, rounded UP to whole rounds of the blocks the CUs hold at once (2 per CU at the
+// 230-240 VGPRs of the H = 768 / 1024 kernels): ViT's 25216 rows made 788 blocks -- one full round
+// of 512 and a 276-block second one; now 1024 equal blocks of 24-25 rows (rpb = ceil(rows / nblk))
+// run two full rounds.  DDL_LN_BWD_ROUNDS=0: the plain count (A/B timing).
 DDL_API int ddl_ln_bwd_nblk(long rows) {
     static const int rpb = ln_env("DDL_LN_BWD_ROWS", 32), cap = ln_env("DDL_LN_BWD_MAXBLK", 1024);
-    return (int)std::max<long>(1, std::min<long>(cap, (rows + rpb - 1) / rpb));
+    static const bool rounds = [] { const char* e = getenv("DDL_LN_BWD_ROUNDS"); return !(e && e[0] == '0'); }();
+    long nblk = std::max<long>(1, std::min<long>(cap, (rows + rpb - 1) / rpb));
+    const long slots = 2L * cu_count();
+    if (rounds && nblk > slots && nblk % slots) nblk = std::min<long>(std::max<long>(cap, slots), (nblk + slots - 1) / slots * slots);
+    return (int)std::min<long>(nblk, rows);
 }
 
 template <typename T>
