@@ -1,0 +1,49 @@
+"""GEMM tuner candidate lists (ops/_native_gemm.py): pure host logic, no GPU.
+
+* the "hybrid" row split is offered exactly when a 256x256-tile grid ends in a partial round and
+  the remainder can be split-K over the chip (ViT-B/16: 297 / 891 tiles; not BERT-base's 192 /
+  768-tile grids, which are under one round or whole rounds);
+* its first launch covers whole rounds of tiles, so the split part is the partial round only;
+* "big192" (256 x 192 tiles) is opt-in (DDL_GEMM_192=1) and only for N % 192 == 0.
+"""
+import importlib
+
+import pytest
+
+NG = importlib.import_module("databricks_distributed_deep_learning_amd.ops._native_gemm")
+
+
+@pytest.mark.parametrize("M,N,K,expect", [
+    (25216, 768, 768, (21760, 3)),      # ViT O-projection: 99 x 3 = 297 tiles
+    (25216, 768, 3072, (21760, 6)),     # ViT FFN2: same grid, K = 3072 allows 6 splits
+    (25216, 2304, 768, (21760, 2)),     # ViT QKV: 99 x 9 = 891 tiles, 126-tile remainder
+    (16384, 768, 768, None),            # BERT: 192 tiles, under one round
+    (16384, 3072, 768, None),           # BERT FFN1: 768 tiles, three whole rounds
+    (25216, 3072, 768, None),           # ViT FFN1: 168-tile remainder cannot split within one round
+    (25216, 768, 200, None),            # K not a whole number of 64-wide k-tiles
+])
+def test_hybrid_rows(M, N, K, expect):
+    assert NG.hybrid_rows(M, N, K) == expect
+    if expect is not None:
+        m1, s = expect
+        tn = -(-N // 256)
+        assert m1 % 256 == 0 and (m1 // 256) * tn <= ((-(-M // 256) * tn) // NG.NUM_CU) * NG.NUM_CU
+        assert (-(-(M - m1) // 256)) * tn * s <= NG.NUM_CU
+
+
+def test_candidates_offer_hybrid_only_for_partial_rounds():
+    kinds = {c[0] for c in NG._candidates(NG.MODE_NT, 25216, 768, 3072, False, 3072, 3072)}
+    assert "hybrid" in kinds and "big" in kinds
+    kinds = {c[0] for c in NG._candidates(NG.MODE_NT, 16384, 768, 3072, False, 3072, 3072)}
+    assert "hybrid" not in kinds
+    # weight-gradient (TN) and row-remapped GEMMs never take it
+    assert not any(c[0] == "hybrid" for c in NG._candidates(NG.MODE_TN, 25216, 768, 3072, False, 768, 3072))
+    assert not any(c[0] == "hybrid" for c in NG._candidates(NG.MODE_NT, 25216, 768, 3072, True, 3072, 3072))
+
+
+def test_big192_is_opt_in(monkeypatch):
+    assert not any(c[0] == "big192" for c in NG._candidates(NG.MODE_NT, 16384, 768, 768, False, 768, 768))
+    monkeypatch.setattr(NG, "_BIG192", True)
+    assert ("big192", 1) in NG._candidates(NG.MODE_NT, 16384, 768, 768, False, 768, 768)
+    assert ("big192", 1) in NG._candidates(NG.MODE_NN, 16384, 2304, 768, False, 768, 2304)
+    assert not any(c[0] == "big192" for c in NG._candidates(NG.MODE_NT, 16384, 1024, 768, False, 768, 768))
