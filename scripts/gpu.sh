@@ -96,7 +96,13 @@ step() {
       local m=$1 cmd
       cmd=$(run_model "$m" 2 1) || return 1
       rm -rf "gpurun_out/pmc_$m"
+      # tune once into a cache first: the counted runs load the GEMM kernel choices instead of
+      # timing every candidate (whose dispatches would otherwise fill the table)
+      export DDL_GEMM_TUNE_CACHE=$PWD/gpurun_out/tune_$m.json
+      rm -f "$DDL_GEMM_TUNE_CACHE"
+      timeout -k 10 300 $cmd > "gpurun_out/pmc_${m}_tune.log" 2>&1 || { tail -20 "gpurun_out/pmc_${m}_tune.log"; return 1; }
       bash scripts/pmc_profile.sh "gpurun_out/pmc_$m" -- $cmd || return 1
+      unset DDL_GEMM_TUNE_CACHE
       python3 scripts/pmc_summary.py "gpurun_out/pmc_$m" --top 30 --title "$m training step (1 warm-up + 2 steps)" \
         > "gpurun_out/pmc_$m.md"
       rm -rf "gpurun_out/pmc_$m"
