@@ -9,7 +9,7 @@
 #   bench [args]          bench.py (default 20 steps, 5 warm-up) -> gpurun_out/bench.log
 #   stock [args]          bench.py --native stock (plain PyTorch-ROCm + torch DDP arm)
 #   ab LIB MODEL [RUNS]   same-box A/B of libddl_LIB.so (scripts/build_ab.sh) vs the tree's library,
-#                         alternating RUNS times (default 3) on MODEL (resnet50 | bert_base)
+#                         alternating RUNS times (default 3) on MODEL (resnet50 | bert_base | vit_b16 | ...)
 #   abenv VAR=VAL MODEL [RUNS]  same-box A/B of an environment toggle (unset vs VAR=VAL), alternating
 #   prof MODEL            rocprofv3 kernel table (steady state) -> gpurun_out/kernels_MODEL.md
 #   pmc MODEL             3 PMC passes summarised             -> gpurun_out/pmc_MODEL.md
@@ -30,6 +30,9 @@ run_model() {   # run_model MODEL STEPS WARMUP -> command words for one profiled
     bert_large_lamb) echo "$TRAIN --preset bert_large_lamb --batch_size 32 --steps $2 --warmup_steps $3 --log_every 0" ;;
     *) echo "unknown model $1" >&2; return 1 ;;
   esac
+}
+ab_value() {    # ab_value LOG -> the throughput of a bench.py (value) or train CLI (samples_per_sec) run
+  tail -1 "$1" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d.get("value", d.get("samples_per_sec")))'
 }
 opt_kernel() {  # the optimizer kernel that ends each step (steady-state cut for prof_summary)
   case $1 in resnet50) echo sgd_k ;; bert_large_lamb) echo lamb_phase2 ;; *) echo adamw_k ;; esac
@@ -62,9 +65,10 @@ step() {
       for i in $(seq 1 "$runs"); do
         for arm in cur "$lib"; do
           if [ "$arm" = cur ]; then unset DDL_NATIVE_LIB; else export DDL_NATIVE_LIB=$v; fi
-          timeout -k 10 300 python bench.py --model "$model" --steps 30 --warmup 5 > "gpurun_out/ab_${arm}_$i.log" 2>&1 \
+          # shellcheck disable=SC2046
+          timeout -k 10 300 $(run_model "$model" 30 5) > "gpurun_out/ab_${arm}_$i.log" 2>&1 \
             || { tail -20 "gpurun_out/ab_${arm}_$i.log"; return 1; }
-          echo "$arm run=$i $(tail -1 "gpurun_out/ab_${arm}_$i.log" | python3 -c 'import sys,json; print(json.loads(sys.stdin.read())["value"])')"
+          echo "$arm run=$i $(ab_value "gpurun_out/ab_${arm}_$i.log")"
         done
       done
       unset DDL_NATIVE_LIB ;;
@@ -73,13 +77,15 @@ step() {
       for i in $(seq 1 "$runs"); do
         for arm in base env; do
           if [ "$arm" = base ]; then
-            timeout -k 10 300 python bench.py --model "$model" --steps 30 --warmup 5 > "gpurun_out/abenv_${arm}_$i.log" 2>&1 \
+            # shellcheck disable=SC2046
+            timeout -k 10 300 $(run_model "$model" 30 5) > "gpurun_out/abenv_${arm}_$i.log" 2>&1 \
               || { tail -20 "gpurun_out/abenv_${arm}_$i.log"; return 1; }
           else
-            env "$kv" timeout -k 10 300 python bench.py --model "$model" --steps 30 --warmup 5 > "gpurun_out/abenv_${arm}_$i.log" 2>&1 \
+            # shellcheck disable=SC2046
+            env "$kv" timeout -k 10 300 $(run_model "$model" 30 5) > "gpurun_out/abenv_${arm}_$i.log" 2>&1 \
               || { tail -20 "gpurun_out/abenv_${arm}_$i.log"; return 1; }
           fi
-          echo "$arm($kv) $model run=$i $(tail -1 "gpurun_out/abenv_${arm}_$i.log" | python3 -c 'import sys,json; print(json.loads(sys.stdin.read())["value"])')"
+          echo "$arm($kv) $model run=$i $(ab_value "gpurun_out/abenv_${arm}_$i.log")"
         done
       done ;;
     prof)
