@@ -22,6 +22,10 @@ ImageNet-shape batches (NHWC 224x224, 1000 classes, SGD-momentum, fp32 master
 weights), random-init weights; weak scaling (fixed per-GPU batch).  BERT-base
 seq-128 fine-tuning (AdamW) is measured in the same run and reported under
 ``extra`` (``--model resnet50`` skips it).
+
+A/B switches read from the environment: ``DDL_PHASE_TIMING=0`` (no per-phase events),
+``DDL_EAGER_OPTIMIZER=1`` (per-bucket optimizer updates during backward on a side stream;
+measured slower on one GPU, ``profiles/ab_r03.md``).
 """
 from __future__ import annotations
 
@@ -91,6 +95,7 @@ def run_one(model: str, args, world: int):
     cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
                       bucket_mb=args.bucket_mb, backend=args.backend,
                       zero_optimizer=args.zero, sync_bn=args.sync_bn,
+                      eager_optimizer=os.environ.get("DDL_EAGER_OPTIMIZER", "0") == "1",
                       phase_timing=os.environ.get("DDL_PHASE_TIMING", "1") != "0")
     tr = Trainer(cfg)
     s = tr.run()
