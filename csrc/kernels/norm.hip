@@ -576,11 +576,16 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
     // raw (unconverted) loads of one row -- input x, dy and the residual -- so the next row
     // pair's loads stay in flight while the current pair's reductions run; with dropout the
     // row's keep bits (4 per lane and column group) are generated once and reused for dx
+    // the row's saved mean / rstd travel with its operands: loaded at finish time they put a
+    // dependent scalar-load miss in front of every row's reductions
     struct RowRaw {
         typename Raw4<T>::type x[VPL], d[VPL], r[VPL];
         uint32_t kb[VPL];
+        float mu, rs;
     };
     auto load_row = [&](long row, RowRaw& R) {
+        R.mu = mean[row];
+        R.rs = rstd[row];
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
             const int col = 256 * k + 4 * lane;
@@ -614,7 +619,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
 #pragma unroll
             for (int k = 0; k < VPL; ++k) ra[k] = ld_raw4(dadd + row * H + 256 * k + 4 * lane);
         }
-        const float mu = mean[row], rs = rstd[row];
+        const float mu = R.mu, rs = R.rs;
         float xh[VPL][4], gy[VPL][4];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll

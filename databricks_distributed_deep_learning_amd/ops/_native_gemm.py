@@ -113,8 +113,11 @@ _DIRECT = os.environ.get("DDL_GEMM_DIRECT", "1") != "0"    # gemm_big.hip regist
 # no epilogue beyond a bf16 bias OR a residual (its bias epilogue / beta = 1).  It runs only where the
 # tuner measures it faster than every native candidate (profiles/tn_wgrad_vs_hipblaslt.log: e.g. NT
 # 16384x768x3072 60.8 vs 68.7 us, NT 25216x768x768 36.9 vs 51.7 us); the fused GELU / dGELU /
-# BatchNorm / statistics epilogues and the weight gradients stay native.  DDL_GEMM_BLAS=0: never.
-_BLAS = os.environ.get("DDL_GEMM_BLAS", "1") != "0"
+# BatchNorm / statistics epilogues and the weight gradients stay native.  Opt-in (DDL_GEMM_BLAS=1):
+# BERT-base runs with it are ~1 % faster in most processes, but 4 of 15 same-box runs came out 4-20 %
+# slower across the whole step (forward AND backward), never seen in 9 runs without it
+# (profiles/ab_r03.md) -- a single benchmark run is better served by the steady native plan.
+_BLAS = os.environ.get("DDL_GEMM_BLAS", "0") == "1"
 _plan_call = False      # set while plan() tunes a signature (no "blas" candidate then)
 
 

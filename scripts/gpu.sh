@@ -32,7 +32,7 @@ run_model() {   # run_model MODEL STEPS WARMUP -> command words for one profiled
   esac
 }
 ab_value() {    # ab_value LOG -> the throughput of a bench.py (value) or train CLI (samples_per_sec) run
-  tail -1 "$1" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d.get("value", d.get("samples_per_sec")))'
+  tail -1 "$1" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d.get("value", d.get("samples_per_sec")), d.get("phases_ms") or "")'
 }
 opt_kernel() {  # the optimizer kernel that ends each step (steady-state cut for prof_summary)
   case $1 in resnet50) echo sgd_k ;; bert_large_lamb) echo lamb_phase2 ;; *) echo adamw_k ;; esac
