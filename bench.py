@@ -81,7 +81,7 @@ def run_one(model: str, args, world: int):
     if args.native == "stock":
         from databricks_distributed_deep_learning_amd.baselines import run_stock
         batch = (args.batch or 256) if model == "resnet50" else (args.bert_batch or 128)
-        return run_stock(model, batch, args.steps, args.warmup, seq_len=128, bucket_mb=args.bucket_mb,
+        return run_stock(model, batch, args.steps, args.warmup, seq_len=128, bucket_mb=args.bucket_mb or 25.0,
                          pad_fraction=args.bert_pad_fraction)
     from databricks_distributed_deep_learning_amd.config import get_preset
     from databricks_distributed_deep_learning_amd.training.loop import Trainer
@@ -99,8 +99,25 @@ def run_one(model: str, args, world: int):
                       phase_timing=os.environ.get("DDL_PHASE_TIMING", "1") != "0")
     tr = Trainer(cfg)
     s = tr.run()
+    tr.close()
     del tr
+    s["gemm_plan"] = gemm_plan_digest(model)
     return s
+
+
+def gemm_plan_digest(model: str) -> str:
+    """Hash of the tuned GEMM kernel plan this process ran (every signature -> (kernel, splits));
+    the full plan goes to stderr.  Two bench processes whose step times differ can then be told
+    apart by plan (tuner picks) or not (same plan: the cause is elsewhere)."""
+    import hashlib
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm
+    plan = {k: list(v) for k, v in sorted(_native_gemm.tuned_choices().items())}
+    if not plan:
+        return ""
+    text = json.dumps(plan, sort_keys=True)
+    digest = hashlib.sha1(text.encode()).hexdigest()[:12]
+    log(f"[bench] {model} gemm plan {digest} ({len(plan)} signatures): {text}")
+    return digest
 
 
 def main() -> int:
@@ -116,12 +133,14 @@ def main() -> int:
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off", "stock"],
                     help="auto/on: HIP kernels; stock: plain PyTorch-ROCm + torch DDP arm; "
                          "off: the framework's CPU-oracle ops (correctness reference, not a baseline)")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--bucket-mb", default="25",
+                    help="gradient bucket MB, or 'auto' (sized from the startup all-reduce probe at N > 1)")
     ap.add_argument("--zero", action="store_true", help="ZeRO-1: shard fp32 master + optimizer state over ranks")
     ap.add_argument("--sync-bn", action="store_true", help="SyncBatchNorm (CV models)")
     ap.add_argument("--backend", default=os.environ.get("DDL_BACKEND", "auto"),
                     help="process-group backend (auto = RCCL on GPU); gloo only for 1-GPU multi-rank rehearsals")
     args = ap.parse_args()
+    args.bucket_mb = 0.0 if str(args.bucket_mb).lower() == "auto" else float(args.bucket_mb)
     # the first step times GEMM kernel candidates per shape (ops/_native_gemm.py);
     # it must never land inside the timed region
     args.warmup = max(1, args.warmup)
@@ -170,7 +189,13 @@ def main() -> int:
             "grad_comm": head.get("comm"),
         },
         "phases_ms": head.get("phases_ms"),
+        "gemm_plan": {m: r.get("gemm_plan", "") for m, r in results.items()},
+        "bucket_policy": head.get("bucket_policy"),
     }
+    if head.get("comm_probe"):
+        line["comm_probe"] = head["comm_probe"]          # startup all-reduce probe (N > 1, native engine)
+    if head.get("comm_buckets"):
+        line["comm_buckets"] = head["comm_buckets"]      # last step: per-bucket ring time / bus GB/s
     if "bert_base" in results and is_r50:
         b = results["bert_base"]
         line["extra"] = {

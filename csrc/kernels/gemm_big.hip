@@ -44,6 +44,13 @@ namespace {
 #ifndef DDL_GROUP_M
 #define DDL_GROUP_M 8      // tile rows per L2 group (tile order inside an XCD's share)
 #endif
+// Deep retire (default): each half-tile is waited for in the phase right before its first
+// read, not with the whole tile at phases 4 / 8 -- five half-tiles (80 KB) stay in flight
+// instead of three, and the tightest DMA gets five phases to land instead of three (the
+// short-K GEMMs' main loop was DMA-latency bound: csrc/bench/gemm_stamps.cpp).
+#ifndef DDL_DEEP_RETIRE
+#define DDL_DEEP_RETIRE 1
+#endif
 constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
 constexpr int TB = 256, BK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB half-tile
@@ -297,7 +304,35 @@ __device__ __forceinline__ bf16x8 frag(const char* hbase, int rbase, int kk) {
 #endif
 #define LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 #define VM6() asm volatile("s_waitcnt vmcnt(6)" ::: "memory")
+#define VMN(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 #define VM0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+
+// Diagnostic build only (-DDDL_GEMM_STAMPS, csrc/bench/gemm_stamps.cpp): waves 0 and 4 record
+// s_memrealtime / s_memtime at four points of every tile (start, main loop start / end,
+// epilogue issued) into a buffer of their own; never compiled into the library.
+#ifdef DDL_GEMM_STAMPS
+__device__ unsigned long long* g_stamps;
+constexpr int STAMP_TILES = 16;
+#define STAMP(ev)                                                                                           \
+    do {                                                                                                    \
+        if ((threadIdx.x & 255) == 0 && stamp_ti < STAMP_TILES) {                                            \
+            const unsigned long long rt = __builtin_amdgcn_s_memrealtime(), ct = __builtin_amdgcn_s_memtime(); \
+            unsigned long long* d = g_stamps + ((((long)blockIdx.y * gridDim.x + blockIdx.x) * STAMP_TILES + stamp_ti) * 2 + \
+                                                (threadIdx.x >> 8)) * 8 + (ev) * 2;                           \
+            d[0] = rt;                                                                                      \
+            d[1] = ct;                                                                                      \
+        }                                                                                                   \
+    } while (0)
+__device__ unsigned long long* g_kstamps;   // [block][k-tile pair < 32]: first tile only, wave 0
+#define KSTAMP(it)                                                                                          \
+    do {                                                                                                    \
+        if (threadIdx.x == 0 && stamp_ti == 0 && (it) < 32)                                                 \
+            g_kstamps[((long)blockIdx.y * gridDim.x + blockIdx.x) * 32 + (it)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define STAMP(ev) do {} while (0)
+#define KSTAMP(it) do {} while (0)
+#endif
 
 __device__ __forceinline__ float act_fn(float v, int act) {
     switch (act) {
@@ -743,8 +778,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         if (DYN && p.sched && threadIdx.x == 0) s_tick = tick;
     };
     int vt = blockIdx.x;
+#ifdef DDL_GEMM_STAMPS
+    int stamp_ti = 0;
+#endif
     coords(vt);
     ask();
+    STAMP(0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = w >> 2, wn = w & 3;
     const int split = blockIdx.y;
@@ -813,6 +852,66 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         else if (hold == 38) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
         else VM6();
     };
+#if DDL_DEEP_RETIRE
+    // Counted waits from the stage-issue history: bit s of `cm` = stage slot s (the DMA of
+    // phase s + 1) of this iteration went out, `pm` = the previous iteration's slots (or the
+    // prologue's: E -> slots 1-4, O A0 / B0 / B1 -> slots 5-7).  Stage order per iteration:
+    // 1 O-A1(kO)  2 E-A0  3 E-B0  4 E-B1  5 E-A1 (kE+2)  6 O-A0  7 O-B0  8 O-B1 (kO+2).  A wait
+    // that retires the half of slot t leaves the ops younger than it in flight: 2 per issued
+    // slot after t (every wave issues 2 DMAs per half).  Half -> wait (the phase before its
+    // first read): E-B1 phase 1, E-A1 phase 2, O-A0/B0 phase 4, O-B1 phase 5, O-A1 phase 6,
+    // E-A0/B0 (next tile) phase 8.
+    auto vm_younger = [&](int n) {
+        switch (n) {
+            case 10: VMN(10); break;
+            case 8: VMN(8); break;
+            case 6: VMN(6); break;
+            case 4: VMN(4); break;
+            case 2: VMN(2); break;
+            default: VM0(); break;
+        }
+    };
+    auto younger = [&](unsigned pm, unsigned cm, int t, int q) -> int {   // slots t+1 .. q
+        const unsigned h = pm | (cm << 8);
+        const unsigned m = ((1u << (q + 1)) - 1u) & ~((1u << (t + 1)) - 1u);
+        return 2 * __builtin_popcount(h & m);
+    };
+    // fresh: the first pair after a store-behind epilogue -- E retired with the stores, O staged
+    // whole before them: retired at phase 4 by `hold` (vm_retire_o), no per-half waits
+    auto phasesE = [&](int kE, bool stO1, bool more, unsigned pm, unsigned& cm, bool fresh, int hold, bool hasO) {
+        // phase 1: E (0,0)
+        readA(0, 0);
+        readB(0, 0, fb0);
+        if (stO1) { sa.stage(p, smem, 1, 1, kE + 1); cm |= 1u; }
+        if (!fresh) vm_younger(younger(pm, cm, 3, 8));          // E-B1(kE)
+        READS_DONE_BARRIER();
+        mma(0, 0, fb0);
+        BARRIER();
+        // phase 2: E (0,1)
+        readB(0, 1, fb1);
+        if (more) { sa.stage(p, smem, 0, 0, kE + 2); cm |= 2u; }
+        if (!fresh) vm_younger(younger(pm, cm, 4, 9));          // E-A1(kE)
+        READS_DONE_BARRIER();
+        mma(0, 1, fb1);
+        BARRIER();
+        // phase 3: E (1,1)
+        readA(0, 1);
+        if (more) { sb.stage(p, smem, 0, 0, kE + 2); cm |= 4u; }
+        READS_DONE_BARRIER();
+        mma(1, 1, fb1);
+        BARRIER();
+        // phase 4: E (1,0); retire O-A0 / O-B0 (kE+1)
+        if (more) { sb.stage(p, smem, 0, 1, kE + 2); cm |= 8u; }
+        if (hasO) {
+            if (!fresh) vm_younger(younger(pm, cm, 6, 11));
+            else if (more) vm_retire_o(hold);
+            else VM0();
+        }
+        BARRIER();
+        mma(1, 0, fb0);
+        BARRIER();
+    };
+#else
     auto phasesE = [&](int kE, bool stO1, bool more, int hold = 0) {
         // phase 1: E (0,0)
         readA(0, 0);
@@ -839,6 +938,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         mma(1, 0, fb0);
         BARRIER();
     };
+
+#endif
 
     // prologue, first part: E <- tile kt0 (all halves)
     auto prologueE = [&]() {
@@ -870,11 +971,57 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         prologueO();
     }
     publish();
+    STAMP(1);
     int hold_o = 0;     // != 0: the coming tile's O was staged before the previous tile's stores
     for (;;) {
         if (nK > 0) {
             const int pairs = nK / 2;
+#if DDL_DEEP_RETIRE
+            unsigned pm = nK > 1 ? 0xFEu : 0x1Eu, cm = 0u;    // the prologue's slots (see vm_younger)
             for (int it = 0; it < pairs; ++it) {
+                KSTAMP(it);
+                const int kE = kt0 + 2 * it, kO = kE + 1;
+                const bool more = kE + 2 < kt_end;
+                const bool moreO = kO + 2 < kt_end;
+                // first pair after a store-behind epilogue: O is already staged whole
+                const bool fresh = !BNB && it == 0 && hold_o;
+                phasesE(kE, !fresh, more, pm, cm, fresh, it == 0 ? hold_o : 0, true);
+                // phase 5: O (0,0)
+                readA(1, 0);
+                readB(1, 0, fb0);
+                if (more) { sa.stage(p, smem, 0, 1, kE + 2); cm |= 16u; }
+                if (!fresh) vm_younger(younger(pm, cm, 7, 12));     // O-B1(kO)
+                READS_DONE_BARRIER();
+                mma(0, 0, fb0);
+                BARRIER();
+                // phase 6: O (0,1)
+                readB(1, 1, fb1);
+                if (moreO) { sa.stage(p, smem, 1, 0, kO + 2); cm |= 32u; }
+                if (!fresh) vm_younger(younger(pm, cm, 8, 13));     // O-A1(kO)
+                READS_DONE_BARRIER();
+                mma(0, 1, fb1);
+                BARRIER();
+                // phase 7: O (1,1)
+                readA(1, 1);
+                if (moreO) { sb.stage(p, smem, 1, 0, kO + 2); cm |= 64u; }
+                READS_DONE_BARRIER();
+                mma(1, 1, fb1);
+                BARRIER();
+                // phase 8: O (1,0); retire E-A0 / E-B0 (kE+2)
+                if (moreO) { sb.stage(p, smem, 1, 1, kO + 2); cm |= 128u; }
+                if (more) vm_younger(younger(pm, cm, 10, 15));
+                BARRIER();
+                mma(1, 0, fb0);
+                BARRIER();
+                pm = cm;
+                cm = 0u;
+            }
+            // odd tile count: the last E tile (its E-B1 / E-A1 retired at phases 1 / 2)
+            if (nK & 1) phasesE(kt_end - 1, false, false, pm, cm, false, 0, false);
+#else
+            const int pairs = nK / 2;
+            for (int it = 0; it < pairs; ++it) {
+                KSTAMP(it);
                 const int kE = kt0 + 2 * it, kO = kE + 1;
                 const bool more = kE + 2 < kt_end;
                 const bool moreO = kO + 2 < kt_end;
@@ -908,12 +1055,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             }
             // odd tile count: the last E tile (fully landed: phase 8 waited vmcnt(0))
             if (nK & 1) phasesE(kt_end - 1, false, false);
+#endif
 #if DDL_STAGGER
             // realign the groups: after this barrier every wave has finished its
             // last MFMA and every fragment read, so the LDS buffers are free
             if (wm == 0) BARRIER();
 #endif
         }
+        STAMP(2);
         if (DIRECT) {
             // dynamic: ticket t of XCD x is its range's tile gridDim.x/8 + t, i.e. the
             // static-order id 8 * (gridDim.x/8 + t) + x
@@ -963,6 +1112,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 epi_direct<EK_DGELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if constexpr (EDGE)
                 epi_direct<EK_GEN, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+            STAMP(3);
+#ifdef DDL_GEMM_STAMPS
+            ++stamp_ti;
+            STAMP(0);
+#endif
             if (!next) {
                 if constexpr (DYN) break;    // the ticket slot's exit bookkeeping below the loop
                 return;
@@ -1002,6 +1156,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // on every path (the compiler's wait for the ticket then lands here, not in
             // the next main loop), after a barrier that follows every wave's read of s_tick
             publish();
+            STAMP(1);
             continue;
         }
         break;

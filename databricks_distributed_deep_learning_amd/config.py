@@ -44,8 +44,9 @@ class TrainConfig:
     lr_warmup_steps: int = 0
     # ---- distributed ------------------------------------------------------
     backend: str = "auto"            # auto|nccl|gloo  (nccl == RCCL on ROCm)
-    bucket_mb: float = 25.0          # gradient bucket size for the reducer (xGMI ring: few-MB latency floor)
+    bucket_mb: float = 25.0          # gradient bucket size for the reducer (<= 0: "auto", from the comm probe)
     first_bucket_mb: float = 4.0     # small first bucket so comm starts early
+    comm_probe: bool = True          # world > 1 with the native engine: time 1/4/16/64 MB all-reduces at start
     comm: str = "auto"               # gradient all-reduce engine: auto|native (C++ RCCL engine)|torch
     grad_reduce_dtype: str = "auto"  # auto|fp32|bf16  all-reduce payload dtype
     broadcast_buffers: bool = False

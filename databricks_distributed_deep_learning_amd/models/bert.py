@@ -105,6 +105,9 @@ class BertLayer(nn.Module):
 
 
 class BertModel(nn.Module):
+    # ZeRO-1 gather waits (parallel/ddp.py): only dispatches to its children's forwards
+    _ddl_gather_router = True
+
     def __init__(self, c: BertConfig):
         super().__init__()
         self.config = c

@@ -131,6 +131,10 @@ class ResNet(nn.Module):
             mods.append(block(self.inplanes, planes, 1, None, zir))
         return nn.Sequential(*mods)
 
+    # ZeRO-1 gather waits (parallel/ddp.py): the root's forward reads the stem's conv / BN
+    # directly (conv_bn_maxpool), every other parameter through a child's forward
+    _ddl_direct_reads = ("conv1", "bn1")
+
     def features(self, x):
         if not self.channels_last_input:
             x = x.permute(0, 2, 3, 1).contiguous()

@@ -87,6 +87,9 @@ class ViTForImageClassification(nn.Module):
         self.classifier = Linear(H, c.num_labels, init_std=c.initializer_range)
         nn.init.zeros_(self.classifier.bias)
 
+    # ZeRO-1 gather waits (parallel/ddp.py): the root's forward reads the patch embedding directly
+    _ddl_direct_reads = ("patch_embed",)
+
     def patchify(self, x):
         """NHWC [B, 224, 224, 3] -> [B, 196, 768] in (kh, kw, c) order."""
         B, Hh, Ww, C = x.shape

@@ -11,13 +11,27 @@ The unique id is created by rank 0 and distributed over the existing
 ``torch.distributed`` group (a 128-byte object), so the engine works under the
 same launchers (``Distributor``, ``torchrun``) as everything else.  RCCL itself
 is the library PyTorch loaded (``torch/lib/librccl.so``), resolved with dlopen.
+
+Failure detection: a :class:`CommWatchdog` thread polls the engine's RCCL
+asynchronous error state and the age of the oldest unfinished collective; on a peer failure
+or a collective older than ``DDL_COMM_TIMEOUT_S`` (default 600 s, 0 = off) it aborts the
+communicator (``ncclCommAbort``: RCCL kernels blocked on a dead peer return, the streams
+drain) and every later engine call raises :class:`CommError` with the reason -- instead of
+the rank hanging until the process-group timeout.
+
+Bucket policy: :func:`probe_allreduce` times all-reduces of 1 / 4 / 16 / 64 MB
+on the engine (bus bandwidth per size), :func:`fit_latency_bandwidth` fits
+``t(S) = alpha + S / beta`` and :func:`auto_buckets` turns that into ``first_bucket_mb`` /
+``bucket_mb`` for ``--bucket-mb auto``.
 """
 from __future__ import annotations
 
 import ctypes
 import glob
 import os
-from typing import Optional, Sequence
+import threading
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -39,6 +53,11 @@ _SIGS = {
     "ddl_comm_stats": ([P, I], L),
     "ddl_comm_destroy": ([P, I], None),
     "ddl_comm_last_error": ([], ctypes.c_char_p),
+    "ddl_comm_async_error": ([P], I),
+    "ddl_comm_oldest_pending_ms": ([P], ctypes.c_double),
+    "ddl_comm_collective_ms": ([P, L], ctypes.c_double),
+    "ddl_comm_abort": ([P], I),
+    "ddl_comm_inject_error": ([P, I], I),
 }
 _DTYPES = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2, torch.int64: 3, torch.int32: 4}
 
@@ -97,10 +116,46 @@ def native_available() -> bool:
         dist.get_backend() == "nccl"
 
 
-class NativeComm:
-    """RCCL communicator over all ranks of ``group`` (default: the world)."""
+class CommWatchdog:
+    """Background thread: ``engine.poll()`` every ``interval`` seconds; the first error it
+    returns aborts the engine (``engine.fail(reason)``) and stops the thread.
 
-    def __init__(self, group=None, device: Optional[torch.device] = None):
+    ``engine`` needs ``poll() -> Optional[str]`` and ``fail(str)`` (NativeComm has both; the
+    CPU tests drive a fake)."""
+
+    def __init__(self, engine, interval: float = 1.0):
+        self.engine = engine
+        self.interval = max(0.01, float(interval))
+        self._stop = threading.Event()
+        self.reason: Optional[str] = None
+        self._t = threading.Thread(target=self._loop, name="ddl-comm-watchdog", daemon=True)
+        self._t.start()
+
+    def _loop(self) -> None:
+        while not self._stop.wait(self.interval):
+            try:
+                reason = self.engine.poll()
+            except Exception as e:  # noqa: BLE001 - a failing poll is itself the failure
+                reason = f"watchdog poll failed: {e}"
+            if reason:
+                self.reason = reason
+                self.engine.fail(reason)
+                return
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._t is not threading.current_thread():
+            self._t.join(timeout=5.0)
+
+
+class NativeComm:
+    """RCCL communicator over all ranks of ``group`` (default: the world).
+
+    ``timeout_s``: a collective unfinished for longer is declared hung and the communicator
+    aborted by the watchdog (env ``DDL_COMM_TIMEOUT_S``, default 600; 0 = no watchdog)."""
+
+    def __init__(self, group=None, device: Optional[torch.device] = None, timeout_s: Optional[float] = None,
+                 poll_s: Optional[float] = None):
         if not torch.cuda.is_available():
             raise CommError("NativeComm needs a GPU")
         self.group = group
@@ -124,11 +179,51 @@ class NativeComm:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
         if not self._h or int(ok.item()) == 0:
             raise CommError(f"ddl_comm_create failed on some rank: {_err() if not self._h else 'peer'}")
+        self.failed: Optional[str] = None
+        self.timeout_s = float(os.environ.get("DDL_COMM_TIMEOUT_S", "600") if timeout_s is None else timeout_s)
+        interval = float(os.environ.get("DDL_COMM_POLL_S", "1.0") if poll_s is None else poll_s)
+        self.watchdog = CommWatchdog(self, interval) if self.timeout_s > 0 else None
 
     # ------------------------------------------------------------------
     def _check(self, rc: int, what: str) -> None:
+        if self.failed:
+            raise CommError(f"{what}: communicator aborted ({self.failed})")
         if rc != 0:
             raise CommError(f"{what} failed ({rc}): {_err()}")
+
+    def poll(self) -> Optional[str]:
+        """The watchdog's check: an RCCL asynchronous error, or a collective on the comm
+        stream for longer than ``timeout_s``; None while healthy."""
+        h = getattr(self, "_h", None)
+        if not h or self.failed:
+            return None
+        rc = int(_fn("ddl_comm_async_error")(h))
+        if rc == -4:
+            return None                       # aborted / closed meanwhile
+        if rc != 0:
+            return f"RCCL asynchronous error {rc} on rank {self.rank} (a peer failed or a connection broke)"
+        age = float(_fn("ddl_comm_oldest_pending_ms")(h))
+        if self.timeout_s > 0 and age > 1e3 * self.timeout_s:
+            return f"collective on rank {self.rank} unfinished after {age / 1e3:.1f} s (timeout {self.timeout_s:g} s)"
+        return None
+
+    def fail(self, reason: str) -> None:
+        """Abort the communicator from any thread; later calls raise CommError(reason)."""
+        self.failed = reason
+        h = getattr(self, "_h", None)
+        if h:
+            _fn("ddl_comm_abort")(h)
+
+    def inject_error(self, code: int) -> None:
+        """Test hook: make RCCL's asynchronous error state read ``code`` (the watchdog's input)."""
+        _fn("ddl_comm_inject_error")(self._h, int(code))
+
+    def collective_ms(self, seq: int) -> float:
+        """Device time of finished collective ``seq`` (its start / done events), -1 if unknown."""
+        h = getattr(self, "_h", None)
+        if not h or seq <= 0:
+            return -1.0
+        return float(_fn("ddl_comm_collective_ms")(h, int(seq)))
 
     def all_reduce(self, t: torch.Tensor, average: bool = False) -> int:
         """In-place all-reduce of a contiguous GPU tensor on the comm stream (async).
@@ -194,11 +289,77 @@ class NativeComm:
         """Destroy the communicator.  ``abort=True`` (``ncclCommAbort``) is the failure
         path: it returns without waiting for peers and unblocks collectives stuck on a
         rank that died, so this rank can raise instead of hanging until the timeout."""
+        wd = getattr(self, "watchdog", None)
+        if wd is not None:
+            wd.stop()
+            self.watchdog = None
         if getattr(self, "_h", None):
-            _fn("ddl_comm_destroy")(self._h, int(abort))
+            _fn("ddl_comm_destroy")(self._h, int(abort or bool(getattr(self, "failed", None))))
             self._h = None
         if _ACTIVE is self:
             set_active(None)
 
     # no __del__: destroying a communicator during interpreter teardown can block
     # on peers that already exited; process exit releases it.
+
+
+# ---------------------------------------------------------------------- bucket policy
+def probe_allreduce(engine, device, sizes_mb: Sequence[float] = (1, 4, 16, 64), iters: int = 5,
+                    dtype: torch.dtype = torch.bfloat16, world: Optional[int] = None) -> List[Dict[str, float]]:
+    """Time all-reduces of each size on ``engine`` (``all_reduce(t)`` + ``wait()``: the native
+    engine, or any stand-in with that contract): one warm-up, then the median of ``iters``
+    host-timed calls with the device synchronised around each.  Returns per size: MB, ms,
+    algorithm bandwidth (GB/s = bytes / t) and bus bandwidth (x 2(n-1)/n, the per-link figure
+    of a ring: comparable across world sizes).  Every rank must call it (collective)."""
+    n = int(world if world is not None else dist.get_world_size())
+    esz = torch.empty((), dtype=dtype).element_size()
+    sync = torch.cuda.synchronize if torch.device(device).type == "cuda" else (lambda: None)
+    out = []
+    for mb in sizes_mb:
+        t = torch.ones(max(1, int(mb * (1 << 20)) // esz), dtype=dtype, device=device)
+        times = []
+        for i in range(iters + 1):
+            sync()
+            t0 = time.perf_counter()
+            engine.all_reduce(t)
+            engine.wait()
+            sync()
+            if i:
+                times.append(time.perf_counter() - t0)
+        ms = 1e3 * sorted(times)[len(times) // 2]
+        nbytes = t.numel() * esz
+        alg = nbytes / (ms * 1e-3) / 1e9
+        out.append({"mb": float(mb), "ms": round(ms, 4), "algbw_gbs": round(alg, 2),
+                    "busbw_gbs": round(alg * 2 * (n - 1) / max(n, 1), 2)})
+    return out
+
+
+def fit_latency_bandwidth(probe: Sequence[Dict[str, float]]) -> Tuple[float, float]:
+    """Least-squares fit of ``t = alpha + bytes / beta`` over the probe points: (alpha in ms,
+    beta in bytes per ms).  A degenerate fit falls back to the largest message's rate."""
+    xs = [p["mb"] * (1 << 20) for p in probe]
+    ys = [p["ms"] for p in probe]
+    k = len(xs)
+    mx, my = sum(xs) / k, sum(ys) / k
+    sxx = sum((x - mx) ** 2 for x in xs)
+    slope = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx if sxx > 0 else 0.0
+    if slope <= 0:
+        big = max(range(k), key=lambda i: xs[i])
+        return 0.0, xs[big] / max(ys[big], 1e-9)
+    return max(0.0, my - slope * mx), 1.0 / slope
+
+
+def auto_buckets(probe: Sequence[Dict[str, float]], total_mb: float) -> Tuple[float, float]:
+    """(first_bucket_mb, bucket_mb) from a probe.
+
+    A bucket of S bytes costs alpha + S / beta on the wire; its fixed part alpha is pure
+    overhead, which stays under ~1/8 of the bucket's time once S >= 8 alpha beta.  So
+    ``bucket_mb`` = 8 alpha beta, clamped to [4, 64] MB and to a quarter of the gradient (at
+    least four buckets to overlap with backward); the first bucket -- the one the backward's
+    first layers fill while every later bucket is still being computed -- is
+    max(1 MB, 2 alpha beta), at most half a bucket, so the first ring starts early."""
+    alpha, beta = fit_latency_bandwidth(probe)
+    knee_mb = alpha * beta / (1 << 20)
+    bucket = min(64.0, max(4.0, 8.0 * knee_mb), max(4.0, total_mb / 4.0))
+    first = min(bucket / 2.0, max(1.0, 2.0 * knee_mb))
+    return round(first, 2), round(bucket, 2)

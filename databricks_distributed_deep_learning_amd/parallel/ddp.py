@@ -83,7 +83,8 @@ class DataParallel(nn.Module):
                  bucket_mb: float = 25.0, first_bucket_mb: float = 4.0,
                  reduce_dtype: Optional[torch.dtype] = None, broadcast_buffers: bool = False,
                  accumulate_fp32: bool = False, process_group=None, broadcast_init: bool = True,
-                 comm: str = "auto", backward_passes_per_step: int = 1, shard: bool = False):
+                 comm: str = "auto", backward_passes_per_step: int = 1, shard: bool = False,
+                 split_tensors: bool = True):
         super().__init__()
         self.module = module
         self.arena = arena if arena is not None else ParamArena(list(module.named_parameters()))
@@ -119,10 +120,13 @@ class DataParallel(nn.Module):
             elif comm == "native":
                 raise RuntimeError("comm='native' needs CUDA tensors, the native library and the nccl backend")
         self.comm = "native" if self.native is not None else "torch"
-        if self.native is not None and hasattr(self.native, "world"):
-            from . import comm as _comm
-            _comm.set_active(self.native)   # SyncBatchNorm rides the same communicator
+        from . import comm as _comm
+        # SyncBatchNorm and the sharded optimizer's norm reductions ride the reducer's
+        # communicator; a reducer without one clears whatever an earlier reducer left active
+        _comm.set_active(self.native if (self.native is not None and hasattr(self.native, "world")) else None)
         self.shard = bool(shard) and self.world > 1
+        self.split_tensors = bool(split_tensors)
+        self._last_step: List[tuple] = []     # (bucket index, engine seq) of the last finished step
         if self.shard:
             unit = self.world * 64
             if self.arena.numel % unit:
@@ -153,19 +157,40 @@ class DataParallel(nn.Module):
 
     # ------------------------------------------------------------------
     def _build_buckets(self, bucket_mb: float, first_bucket_mb: float) -> List[Bucket]:
+        """Whole tensors per bucket, in arena order; a single tensor larger than two buckets
+        (BERT's 47 MB word embedding) is cut into bucket-sized pieces of its own
+        (``split_tensors``): they all launch when its gradient lands, and the per-bucket
+        optimizer starts on the first piece while the later ones are still on the wire.
+        Piece boundaries sit on the flat optimizer's 8192-element row grid (relative to the
+        tensor's start), so a range step updates whole rows."""
         esz = torch.empty((), dtype=self.reduce_dtype).element_size()
         buckets: List[Bucket] = []
         cap = int(first_bucket_mb * (1 << 20)) // esz
+        full = max(1, int(bucket_mb * (1 << 20)) // esz)
         cur: List[int] = []
         start = 0
-        for ei, e in enumerate(self.arena.entries):
+        ents = self.arena.entries
+        for ei, e in enumerate(ents):
+            nxt = ents[ei + 1].offset if ei + 1 < len(ents) else self.arena.numel
+            if self.split_tensors and e.numel > 2 * full:
+                if cur:                            # close the bucket in progress first
+                    buckets.append(Bucket(len(buckets), start, e.offset, cur))
+                    cur, start = [], e.offset
+                piece = -(-full // 8192) * 8192
+                a = start
+                while a < nxt:
+                    b = nxt if nxt - (a + piece) < piece // 2 else a + piece   # no tiny tail piece
+                    buckets.append(Bucket(len(buckets), a, b, [ei]))
+                    a = b
+                start = nxt
+                cap = full
+                continue
             end = e.offset + e.numel
             cur.append(ei)
             if end - start >= cap:
-                nxt = self.arena.entries[ei + 1].offset if ei + 1 < len(self.arena.entries) else self.arena.numel
                 buckets.append(Bucket(len(buckets), start, nxt, cur))
                 cur, start = [], nxt
-                cap = int(bucket_mb * (1 << 20)) // esz
+                cap = full
         if cur:
             buckets.append(Bucket(len(buckets), start, self.arena.numel, cur))
         return buckets
@@ -201,15 +226,37 @@ class DataParallel(nn.Module):
         return [(b.start, b.end) for b in self.buckets]
 
     def _install_gather_waits(self) -> None:
-        """Forward pre-hook per module with parameters: wait for the all-gathers of the
-        buckets holding them (stream waits, no host sync)."""
+        """Forward pre-hook per module: wait for the all-gathers of the buckets holding the
+        parameters its forward may read (stream waits, no host sync).
+
+        A fused op reads the parameters of modules whose own forward never runs (a
+        bottleneck block hands ``bn3`` / ``downsample.bn`` to ``conv_bn_add_bn``; ResNet's
+        stem and ViT's patch embedding are read by the root's forward), so a module waits for
+        its WHOLE subtree's buckets by default -- any parameter a forward can reach is in
+        its subtree.  Routers (the wrapped root, ``nn.Sequential`` / ``nn.ModuleList`` and
+        modules with ``_ddl_gather_router = True``) only dispatch to children whose own hooks
+        wait: they wait for their direct parameters plus the subtrees of the children named
+        in ``_ddl_direct_reads`` -- that keeps a model's all-gathers overlapped with its
+        forward instead of all waited for before the first layer."""
         index = {id(e.param): ei for ei, e in enumerate(self.arena.entries)}
-        for mod in self.module.modules():
+
+        def buckets_of(params):
             bks = set()
-            for prm in mod.parameters(recurse=False):
+            for prm in params:
                 ei = index.get(id(prm))
                 if ei is not None:
                     bks.update(self._entry_buckets.get(ei, []))
+            return bks
+
+        for mod in self.module.modules():
+            router = mod is self.module or isinstance(mod, (nn.Sequential, nn.ModuleList)) or \
+                bool(getattr(mod, "_ddl_gather_router", False))
+            if router:
+                bks = buckets_of(mod.parameters(recurse=False))
+                for name in getattr(mod, "_ddl_direct_reads", ()):
+                    bks |= buckets_of(getattr(mod, name).parameters())
+            else:
+                bks = buckets_of(mod.parameters())
             if bks:
                 need = sorted(bks)
                 self._prehooks.append(mod.register_forward_pre_hook(
@@ -384,14 +431,25 @@ class DataParallel(nn.Module):
                 self.arena.grad.zero_()
                 self._acc_active = True
 
-    def replica_fingerprint(self) -> torch.Tensor:
+    def replica_fingerprint(self, chunk: int = 1 << 22) -> torch.Tensor:
         """fp64 [sum, position-weighted sum] of this rank's parameter arena (2 numbers per
-        check; weighted so a permutation or a swapped bucket does not cancel out)."""
-        flat = self.arena.flat
+        check; weighted so a permutation or a swapped bucket does not cancel out).
+
+        Walked in ``chunk``-element pieces (fp32 partial sums per piece, accumulated in
+        fp64) with a period-4093 weight pattern built once, so a check costs a few MB of
+        scratch instead of an fp64 copy of the whole arena."""
+        flat = self.arena.flat.detach()
         n = flat.numel()
-        w = torch.arange(1, n + 1, device=flat.device, dtype=torch.float64).remainder_(4093.0).add_(1.0)
-        x = flat.detach().double()
-        return torch.stack([x.sum(), (x * w).sum()])
+        period = 4093
+        chunk = max(period, chunk - chunk % period)      # every piece starts on a weight period
+        base = torch.arange(1, chunk + 1, device=flat.device, dtype=torch.float32).remainder_(float(period)).add_(1.0)
+        s = torch.zeros((), dtype=torch.float64, device=flat.device)
+        ws = torch.zeros((), dtype=torch.float64, device=flat.device)
+        for lo in range(0, n, chunk):
+            x = flat[lo:lo + chunk].float()
+            s += x.sum(dtype=torch.float64)
+            ws += (x * base[:x.numel()]).sum(dtype=torch.float64)
+        return torch.stack([s, ws])
 
     def check_replicas(self, rtol: float = 0.0) -> None:
         """Debug / race check: data-parallel replicas must hold IDENTICAL parameters
@@ -428,6 +486,7 @@ class DataParallel(nn.Module):
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
+        self._last_step = [(b.index, b.seq) for b in self._order]
         if self.shard:
             for b in self.buckets:
                 if b.handle is not None:
@@ -487,9 +546,45 @@ class DataParallel(nn.Module):
             self._acc32.zero_()
         self._acc_active = False
 
+    def bucket_timings(self) -> List[dict]:
+        """Per bucket of the last finished step, in launch order: size, device time of its
+        collective on the comm stream (start -> done events of the native engine) and the bus
+        bandwidth that implies (x 2(n-1)/n for an all-reduce, (n-1)/n for a reduce-scatter).
+        Empty without the native engine (torch / gloo path) or before the first step.  Reads
+        events only: call it after the step's work has been synchronised."""
+        eng = self.native
+        if eng is None or not hasattr(eng, "collective_ms"):
+            return []
+        esz = torch.empty((), dtype=self.reduce_dtype).element_size()
+        n = max(1, self.world)
+        factor = (n - 1) / n if self.shard else 2 * (n - 1) / n
+        out = []
+        for bi, seq in self._last_step:
+            b = self.buckets[bi]
+            mb = (b.end - b.start) * esz / (1 << 20)
+            ms = eng.collective_ms(seq) if seq > 0 else -1.0
+            bus = (b.end - b.start) * esz * factor / (ms * 1e-3) / 1e9 if ms > 0 else None
+            out.append({"bucket": bi, "mb": round(mb, 2), "ms": round(ms, 4) if ms >= 0 else None,
+                        "busbw_gbs": round(bus, 1) if bus else None})
+        return out
+
     def bucket_sizes_mb(self) -> List[float]:
         esz = torch.empty((), dtype=self.reduce_dtype).element_size()
         return [(b.end - b.start) * esz / (1 << 20) for b in self.buckets]
+
+    def close(self, abort: bool = False) -> None:
+        """Release the reducer: remove its hooks and destroy its native communicator (which
+        also clears it as the process's active engine).  ``abort``: the failure path
+        (``ncclCommAbort``, no waiting on peers)."""
+        for h in self._hooks + self._prehooks:
+            h.remove()
+        self._hooks, self._prehooks = [], []
+        if self.native is not None and hasattr(self.native, "close"):
+            self.native.close(abort=abort)
+        from . import comm as _comm
+        if _comm.active() is self.native:
+            _comm.set_active(None)
+        self.native = None
 
     def state_dict(self, *a, **k):
         return self.module.state_dict(*a, **k)

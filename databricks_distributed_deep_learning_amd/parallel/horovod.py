@@ -20,7 +20,7 @@ from .launcher import Distributor
 
 Average = "average"
 Sum = "sum"
-Adasum = "adasum"  # accepted for API compatibility; implemented as Average
+Adasum = "adasum"  # scale-invariant pairwise combination (``adasum_combine``), not an average
 
 
 class HorovodRunner:
@@ -61,17 +61,65 @@ def _prep(t: torch.Tensor):
     return t, False
 
 
+def adasum_combine(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Horovod's Adasum of two gradients: ``(1 - a.b / 2|a|^2) a + (1 - a.b / 2|b|^2) b``.
+
+    Orthogonal gradients add, identical ones average, and the result does not change
+    when either input is scaled -- the property that lets Adasum keep the learning rate
+    of a single worker as the worker count grows.  Dot products in fp64."""
+    a64, b64 = a.double(), b.double()
+    dot = (a64 * b64).sum()
+    na, nb = (a64 * a64).sum(), (b64 * b64).sum()
+    ca = torch.where(na > 0, 1.0 - dot / (2.0 * na), torch.ones_like(na))
+    cb = torch.where(nb > 0, 1.0 - dot / (2.0 * nb), torch.ones_like(nb))
+    return (ca * a64 + cb * b64).to(a.dtype)
+
+
+def adasum_tree(parts) -> torch.Tensor:
+    """Adasum over ranks in Horovod's recursive-doubling order: (0,1), (2,3), ... then
+    the pairs of pairs; an odd one out is carried up a level unchanged."""
+    parts = list(parts)
+    while len(parts) > 1:
+        parts = [adasum_combine(parts[i], parts[i + 1]) if i + 1 < len(parts) else parts[i]
+                 for i in range(0, len(parts), 2)]
+    return parts[0]
+
+
+def _gather_rows(t: torch.Tensor) -> torch.Tensor:
+    """[world, numel] copy of every rank's flat ``t`` (rank order)."""
+    flat = t.reshape(-1).contiguous()
+    out = torch.empty((size(), flat.numel()), dtype=flat.dtype, device=flat.device)
+    dist.all_gather_into_tensor(out, flat) if flat.is_cuda else dist.all_gather(list(out.unbind(0)), flat)
+    return out
+
+
+def adasum_allreduce(tensor: torch.Tensor, segments: Optional[Iterable] = None) -> torch.Tensor:
+    """Adasum of ``tensor`` over all ranks, identical on every rank (each rank combines the
+    gathered copies in the same order).  ``segments`` = (offset, numel) ranges combined
+    independently (Horovod applies Adasum per tensor); default: the whole tensor."""
+    rows = _gather_rows(tensor)
+    flat = rows[0].clone()
+    for off, n in (segments or [(0, flat.numel())]):
+        flat[off:off + n] = adasum_tree([rows[r, off:off + n] for r in range(rows.shape[0])])
+    return flat.view_as(tensor)
+
+
 def allreduce(tensor: torch.Tensor, average: Optional[bool] = None, name: Optional[str] = None,
               op: str = Average) -> torch.Tensor:
     if average is not None:
         op = Average if average else Sum
+    if op not in (Average, Sum, Adasum):
+        raise ValueError(f"unknown reduction op {op!r}")
     out = tensor.detach().clone()
     if size() == 1:
         return out
     t, moved = _prep(out)
-    dist.all_reduce(t)
-    if op in (Average, Adasum):
-        t.div_(size())
+    if op == Adasum:
+        t = adasum_allreduce(t)
+    else:
+        dist.all_reduce(t)
+        if op == Average:
+            t.div_(size())
     return t.to(tensor.device) if moved else t
 
 
@@ -144,24 +192,43 @@ class _DistributedOptimizer:
 
         class _Holder(torch.nn.Module):
             pass
+        if op not in (Average, Sum, Adasum):
+            raise ValueError(f"unknown reduction op {op!r}")
+        self.op = op
+        self.backward_passes_per_step = backward_passes_per_step
+        if op == Adasum:
+            # Adasum needs every rank's whole gradient of a tensor at once (its dot products):
+            # gradients accumulate locally in the arena and are combined per tensor at step()
+            self.arena.rebind_grads()
+            self._reducer = None
+            return
         # backward_passes_per_step = k: each gradient is all-reduced on its k-th arrival
         # (the reducer counts per parameter, as Horovod does); passes 1..k-1 accumulate
         # locally into the arena and launch nothing
         self._reducer = DataParallel(_Holder(), arena=self.arena, bucket_mb=bucket_mb, broadcast_init=False,
                                      backward_passes_per_step=backward_passes_per_step)
-        self.backward_passes_per_step = backward_passes_per_step
-        self.op = op
 
     @property
     def param_groups(self):
         return self.optimizer.param_groups
 
     def zero_grad(self, set_to_none: bool = False) -> None:
-        self._reducer.zero_grad()
+        if self._reducer is None:
+            self.arena.zero_grad()
+        else:
+            self._reducer.zero_grad()
 
     def synchronize(self) -> None:
+        if self._reducer is None:       # Adasum: per-tensor combination of the gathered gradients
+            self.arena.rebind_grads()   # gradients a set_to_none zero_grad detached from the arena
+            if size() > 1:
+                g, moved = _prep(self.arena.grad)
+                segs = [(e.offset, e.numel) for e in self.arena.entries]
+                out = adasum_allreduce(g, segs)
+                self.arena.grad.copy_(out.to(self.arena.grad.device) if moved else out)
+            return
         self._reducer.finish()
-        if self.op in (Average, Adasum) and size() > 1:
+        if self.op == Average and size() > 1:
             self.arena.grad.mul_(1.0 / size())
 
     def step(self, closure=None):

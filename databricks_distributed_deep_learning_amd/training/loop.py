@@ -61,9 +61,20 @@ class Trainer:
         self.arena = ParamArena(list(model.named_parameters()), pad_multiple=self.world * 64 if zero else 1)
         accumulate_fp32 = cfg.grad_accum > 1 and self.dtype != torch.float32
         rd = {"auto": None, "fp32": torch.float32, "bf16": torch.bfloat16}[cfg.grad_reduce_dtype]
-        self.ddp = DataParallel(model, self.arena, bucket_mb=cfg.bucket_mb, first_bucket_mb=cfg.first_bucket_mb,
+        comm, self.comm_probe = self._comm_engine(rd)
+        bucket_mb, first_mb = cfg.bucket_mb, cfg.first_bucket_mb
+        if bucket_mb <= 0:      # "auto": sized from the probe (fixed defaults without one)
+            from ..parallel.comm import auto_buckets
+            esz = torch.empty((), dtype=rd or self.arena.dtype).element_size()
+            first_mb, bucket_mb = auto_buckets(self.comm_probe, self.arena.numel * esz / 2 ** 20) \
+                if self.comm_probe else (4.0, 25.0)
+        self.bucket_policy = {"bucket_mb": bucket_mb, "first_bucket_mb": first_mb,
+                              "source": "probe" if cfg.bucket_mb <= 0 and self.comm_probe else "config"}
+        # LAMB's trust ratio needs every tensor whole in one optimizer range: no split tensors
+        self.ddp = DataParallel(model, self.arena, bucket_mb=bucket_mb, first_bucket_mb=first_mb,
                                 reduce_dtype=rd, broadcast_buffers=cfg.broadcast_buffers,
-                                accumulate_fp32=accumulate_fp32, comm=cfg.comm, shard=zero)
+                                accumulate_fp32=accumulate_fp32, comm=comm, shard=zero,
+                                split_tensors=cfg.resolved_optimizer != "lamb")
         # ZeRO-1: the optimizer owns chunk `rank` of every reduce-scattered bucket and hands its
         # updated chunks back through the reducer's overlapped per-bucket all-gathers
         self.opt = build_optimizer(cfg.resolved_optimizer, self.arena, cfg,
@@ -89,6 +100,28 @@ class Trainer:
             self.step = int(meta["step"])
 
     # ------------------------------------------------------------------
+    def _comm_engine(self, reduce_dtype):
+        """(comm argument for DataParallel, probe results).  With several ranks on GPUs and
+        the native engine available, the engine is created here so it can be probed
+        (``parallel.comm.probe_allreduce``: 1 / 4 / 16 / 64 MB all-reduces, bus GB/s) before
+        the buckets are laid out -- ``bucket_mb <= 0`` sizes them from the probe."""
+        c = self.cfg
+        if self.world == 1 or c.comm not in ("auto", "native") or self.device.type != "cuda":
+            return c.comm, []
+        from ..parallel.comm import CommError, NativeComm, native_available, probe_allreduce
+        if not native_available():
+            return c.comm, []
+        try:
+            eng = NativeComm()
+        except CommError:
+            if c.comm == "native":
+                raise
+            return "torch", []
+        probe = []
+        if c.comm_probe or c.bucket_mb <= 0:
+            probe = probe_allreduce(eng, self.device, dtype=reduce_dtype or self.arena.dtype, world=self.world)
+        return eng, probe
+
     def _make_loader(self):
         c = self.cfg
         if self.task == "cv":
@@ -187,6 +220,11 @@ class Trainer:
                 return
             self.train_step()
 
+    def close(self) -> None:
+        """Release the reducer's hooks and native communicator (the next Trainer in this
+        process -- bench.py runs two -- then starts from a clean active-engine slot)."""
+        self.ddp.close()
+
     def _abort_comm(self) -> None:
         """Failure path: abort the native RCCL communicator so collectives blocked on a
         dead peer return and this rank exits instead of hanging until the timeout."""
@@ -276,7 +314,13 @@ class Trainer:
             "final_loss": last_loss, "native": ops.native_mode(),
             "buckets_mb": [round(b, 2) for b in self.ddp.bucket_sizes_mb()],
             "comm": self.ddp.comm, "phases_ms": {k: round(v, 3) for k, v in phases.items()},
+            "bucket_policy": self.bucket_policy,
         }
+        if self.comm_probe:
+            summary["comm_probe"] = self.comm_probe
+        timings = self.ddp.bucket_timings()       # the last step's rings (synchronised by the barrier above)
+        if timings:
+            summary["comm_buckets"] = timings
         summary.update(memory_stats(self.device))
         if c.checkpoint_dir and not c.checkpoint_every:
             self.save_checkpoint()
@@ -291,7 +335,9 @@ def train(cfg: Optional[TrainConfig] = None, **overrides) -> Dict[str, Any]:
     """Notebook-style entry point.  ``train(get_preset("resnet50_ddp"), steps=20)``."""
     cfg = (cfg or TrainConfig()).replace(**overrides) if overrides else (cfg or TrainConfig())
     trainer = Trainer(cfg)
-    return trainer.run()
+    out = trainer.run()
+    trainer.close()
+    return out
 
 
 def main(argv=None) -> int:

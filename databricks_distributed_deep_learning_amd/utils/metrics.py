@@ -67,9 +67,13 @@ class PhaseTimer:
     gradient all-reduces after its own backward work -- the EXPOSED communication.
     On the CPU marks are host clock readings."""
 
-    def __init__(self, device: torch.device, enabled: bool = True):
+    def __init__(self, device: torch.device, enabled: bool = True, max_pending: int = 64):
         self.cuda = device.type == "cuda"
         self.enabled = enabled
+        # steps whose marks may wait for summary(); beyond it end_step() folds the oldest
+        # FINISHED steps into the totals (an event query, never a sync) and recycles their
+        # events, so a long run without log points keeps a bounded event / host footprint
+        self.max_pending = max(1, int(max_pending))
         self._pending: list = []       # per step: [(name, event or time), ...]
         self._cur: list = []
         self._pool: list = []          # resolved events, re-recorded by later marks
@@ -94,21 +98,32 @@ class PhaseTimer:
     def end_step(self) -> None:
         if self.enabled and len(self._cur) > 1:
             self._pending.append(self._cur)
+            if len(self._pending) > self.max_pending:
+                self._resolve(only_finished=True)
         self._cur = []
 
-    def _resolve(self) -> None:
-        for marks in self._pending:
-            for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
-                if self.cuda:
-                    b.synchronize()
-                    ms = a.elapsed_time(b)
-                else:
-                    ms = 1000.0 * (b - a)
-                self.totals[name] = self.totals.get(name, 0.0) + ms
+    def _fold(self, marks) -> None:
+        for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
             if self.cuda:
-                self._pool.extend(e for _, e in marks)
-            self.steps += 1
-        self._pending = []
+                b.synchronize()
+                ms = a.elapsed_time(b)
+            else:
+                ms = 1000.0 * (b - a)
+            self.totals[name] = self.totals.get(name, 0.0) + ms
+        if self.cuda:
+            self._pool.extend(e for _, e in marks)
+        self.steps += 1
+
+    def _resolve(self, only_finished: bool = False) -> None:
+        """Fold pending steps into the totals, oldest first; ``only_finished``: stop at the
+        first step whose last event has not completed (no host wait)."""
+        n = 0
+        for marks in self._pending:
+            if only_finished and self.cuda and not marks[-1][1].query():
+                break
+            self._fold(marks)
+            n += 1
+        self._pending = self._pending[n:]
 
     def summary(self, reset: bool = False) -> Dict[str, float]:
         """Mean milliseconds per step of each phase since the last reset."""

@@ -199,3 +199,72 @@ def test_eager_optimizer_matches_post_backward_step(pg, preset, over):
         del t
     for a, b in zip(*finals):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
+
+
+def test_engine_sequence_numbers_and_inplace_all_gather(pg):
+    """ZeRO-1's engine contract at world 1: reduce-scatter / all-gather / all-reduce share one
+    increasing sequence, wait_upto(seq) orders the compute stream after THAT collective, and an
+    all-gather whose send buffer is its own slice of recv (the in-place flat[lo:hi] ->
+    flat[a:b] gather of DataParallel.gather_params) leaves the data intact."""
+    from databricks_distributed_deep_learning_amd.parallel.comm import NativeComm
+    c = NativeComm(timeout_s=0)
+    flat = torch.randn(4096, device=pg, dtype=torch.bfloat16)
+    want = flat.clone()
+    s1 = c.reduce_scatter(flat[:1024].clone(), torch.empty(1024, device=pg, dtype=torch.bfloat16))
+    s2 = c.all_gather(flat[1024:2048], flat[1024:2048])       # send is recv itself (world 1: its own slice)
+    s3 = c.all_reduce(flat[2048:])
+    assert 0 < s1 < s2 < s3
+    c.wait_upto(s2)
+    torch.testing.assert_close(flat[1024:2048], want[1024:2048])
+    c.wait_upto(s3)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(flat, want)
+    # per-collective device time from the engine's start / done events
+    assert all(c.collective_ms(s) >= 0 for s in (s1, s2, s3))
+    assert c.collective_ms(s3 + 5) == -1.0
+    c.close()
+
+
+def test_watchdog_aborts_on_async_error(pg):
+    """An RCCL asynchronous error (injected: what a peer failure looks like) is seen by the
+    watchdog within seconds; the communicator is aborted and the next call raises CommError."""
+    import time
+    from databricks_distributed_deep_learning_amd.parallel.comm import CommError, NativeComm
+    c = NativeComm(timeout_s=30, poll_s=0.05)
+    x = torch.ones(1024, device=pg)
+    c.all_reduce(x)
+    c.wait()
+    torch.cuda.synchronize()
+    assert c.poll() is None and c.failed is None
+    t0 = time.time()
+    c.inject_error(6)            # ncclRemoteError
+    while c.failed is None and time.time() - t0 < 10:
+        time.sleep(0.02)
+    assert c.failed and "asynchronous error 6" in c.failed, c.failed
+    assert time.time() - t0 < 5
+    with pytest.raises(CommError):
+        c.all_reduce(x)
+    c.close()
+
+
+def test_engine_probe_and_bucket_timings(pg):
+    """The startup probe runs on the engine, and the reducer reports per-bucket ring times of
+    the last step (world 1: every number exists, bus bandwidth is 0 by the 2(n-1)/n factor)."""
+    from databricks_distributed_deep_learning_amd.models import resnet18
+    from databricks_distributed_deep_learning_amd.optim.arena import ParamArena
+    from databricks_distributed_deep_learning_amd.parallel.comm import NativeComm, auto_buckets, probe_allreduce
+    from databricks_distributed_deep_learning_amd.parallel.ddp import DataParallel
+    c = NativeComm(timeout_s=0)
+    probe = probe_allreduce(c, pg, sizes_mb=(1, 4), iters=3, world=1)
+    assert [p["mb"] for p in probe] == [1.0, 4.0] and all(p["ms"] > 0 for p in probe)
+    first, bucket = auto_buckets(probe, 44.0)
+    assert 1.0 <= first <= bucket <= 64.0
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).to(pg)
+    ddp = DataParallel(m, ParamArena(list(m.named_parameters())), bucket_mb=bucket, first_bucket_mb=first, comm=c)
+    m(torch.randn(2, 32, 32, 3, device=pg)).float().square().mean().backward()
+    ddp.finish()
+    torch.cuda.synchronize()
+    t = ddp.bucket_timings()
+    assert len(t) == len(ddp.buckets) and all(r["ms"] is not None and r["ms"] >= 0 for r in t), t
+    ddp.close()

@@ -378,3 +378,104 @@ def test_zero1_reduce_scatter_matches_replicated(opt_name, accum):
     out = Distributor(num_processes=2, use_gpu=False).run(_zero_rs_equivalence, opt_name, accum)
     assert out["err"] < 1e-5, out
     assert out["nbuckets"] > 1 and out["local"] * 2 == out["arena"] and out["sd"] == out["arena"], out
+
+
+# ---------------------------------------------------------------- comm probe / bucket policy
+def _probe_and_buckets():
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.parallel.comm import auto_buckets, probe_allreduce
+    eng = _GlooEngine()
+    probe = probe_allreduce(eng, "cpu", sizes_mb=(0.25, 1, 4), iters=3, dtype=torch.float32)
+    first, bucket = auto_buckets(probe, total_mb=200.0)
+    return {"probe": probe, "first": first, "bucket": bucket, "calls": len(eng.calls), "world": dist.get_world_size()}
+
+
+def test_comm_probe_drives_auto_buckets_gloo():
+    out = Distributor(num_processes=2, use_gpu=False).run(_probe_and_buckets)
+    assert out["calls"] == 3 * 4 and [p["mb"] for p in out["probe"]] == [0.25, 1.0, 4.0], out
+    assert all(p["ms"] > 0 and p["busbw_gbs"] > 0 for p in out["probe"]), out
+    assert 1.0 <= out["first"] <= out["bucket"] / 2 + 1e-9 and 4.0 <= out["bucket"] <= 64.0, out
+
+
+def test_auto_buckets_from_latency_bandwidth_model():
+    from databricks_distributed_deep_learning_amd.parallel.comm import auto_buckets, fit_latency_bandwidth
+    # t = 0.02 ms + S / beta with alpha * beta = 2 MiB (~105 GB/s): 16 MB buckets, 4 MB first bucket
+    beta = 2 ** 21 / 0.02
+    probe = [{"mb": mb, "ms": 0.02 + mb * 2 ** 20 / beta} for mb in (1, 4, 16, 64)]
+    a, b = fit_latency_bandwidth(probe)
+    assert abs(a - 0.02) < 1e-6 and abs(b / beta - 1) < 1e-6
+    assert auto_buckets(probe, total_mb=218.0) == (4.0, 16.0)
+    # a small model caps buckets at a quarter of its gradient (>= 4 MB)
+    assert auto_buckets(probe, total_mb=20.0) == (2.5, 5.0)
+    # latency-free links: floor of 4 MB buckets, 1 MB first bucket
+    flat = [{"mb": mb, "ms": mb * 2 ** 20 / beta} for mb in (1, 4, 16, 64)]
+    assert auto_buckets(flat, total_mb=500.0) == (1.0, 4.0)
+
+
+def test_watchdog_fails_engine_within_seconds():
+    import time
+    from databricks_distributed_deep_learning_amd.parallel.comm import CommWatchdog
+
+    class Eng:
+        def __init__(self):
+            self.err, self.failed, self.polls = None, None, 0
+
+        def poll(self):
+            self.polls += 1
+            return self.err
+
+        def fail(self, reason):
+            self.failed = reason
+
+    e = Eng()
+    wd = CommWatchdog(e, interval=0.02)
+    time.sleep(0.1)
+    assert e.failed is None and e.polls > 1
+    t0 = time.time()
+    e.err = "RCCL asynchronous error 6 on rank 1"
+    while e.failed is None and time.time() - t0 < 5:
+        time.sleep(0.01)
+    assert e.failed == e.err and time.time() - t0 < 2
+    wd.stop()
+    assert wd.reason == e.err
+
+
+def _split_bucket_equivalence(opt_name):
+    """A tensor larger than two buckets is cut into bucket-sized pieces (BERT's word embedding):
+    the pieces all-reduce separately and the per-bucket optimizer ranges still give the same
+    update as replicated full-batch training."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.optim import ParamArena
+    from databricks_distributed_deep_learning_amd.optim.flat import FlatAdamW, FlatSGD
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    rank, world = dist.get_rank(), dist.get_world_size()
+    cls = {"sgd": FlatSGD, "adamw": FlatAdamW}[opt_name]
+    finals, layout = [], None
+    for split in (False, True):
+        torch.manual_seed(3)
+        emb = torch.nn.Embedding(600, 64)          # 38400 elements: > 2 x 16384-element buckets
+        head = torch.nn.Linear(64, 5)
+        model = torch.nn.ModuleDict({"emb": emb, "head": head})
+        arena = ParamArena(list(model.named_parameters()))
+        ddp = DataParallel(model, arena, bucket_mb=16384 * 4 / 2 ** 20, first_bucket_mb=0.001, split_tensors=split)
+        opt = cls(arena, lr=0.05)
+        ids = torch.randint(0, 600, (8, 12), generator=torch.Generator().manual_seed(7 + rank))
+        for _ in range(2):
+            ddp.zero_grad()
+            head(emb(ids).mean(1)).square().mean().backward()
+            opt.begin_step()
+            ddp.finish(on_ready=lambda g, lo, hi: opt.step_range(g, 1.0 / world, lo, hi))
+            opt.end_step()
+        finals.append(torch.cat([p.detach().flatten() for p in model.parameters()]))
+        if split:
+            layout = [(b.start, b.end, b.entry_ids) for b in ddp.buckets]
+    return {"err": (finals[0] - finals[1]).abs().max().item(), "layout": layout}
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adamw"])
+def test_split_tensor_buckets_match(opt_name):
+    out = Distributor(num_processes=2, use_gpu=False).run(_split_bucket_equivalence, opt_name)
+    pieces = [b for b in out["layout"] if len(b[2]) == 1 and b[1] - b[0] >= 8192]
+    assert len(pieces) >= 2, out["layout"]
+    assert all((b[0] - pieces[0][0]) % 8192 == 0 for b in pieces), out["layout"]
+    assert out["err"] < 1e-6, out

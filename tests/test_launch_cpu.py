@@ -199,3 +199,54 @@ def test_replica_divergence_check(corrupt):
         assert out.startswith("caught: rank 0"), out
     else:
         assert out == "ok"
+
+
+def test_adasum_combine_properties():
+    """Adasum (Horovod): orthogonal gradients add, identical ones are returned unchanged, and
+    scaling one input does not change the other's coefficient's sign / the result's direction."""
+    from databricks_distributed_deep_learning_amd.parallel.horovod import adasum_combine, adasum_tree
+    a = torch.tensor([1.0, 0.0, 0.0])
+    b = torch.tensor([0.0, 2.0, 0.0])
+    assert torch.allclose(adasum_combine(a, b), a + b)
+    assert torch.allclose(adasum_combine(a, a), a)
+    c = torch.tensor([3.0, 1.0, -2.0])
+    d = torch.tensor([1.0, -1.0, 0.5])
+    ref = (1 - c @ d / (2 * c @ c)) * c + (1 - c @ d / (2 * d @ d)) * d
+    assert torch.allclose(adasum_combine(c, d), ref, atol=1e-6)
+    # a zero gradient leaves the other one unchanged
+    assert torch.allclose(adasum_combine(torch.zeros(3), d), d)
+    # tree order: ((0,1),(2,3)); an odd rank is carried up a level
+    p = [torch.randn(5, generator=torch.Generator().manual_seed(i)) for i in range(3)]
+    assert torch.allclose(adasum_tree(p), adasum_combine(adasum_combine(p[0], p[1]), p[2]))
+
+
+def _hvd_adasum():
+    from databricks_distributed_deep_learning_amd.parallel import hvd
+    from databricks_distributed_deep_learning_amd.parallel.horovod import adasum_combine
+    hvd.init()
+    r = hvd.rank()
+    g = [torch.randn(7, generator=torch.Generator().manual_seed(40 + k)) for k in range(2)]
+    red = hvd.allreduce(g[r], op=hvd.Adasum)
+    err_t = (red - adasum_combine(g[0], g[1])).abs().max().item()
+    # DistributedOptimizer(op=Adasum): per-tensor Adasum of the two ranks' gradients
+    torch.manual_seed(3)
+    m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 2))
+    x = torch.randn(8, 6, generator=torch.Generator().manual_seed(9))
+    grads = []
+    for k in range(2):
+        m.zero_grad()
+        m(x[4 * k:4 * k + 4]).square().sum().backward()
+        grads.append([p.grad.clone() for p in m.parameters()])
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), named_parameters=m.named_parameters(),
+                                   op=hvd.Adasum)
+    opt.zero_grad()
+    m(x[4 * r:4 * r + 4]).square().sum().backward()
+    opt.synchronize()
+    err_o = max((p.grad - adasum_combine(grads[0][i], grads[1][i])).abs().max().item()
+                for i, p in enumerate(m.parameters()))
+    return err_t, err_o
+
+
+def test_horovod_adasum_world2():
+    res = HorovodRunner(np=2, use_gpu=False).run(_hvd_adasum)
+    assert res[0] < 1e-6 and res[1] < 1e-5, res

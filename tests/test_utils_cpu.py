@@ -53,3 +53,19 @@ def test_transposed_weight_cache_follows_flat_optimizer():
         opt.step()
         opt.load_state_dict(st)           # weights restored from the master copy
         assert torch.equal(_transposed(lin.weight, lin.weight), lin.weight.t())
+
+
+def test_phase_timer_pending_is_bounded():
+    """Without log points the pending marks are folded once max_pending steps accumulate, and
+    the summary still averages over every step."""
+    import torch
+    from databricks_distributed_deep_learning_amd.utils.metrics import PhaseTimer
+    pt = PhaseTimer(torch.device("cpu"), max_pending=4)
+    for _ in range(10):
+        pt.begin()
+        pt.mark("fwd")
+        pt.mark("bwd")
+        pt.end_step()
+        assert len(pt._pending) <= 4
+    out = pt.summary(reset=True)
+    assert pt.steps == 0 and set(out) == {"fwd_ms", "bwd_ms"}
