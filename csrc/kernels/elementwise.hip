@@ -423,6 +423,23 @@ __global__ __launch_bounds__(256) void acc_f32_k(T* __restrict__ dst, const floa
         dst[i] = from_f<T>(to_f(dst[i]) + src[i]);
 }
 
+// Gradient-accumulation drain (micro-step of grad_accum): acc (fp32) += g; g = 0 -- one pass
+// over the arena instead of an ATen add plus a zero fill; 8 elements per thread per
+// iteration (16-byte gradient loads / stores, two float4 on the accumulator).
+template <typename T>
+__global__ __launch_bounds__(256) void drain_acc_k(float* __restrict__ acc, T* __restrict__ g, long n8) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        float v[8], a[8];
+        load8(g + i * 8, v);
+        load8(acc + i * 8, a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += v[e];
+        store8(acc + i * 8, a);
+        const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        store8(g + i * 8, z);
+    }
+}
+
 #define DISPATCH_T(dtype, KERNEL_CALL_BF16, KERNEL_CALL_F32) \
     do { if ((dtype) == 1) { KERNEL_CALL_BF16; } else { KERNEL_CALL_F32; } } while (0)
 
@@ -670,6 +687,16 @@ DDL_API int ddl_acc_f32(int dtype, void* dst, const float* src, long n, hipStrea
     const int g = (int)std::min<long>(1024, (n + 255) / 256);
     DISPATCH_T(dtype, (acc_f32_k<bf16_t><<<g, 256, 0, st>>>((bf16_t*)dst, src, n)),
                (acc_f32_k<float><<<g, 256, 0, st>>>((float*)dst, src, n)));
+    DDL_RETURN_LAUNCH();
+}
+
+// acc (fp32) += g (bf16 / fp32); g = 0.  n % 8 == 0, 16-byte aligned buffers.
+DDL_API int ddl_drain_acc(int dtype, float* acc, void* g, long n, hipStream_t st) {
+    if (n % 8) return -1;
+    const long n8 = n / 8;
+    const int grid = (int)std::min<long>(4096, (n8 + 255) / 256);
+    DISPATCH_T(dtype, (drain_acc_k<bf16_t><<<grid, 256, 0, st>>>(acc, (bf16_t*)g, n8)),
+               (drain_acc_k<float><<<grid, 256, 0, st>>>(acc, (float*)g, n8)));
     DDL_RETURN_LAUNCH();
 }
 

@@ -954,7 +954,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             sa.stage(p, smem, 1, 0, kt0 + 1);
             sb.stage(p, smem, 1, 0, kt0 + 1);
             sb.stage(p, smem, 1, 1, kt0 + 1);
+#if DDL_DEEP_RETIRE
+            VMN(10);      // E-A0 / E-B0 only: E-B1 / E-A1 are retired at phases 1 / 2 (vm_younger)
+#else
             VM6();
+#endif
         } else {
             VM0();
         }
@@ -1019,7 +1023,6 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // odd tile count: the last E tile (its E-B1 / E-A1 retired at phases 1 / 2)
             if (nK & 1) phasesE(kt_end - 1, false, false, pm, cm, false, 0, false);
 #else
-            const int pairs = nK / 2;
             for (int it = 0; it < pairs; ++it) {
                 KSTAMP(it);
                 const int kE = kt0 + 2 * it, kO = kE + 1;

@@ -128,6 +128,7 @@ _SIGS = {
     "ddl_conv_w_dgrad_batch": [P, P, I, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
     "ddl_acc_f32": [I, P, P, L, P],
+    "ddl_drain_acc": [I, P, P, L, P],
     "ddl_softmax_topk": [I, P, L, I, I, P, P, P, P],
     "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],
     "ddl_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, I, P],

@@ -36,6 +36,7 @@ def set_big_gemm(enabled: bool) -> None:
 
 
 _forced: Optional[str] = None
+_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow")
 # per-call device timing for diagnostics (scripts/debug/gemm_trace.py): list of
 # (signature, (kernel, splits), start event, end event) while enabled
 _trace: Optional[list] = None
@@ -51,7 +52,7 @@ def trace(enabled: bool = True) -> Optional[list]:
 
 @contextlib.contextmanager
 def force_kernel(kind: Optional[str]):
-    """Route every GEMM inside the block to one kernel kind ("big", "small", "blas", ... -- see ``gemm``)."""
+    """Route every GEMM inside the block to one kernel kind ("big", "small", ... -- see ``gemm``)."""
     global _forced
     prev, _forced = _forced, kind
     try:
@@ -109,18 +110,6 @@ _HYBRID = os.environ.get("DDL_GEMM_HYBRID", "1") != "0"   # tuner candidate (A/B
 # one and the whole-round grid buys nothing.  DDL_GEMM_192=1 offers it (forcing: kernel="big192").
 _BIG192 = os.environ.get("DDL_GEMM_192", "0") == "1"
 _DIRECT = os.environ.get("DDL_GEMM_DIRECT", "1") != "0"    # gemm_big.hip register epilogue (big192 needs it)
-# tuner candidate "blas": hipBLASLt (torch.mm / addmm) for the plain library GEMMs -- NT / NN, bf16,
-# no epilogue beyond a bf16 bias OR a residual (its bias epilogue / beta = 1).  It runs only where the
-# tuner measures it faster than every native candidate (profiles/tn_wgrad_vs_hipblaslt.log: e.g. NT
-# 16384x768x3072 60.8 vs 68.7 us, NT 25216x768x768 36.9 vs 51.7 us); the fused GELU / dGELU /
-# BatchNorm / statistics epilogues and the weight gradients stay native.  Opt-in (DDL_GEMM_BLAS=1):
-# BERT-base runs with it are ~1 % faster in most processes, but 4 of 15 same-box runs came out 4-20 %
-# slower across the whole step (forward AND backward), never seen in 9 runs without it
-# (profiles/ab_r03.md) -- a single benchmark run is better served by the steady native plan.
-_BLAS = os.environ.get("DDL_GEMM_BLAS", "0") == "1"
-_plan_call = False      # set while plan() tunes a signature (no "blas" candidate then)
-
-
 def hybrid_rows(M: int, N: int, K: int):
     """Row split of a 256x256-tile GEMM whose tile grid ends in a partial round, or None.
 
@@ -148,41 +137,10 @@ def _at(t, off: int):
     return None if t is None else t.as_strided((1,), (1,), t.storage_offset() + off)
 
 
-def blas_ok(mode: int, C, bias, act, aux, conv_arr, row_remap, residual, colstats=None, bnb=None) -> bool:
-    """Whether a GEMM call is a plain library GEMM hipBLASLt can run unchanged (the "blas" kind)."""
-    return (mode in (MODE_NT, MODE_NN) and C.dtype == torch.bfloat16 and act is None and aux is None
-            and conv_arr is None and not row_remap and colstats is None and bnb is None
-            and not (bias is not None and residual is not None)
-            and (bias is None or (bias.dtype == C.dtype and bias.dim() == 1)))
-
-
-def _blas(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, residual, accumulate) -> None:
-    """C[M, N] (row stride ldc) = A op(B) (+ bias | + residual) through torch.mm / addmm (hipBLASLt);
-    A is [M, K] (lda), B is [N, K] (NT) or [K, N] (NN) with row stride ldb -- the native layouts."""
-    a = A.as_strided((M, K), (lda, 1))
-    b = B.as_strided((N, K), (ldb, 1)).t() if mode == MODE_NT else B.as_strided((K, N), (ldb, 1))
-    c = C.as_strided((M, N), (ldc, 1))
-    r = None if residual is None else residual.as_strided((M, N), (ldc, 1))
-    if accumulate or (r is not None and r.data_ptr() == c.data_ptr()):
-        c.addmm_(a, b)
-        extra = bias if bias is not None else (r if accumulate else None)
-        if extra is not None:
-            c.add_(extra)
-    elif bias is not None:
-        torch.addmm(bias, a, b, out=c)
-    elif r is not None:
-        torch.addmm(r, a, b, out=c)
-    else:
-        torch.mm(a, b, out=c)
-
-
 def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr,
             row_remap, residual, accumulate, colstats=None, bnb=None) -> None:
-    if kind == "blas":
-        if blas_ok(mode, C, bias, act, aux, conv_arr, row_remap, residual, colstats, bnb):
-            _blas(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, residual, accumulate)
-            return
-        # a cached choice reused by a call the library cannot express (e.g. an fp32 bias)
+    if kind not in _KINDS:
+        # a cached plan entry from another build (e.g. the removed hipBLASLt candidate)
         kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)
     if kind == "hybrid":
         # rows [0, M1): whole rounds of unsplit tiles; rows [M1, M): split-K s over the chip
@@ -268,6 +226,7 @@ _tuned: dict = {}
 _timings: dict = {}
 _NARROW_STATS = os.environ.get("DDL_TUNE_NARROW_STATS", "0") != "0"   # same-box A/B neutral: off
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
+_TUNE_ROUNDS = max(1, int(os.environ.get("DDL_GEMM_TUNE_ROUNDS", "5")))   # interleaved timing rounds per candidate
 # optional persistent cache (JSON): later processes skip the timing runs
 _CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
 
@@ -367,8 +326,6 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
         if _NARROW_STATS and N % 64 == 0 and ("narrow", 1) not in cands:
             cands.append(("narrow", 1))
         cs_s = torch.empty_like(colstats)
-    if _BLAS and not _plan_call and blas_ok(mode, C, bias, act, aux, conv_arr, row_remap, residual, colstats, bnb):
-        cands = cands + [("blas", 1)]
     if len(cands) == 1:
         _timings[key] = {cands[0]: 0.0}
         return cands[0]
@@ -376,31 +333,25 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     aux_s = aux
     if aux is not None and act in ("gelu", "relu", "tanh"):   # aux is an output for these
         aux_s = torch.empty_like(aux)
-    timed = []
+    runs = []
     for kind, s in cands:
-        run = lambda: _launch(kind, s, mode, A, lda, B, ldb, Cs, ldc, M, N, K, bias, act, aux_s,  # noqa: E731
-                              conv_arr, row_remap, residual, False, cs_s, bnb)
-        run()
-        t = _time_runs(run, 2)
-        if t < 0.25:                      # short kernels: average more runs (timer noise)
-            reps = min(24, max(4, int(1.0 / max(t, 1e-3))))
-            t = _time_runs(run, reps)
-        timed.append((t, kind, s))
-    timed.sort()
-    _timings[key] = {(kind, s): t for t, kind, s in timed}
-    if len(timed) > 1 and timed[1][0] < 1.15 * timed[0][0]:
-        # a close call: re-time the two leaders with more runs before committing
-        final = []
-        for _, kind, s in timed[:2]:
-            run = lambda: _launch(kind, s, mode, A, lda, B, ldb, Cs, ldc, M, N, K, bias, act, aux_s,  # noqa: E731
-                                  conv_arr, row_remap, residual, False, cs_s, bnb)
-            reps = min(48, max(6, int(3.0 / max(timed[0][0], 1e-3))))
-            final.append((_time_runs(run, reps), kind, s))
-        final.sort()
-        for t, kind, s in final:
-            _timings[key][(kind, s)] = t
-        return (final[0][1], final[0][2])
-    return (timed[0][1], timed[0][2])
+        run = lambda kind=kind, s=s: _launch(kind, s, mode, A, lda, B, ldb, Cs, ldc, M, N, K, bias, act,  # noqa: E731
+                                             aux_s, conv_arr, row_remap, residual, False, cs_s, bnb)
+        run()                              # first launch: code object load, caches
+        runs.append(run)
+    # Candidates are timed INTERLEAVED over rounds and ranked by their median: a one-shot
+    # sequential timing let clock / cache drift between candidates decide close calls, so
+    # fresh processes could tune different plans for the same shapes.
+    est = [_time_runs(r, 1) for r in runs]
+    reps = max(1, min(24, int(0.5 / max(min(est), 1e-3))))
+    rounds = [[] for _ in runs]
+    for _ in range(_TUNE_ROUNDS):
+        for ci, r in enumerate(runs):
+            rounds[ci].append(_time_runs(r, reps))
+    med = [sorted(v)[len(v) // 2] for v in rounds]
+    _timings[key] = {c: t for c, t in zip(cands, med)}
+    best = min(range(len(cands)), key=lambda i: med[i])
+    return cands[best]
 
 
 def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap, residual,
@@ -411,11 +362,7 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
                                    _big_allowed(mode, K, lda, ldb) and act in (None, "relu", "gelu", "dgelu")
                                    and not (act == "dgelu" and aux is None)):
         kernel = "big"                    # 192-wide tiles: NT / NN with a register epilogue only
-    if kernel == "blas" and not blas_ok(mode, C, bias, act, aux, conv_arr, row_remap, residual, colstats, bnb):
-        kernel = "big"                    # hipBLASLt: plain NT / NN (+ bias | residual) only
-    if kernel == "blas":
-        choice = ("blas", 1)
-    elif kernel is not None:
+    if kernel is not None:
         if kernel == "big" and not _big_allowed(mode, K, lda, ldb):
             kernel = "small"              # no 256x256 variant for these
         hy = hybrid_rows(M, N, K) if kernel == "hybrid" and mode in (MODE_NT, MODE_NN) and not row_remap \
@@ -463,16 +410,9 @@ def plan(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
          full: bool = False):
     """The kernel kind (``full``: the (kind, splits) pair) a plain call of this signature
     runs, tuning it now if needed."""
-    global _plan_call
     conv_arr = None if conv is None else (ctypes.c_int * len(conv))(*[int(v) for v in conv])
-    # the callers (convolutions) choose fused epilogues from this answer, which hipBLASLt cannot run:
-    # a signature tuned here never offers "blas"
-    _plan_call = True
-    try:
-        ch = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, None, None, None, None, conv, conv_arr, False,
-                     residual, None, None)
-    finally:
-        _plan_call = False
+    ch = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, None, None, None, None, conv, conv_arr, False,
+                 residual, None, None)
     return ch if full else ch[0]
 
 
@@ -485,8 +425,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
     """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
     "narrow" (128x64), "tnarrow" (weight gradient computed transposed on 128x64 tiles), "big192"
     (256x192 tiles of the 256x256 kernel: NT / NN, register epilogue) or
-    "hybrid" (256x256 tiles, the rows past the last whole round split-K: ``hybrid_rows``) or "blas"
-    (hipBLASLt through torch.mm / addmm: plain NT / NN, bf16, a bf16 bias or a residual; ``blas_ok``).
+    "hybrid" (256x256 tiles, the rows past the last whole round split-K: ``hybrid_rows``).  Every
+    kind is a hand-written kernel of this library (no vendor GEMM library is ever called).
 
     ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm
     statistics partials of the bf16 output; the function then returns the number of

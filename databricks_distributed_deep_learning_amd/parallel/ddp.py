@@ -67,6 +67,18 @@ class Bucket:
     eager_done: bool = False     # set_eager callback already issued on the side stream
 
 
+def _drain_into(acc32: torch.Tensor, grad: torch.Tensor) -> None:
+    """acc32 += grad; grad = 0 -- one native pass over the arena on the GPU (ddl_drain_acc),
+    an add + zero fill elsewhere."""
+    if grad.is_cuda and grad.numel() % 8 == 0:
+        from ..ops import _lib
+        if _lib.available():
+            _lib.call("ddl_drain_acc", _lib.dcode(grad), acc32.data_ptr(), grad.data_ptr(), grad.numel())
+            return
+    acc32.add_(grad)
+    grad.zero_()
+
+
 class ReplicaDivergence(RuntimeError):
     """Data-parallel replicas no longer hold identical parameters (see ``check_replicas``)."""
 
@@ -427,8 +439,7 @@ class DataParallel(nn.Module):
                 # drain this micro-step's bf16 grads into the fp32 accumulator
                 if self._acc32 is None:
                     self._acc32 = torch.zeros(self.arena.numel, dtype=torch.float32, device=self.arena.device)
-                self._acc32.add_(self.arena.grad)
-                self.arena.grad.zero_()
+                _drain_into(self._acc32, self.arena.grad)
                 self._acc_active = True
 
     def replica_fingerprint(self, chunk: int = 1 << 22) -> torch.Tensor:

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-4 GPU session steps (run through gpurun on the MI355X box):
+#   bash scripts/r4_session.sh STEP [STEP ...]
+#   stamps      per-tile / per-k-step GEMM timeline + sampled correctness, deep retire on (d1) / off (d0)
+#   gemmtests   GEMM + drain-acc + comm GPU tests
+#   bertx N     N fresh-process BERT-base bench runs (30 steps): spread + GEMM plan digests
+#   both        bench.py default (ResNet-50 + BERT-base)
+# Each step runs under its own time limit; the script stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+SHAPES="0 16384 768 768 0 16384 3072 768 0 16384 2304 768 0 16384 768 3072 1 16384 768 768 1 16384 3072 768 1 16384 768 3072 0 8192 8192 8192 0 1000 1000 1000 1 4100 300 520"
+while [ $# -gt 0 ]; do
+  s=$1; shift
+  case $s in
+    stamps)
+      for v in d1 d0; do
+        [ -x build/gemm_stamps_$v ] || continue
+        timeout -k 10 150 build/gemm_stamps_$v $SHAPES > gpurun_out/stamps_$v.log 2>&1 || { tail -5 gpurun_out/stamps_$v.log; exit 1; }
+        echo "== $v"; grep -E "^mode|check|k-pair|waves 0-3" gpurun_out/stamps_$v.log
+      done ;;
+    stampsdirect0)
+      # LDS-staged epilogue (row-contiguous full-line stores, no persistent grid) vs the register epilogue
+      DDL_GEMM_DIRECT=0 timeout -k 10 150 build/gemm_stamps_d1 0 16384 768 768 0 16384 3072 768 > gpurun_out/stamps_direct0.log 2>&1 \
+        || { tail -5 gpurun_out/stamps_direct0.log; exit 1; }
+      echo "== direct0"; grep -E "^mode|check|waves 0-3" gpurun_out/stamps_direct0.log ;;
+    gemmtests)
+      timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_comm_gpu.py "tests/test_kernels_gpu.py::test_drain_acc" \
+        -x -q --timeout 150 --timeout-method thread > gpurun_out/gemmtests.log 2>&1 || { tail -30 gpurun_out/gemmtests.log; exit 1; }
+      tail -2 gpurun_out/gemmtests.log ;;
+    bertx)
+      n=3
+      if [[ ${1:-} =~ ^[0-9]+$ ]]; then n=$1; shift; fi
+      for i in $(seq 1 "$n"); do
+        timeout -k 10 300 python bench.py --model bert_base --steps 30 --warmup 5 > gpurun_out/bertx_$i.log 2>&1 || { tail -20 gpurun_out/bertx_$i.log; exit 1; }
+        tail -1 gpurun_out/bertx_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print("bert run", d["value"], d.get("gemm_plan"), d.get("phases_ms"))'
+      done ;;
+    both)
+      timeout -k 10 500 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_both.log 2>&1 || { tail -20 gpurun_out/bench_both.log; exit 1; }
+      tail -1 gpurun_out/bench_both.log ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

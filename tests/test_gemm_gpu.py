@@ -530,39 +530,3 @@ def test_big192_tiles(M, N, K, epi):
             sums = kw["colstats"].view(-1, 2, N)[:rows, 0].sum(0)
             assert _rel_err(sums, c.float().sum(0)) < 1e-3
         assert _rel_err(c, exp) < 1e-2, (mode, epi)
-
-
-@pytest.mark.parametrize("M,N,K", [(16384, 768, 3072), (1000, 768, 768), (513, 2304, 768)])
-def test_blas_kind_matches_native(M, N, K):
-    """Kernel kind "blas" (hipBLASLt via torch.mm / addmm, a tuner candidate for plain NT / NN GEMMs)
-    on the native layouts: the same result as the 256x256 kernel for plain / bf16-bias / residual
-    calls, and the tuner times it next to the native candidates for such a call."""
-    dev = gpu_device()
-    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
-    torch.manual_seed(5)
-    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
-    b = torch.randn(N, device=dev).to(torch.bfloat16)
-    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
-    ref = a.float() @ w.float().t()
-    for mode in (NG.MODE_NT, NG.MODE_NN):
-        wop = w if mode == NG.MODE_NT else w.t().contiguous()
-        ldb = K if mode == NG.MODE_NT else N
-        for kw, exp in ((dict(), ref), (dict(bias=b), ref + b.float()), (dict(residual=res), ref + res.float())):
-            outs = {}
-            for kern in ("big", "blas"):
-                c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-                NG.gemm(mode, a, K, wop, ldb, c, N, M, N, K, kernel=kern, **kw)
-                outs[kern] = c
-            torch.cuda.synchronize()
-            assert _rel_err(outs["blas"], exp) < 1e-2
-            assert _rel_err(outs["blas"], outs["big"]) < 1e-2
-    # tuned call: "blas" is among the timed candidates of a plain bias GEMM, not of a GELU one
-    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    NG.gemm(NG.MODE_NT, a, K, w, K, c, N, M, N, K, bias=b)
-    NG.gemm(NG.MODE_NT, a, K, w, K, c, N, M, N, K, bias=b, act="gelu", aux=torch.empty_like(c))
-    torch.testing.assert_close(c.float(), torch.nn.functional.gelu(ref + b.float()), atol=0.1, rtol=0.05)
-    if NG._TUNE and NG._BLAS:
-        key = lambda act: f"0|{M}|{N}|{K}|{K}|{K}|{N}||0|{act}|{c.dtype}|1|0|0"  # noqa: E731
-        assert ("blas", 1) in NG._timings.get(key(None), {("blas", 1): 0})
-        assert ("blas", 1) not in NG._timings.get(key("gelu"), {})

@@ -49,55 +49,9 @@ def test_big192_is_opt_in(monkeypatch):
     assert not any(c[0] == "big192" for c in NG._candidates(NG.MODE_NT, 16384, 1024, 768, False, 768, 768))
 
 
-# ---- "blas" (hipBLASLt through torch.mm / addmm): which calls qualify, and the layout mapping ----
-def _bf(*shape):
-    import torch
-    return torch.randn(*shape, dtype=torch.float32).to(torch.bfloat16)
-
-
-def test_blas_ok_plain_calls_only():
-    import torch
-    C = torch.empty(4, 4, dtype=torch.bfloat16)
-    b16, b32 = torch.zeros(4, dtype=torch.bfloat16), torch.zeros(4)
-    ok = lambda mode=NG.MODE_NT, C=C, bias=None, act=None, aux=None, conv=None, rr=False, res=None, cs=None: \
-        NG.blas_ok(mode, C, bias, act, aux, conv, rr, res, cs)  # noqa: E731
-    assert ok() and ok(NG.MODE_NN) and ok(bias=b16) and ok(res=C)
-    assert not ok(NG.MODE_TN) and not ok(NG.MODE_CONV)          # weight gradients / convolutions: native
-    assert not ok(act="gelu") and not ok(act="dgelu", aux=C)     # fused epilogues: native
-    assert not ok(bias=b32)                                      # fp32 bias on a bf16 GEMM
-    assert not ok(bias=b16, res=C)                               # bias AND residual: one addmm input only
-    assert not ok(cs=torch.empty(8)) and not ok(rr=True)
-    assert not ok(C=torch.empty(4, 4))                           # fp32 output
-
-
-@pytest.mark.parametrize("mode", ["NT", "NN"])
-@pytest.mark.parametrize("epi", ["none", "bias", "residual", "residual_inplace", "accumulate"])
-def test_blas_launch_matches_reference(mode, epi):
-    """The "blas" launch reads the native operand layouts (row strides lda / ldb / ldc) and adds
-    the same epilogue operands as the native kernels: checked against an fp32 reference on CPU."""
-    import torch
-    torch.manual_seed(0)
-    M, N, K, ldc = 48, 40, 64, 56                     # ldc > N: a strided output block
-    md = NG.MODE_NT if mode == "NT" else NG.MODE_NN
-    A = _bf(M, K)
-    B = _bf(N, K) if mode == "NT" else _bf(K, N)
-    Bm = B.float().t() if mode == "NT" else B.float()
-    C = _bf(M, ldc)
-    C0 = C.clone()
-    bias = _bf(N) if epi == "bias" else None
-    res = None
-    if epi == "residual":
-        res = _bf(M, ldc)
-    elif epi == "residual_inplace":
-        res = C
-    ref = A.float() @ Bm
-    if bias is not None:
-        ref = ref + bias.float()
-    if res is not None:
-        ref = ref + (C0 if res is C else res)[:, :N].float()
-    if epi == "accumulate":
-        ref = ref + C0[:, :N].float()
-    NG._launch("blas", 1, md, A, K, B, B.shape[1], C, ldc, M, N, K, bias, None, None, None, False, res,
-               epi == "accumulate")
-    torch.testing.assert_close(C[:, :N].float(), ref, atol=0.1, rtol=0.02)
-    assert torch.equal(C[:, N:], C0[:, N:])          # columns past N untouched
+def test_no_vendor_gemm_kind():
+    """Every tuner candidate is a kernel of this library: a stale plan entry naming another
+    kind (e.g. the removed hipBLASLt "blas" candidate) falls back to the native heuristic."""
+    assert "blas" not in NG._KINDS and not hasattr(NG, "_blas")
+    for mode in (NG.MODE_NT, NG.MODE_NN, NG.MODE_TN):
+        assert all(k in NG._KINDS for k, _ in NG._candidates(mode, 16384, 768, 768, False, 768, 768, plain=True))

@@ -381,3 +381,20 @@ def test_patch_embed_implicit_im2col(B, H, P, D):
     _close(w.grad, wr.grad, 3e-2, 1e-2, "patch embed dW")
     _close(b.grad, br.grad, 3e-2, 1e-2, "patch embed db")
     assert ops.patch_embed(x, w, b, P).shape == (B, (H // P) ** 2, D)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_drain_acc(dtype):
+    """Grad-accumulation drain (ddl_drain_acc): acc32 += g and g = 0 in one pass, against the
+    fp32 reference; also through DataParallel.no_sync (accumulate_fp32)."""
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd.parallel.ddp import _drain_into
+    torch.manual_seed(0)
+    n = 3 * 8192 + 40
+    g = torch.randn(n, device=dev).to(dtype)
+    acc = torch.randn(n, device=dev)
+    ref = acc + g.float()
+    _drain_into(acc, g)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, ref) and not g.any()
