@@ -77,9 +77,20 @@ def self_launch(n: int) -> int:
     return rc
 
 
+# per-GPU micro-batch defaults of the extra configs (BASELINE.json:10-11); BERT-large: seq 512,
+# LAMB, 4 micro-batches per optimizer step (the train CLI's preset sizes its batch to HBM instead)
+_EXTRA = {"vit_b16": dict(preset="vit_b16", batch=128, seq=None, accum=1),
+          "bert_large": dict(preset="bert_large_lamb", batch=32, seq=512, accum=4)}
+
+
 def run_one(model: str, args, world: int):
     if args.native == "stock":
         from databricks_distributed_deep_learning_amd.baselines import run_stock
+        if model in _EXTRA:
+            e = _EXTRA[model]
+            return run_stock(model, args.batch or e["batch"], args.steps, args.warmup, seq_len=e["seq"] or 128,
+                             bucket_mb=args.bucket_mb or 25.0, grad_accum=e["accum"],
+                             dropout=0.0 if model == "vit_b16" else 0.1)
         batch = (args.batch or 256) if model == "resnet50" else (args.bert_batch or 128)
         return run_stock(model, batch, args.steps, args.warmup, seq_len=128, bucket_mb=args.bucket_mb or 25.0,
                          pad_fraction=args.bert_pad_fraction)
@@ -87,6 +98,9 @@ def run_one(model: str, args, world: int):
     from databricks_distributed_deep_learning_amd.training.loop import Trainer
     if model == "resnet50":
         cfg = get_preset("resnet50_ddp", batch_size=args.batch or 256)
+    elif model in _EXTRA:
+        e = _EXTRA[model]
+        cfg = get_preset(e["preset"], batch_size=args.batch or e["batch"])
     else:
         # --bert-pad-fraction > 0: HF-style right-padded batches with an attention mask (the
         # masked attention path a real fine-tune runs); 0 = full-length sequences, no mask
@@ -125,7 +139,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="both", choices=["both", "resnet50", "bert_base"])
+    ap.add_argument("--model", default="both", choices=["both", "resnet50", "bert_base", "vit_b16", "bert_large"],
+                    help="both = the headline pair; vit_b16 / bert_large: the other BASELINE configs")
     ap.add_argument("--batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
     ap.add_argument("--bert-batch", type=int, default=0, help="BERT-base per-GPU batch (default 128)")
     ap.add_argument("--bert-pad-fraction", type=float, default=0.0,
@@ -164,10 +179,12 @@ def main() -> int:
 
     head = results.get("resnet50") or results[order[0]]
     is_r50 = "resnet50" in results
+    names = {"resnet50": "ResNet-50 images/sec", "bert_base": "BERT-base samples/sec",
+             "vit_b16": "ViT-B/16 images/sec", "bert_large": "BERT-large (seq 512, LAMB) samples/sec"}
     line = {
-        "metric": "ResNet-50 images/sec (whole node)" if is_r50 else "BERT-base samples/sec (whole node)",
+        "metric": names[order[0] if not is_r50 else "resnet50"] + " (whole node)",
         "value": round(head["samples_per_sec"], 2),
-        "unit": "images/s" if is_r50 else "samples/s",
+        "unit": "images/s" if (is_r50 or order[0] == "vit_b16") else "samples/s",
         "n_gpus": ddist.world_size(),
         "steps": args.steps,
         "warmup": args.warmup,
@@ -182,7 +199,8 @@ def main() -> int:
             "global_batch": head["global_batch"],
             "per_gpu_batch": head["per_rank_batch"],
             "seq_len": head["seq_len"],
-            "image_size": 224 if is_r50 else None,
+            "image_size": 224 if head.get("task") == "cv" else None,
+            "grad_accum": head.get("grad_accum", 1),
             "optimizer": head["optimizer"],
             "parallelism": f"dp{ddist.world_size()}",
             "native_kernels": head["native"],

@@ -93,6 +93,7 @@ struct BigParams {
     int tiles_m, tiles_n;
     int ek;                   // register-epilogue variant (EK_*), set by the launcher
     int behind_mask;          // store-behind beyond plain bf16 tiles: BEHIND_* bits (DDL_GEMM_BEHIND)
+    int epi_lds;              // DDL_GEMM_EPI_LDS=1: plain bf16 tiles stored as whole rows through LDS
     const uint8_t* bn_mask;   // ACT_BNB: BatchNorm backward reduction fused into the dgrad (gemm.hip Params)
     const float* bn_mean;
     const float* bn_istd;
@@ -713,6 +714,63 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
         }
 }
 
+// Row-contiguous variant of the plain bf16 register epilogue (EK_BF16, no residual / statistics):
+// the packed tile goes through LDS one 128-row half at a time (64 KB, XOR-swizzled 16-byte chunks
+// of 512-byte rows) and every store instruction then writes whole 128-byte lines -- the register
+// epilogue's stores cover 32 bytes of a line each (two waves per line).  `stage` = 64 KB of LDS no
+// DMA is writing; raw barriers (a __syncthreads fence would drain in-flight LDS-DMA).
+__device__ __forceinline__ void epi_lds_bf16(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm,
+                                             int wn, int lane, char* stage) {
+    const int g4 = (lane >> 4) * 4, r16 = lane & 15;
+    float bv[2][2][4];
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (p.bias) {
+                const uint2 b2 = *reinterpret_cast<const uint2*>((const bf16_t*)p.bias + n0 + qn * 128 + wn * 32 + j * 16 + g4);
+                bv[qn][j][0] = __uint_as_float(b2.x << 16);
+                bv[qn][j][1] = __uint_as_float(b2.x & 0xffff0000u);
+                bv[qn][j][2] = __uint_as_float(b2.y << 16);
+                bv[qn][j][3] = __uint_as_float(b2.y & 0xffff0000u);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bv[qn][j][e] = 0.f;
+            }
+        }
+    const int rc = threadIdx.x & 31, rr = threadIdx.x >> 5;    // store side: 16 rows x 32 chunks per pass
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const f32x4& a = acc[qm][qn][i][j];
+                    const int r = wm * 64 + i * 16 + r16;
+                    const int c = qn * 128 + wn * 32 + j * 16 + g4;
+                    const int off = r * 512 + (((c >> 3) ^ (r & 15)) << 4) + (c & 7) * 2;
+                    *reinterpret_cast<uint2*>(stage + off) =
+                        make_uint2(pack2bf(a[0] + bv[qn][j][0], a[1] + bv[qn][j][1]),
+                                   pack2bf(a[2] + bv[qn][j][2], a[3] + bv[qn][j][3]));
+                }
+        LGKM0();
+        BARRIER();
+        uint4 v[8];
+#pragma unroll
+        for (int ps = 0; ps < 8; ++ps) {
+            const int r = ps * 16 + rr;
+            v[ps] = *reinterpret_cast<const uint4*>(stage + r * 512 + ((rc ^ (r & 15)) << 4));
+        }
+#pragma unroll
+        for (int ps = 0; ps < 8; ++ps)
+            *reinterpret_cast<uint4*>((bf16_t*)p.C + (long)(m0 + qm * 128 + ps * 16 + rr) * p.ldc + n0 + rc * 8) = v[ps];
+        LGKM0();
+        BARRIER();      // every read of this half done before the next half (or a DMA) overwrites it
+    }
+}
+
 // DIRECT: epilogue from registers (direct4) and, with it, a persistent grid: a
 // block walks tiles blockIdx.x, +gridDim.x, ...; after a tile's last MFMA it
 // stages the next tile's first K-tile, stores this tile from registers, then
@@ -1084,11 +1142,13 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // (a residual's loads retire in order behind the next prologue's, so the counts
             // below stay upper bounds)
             // (not with 192-wide tiles: the store counts its vmcnt waits assume are the 256-wide ones)
-            const bool behind = !N192 && next && nK > 0 && interior &&
+            // whole-row stores through LDS (buffer O's 64 KB; the next prologue is issued after them)
+            const bool lds_epi = !N192 && !BNB && p.epi_lds && interior && p.ek == EK_BF16 && !p.res && !p.colstats;
+            const bool behind = !N192 && !lds_epi && next && nK > 0 && interior &&
                 ((p.ek == EK_BF16 && (!p.bias || (p.behind_mask & BEHIND_BIAS)) &&
                   (!p.res || (p.behind_mask & BEHIND_RES))) ||
                  (p.ek == EK_GELU && (p.behind_mask & BEHIND_GELU)));
-            if (next) {
+            if (next && !lds_epi) {
                 coords(vn);
                 ask();
                 sa.init(p, m0);
@@ -1105,7 +1165,16 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // edge tiles and the rarer epilogue options the general one
             if (BNB)   // checked on every tile: a lean interior twin spills (measured slower)
                 epi_direct<EK_BNBC>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
-            else if (interior && p.ek == EK_BF16)
+            else if (lds_epi) {
+                epi_lds_bf16(p, acc, m0c, n0c, wm, wn, lane, smem + half_off(1, 0, 0));
+                if (next) {
+                    coords(vn);
+                    ask();
+                    sa.init(p, m0);
+                    sb.init(p, n0);
+                    if (nK > 0) prologueE();
+                }
+            } else if (interior && p.ek == EK_BF16)
                 epi_direct<EK_BF16, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_F32)
                 epi_direct<EK_F32, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
@@ -1384,9 +1453,19 @@ int behind_mask() {
     return m;
 }
 
+// DDL_GEMM_EPI_LDS=1: plain bf16 interior tiles store whole rows through LDS (epi_lds_bf16)
+bool epi_lds_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_EPI_LDS");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 template <int LA, int LB>
 int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st, bool n192 = false) {
     p.behind_mask = behind_mask();
+    p.epi_lds = epi_lds_enabled() ? 1 : 0;
     const int tbn = n192 ? 192 : TB;
     p.tiles_m = (p.M + TB - 1) / TB;
     p.tiles_n = (p.N + tbn - 1) / tbn;

@@ -24,6 +24,11 @@ while [ $# -gt 0 ]; do
       DDL_GEMM_DIRECT=0 timeout -k 10 150 build/gemm_stamps_d1 0 16384 768 768 0 16384 3072 768 > gpurun_out/stamps_direct0.log 2>&1 \
         || { tail -5 gpurun_out/stamps_direct0.log; exit 1; }
       echo "== direct0"; grep -E "^mode|check|waves 0-3" gpurun_out/stamps_direct0.log ;;
+    stampsepilds)
+      # whole-row stores through LDS for plain bf16 tiles (DDL_GEMM_EPI_LDS=1) vs the register epilogue
+      DDL_GEMM_EPI_LDS=1 timeout -k 10 150 build/gemm_stamps_d1 $SHAPES > gpurun_out/stamps_epilds.log 2>&1 \
+        || { tail -5 gpurun_out/stamps_epilds.log; exit 1; }
+      echo "== epilds"; grep -E "^mode|check|waves 0-3" gpurun_out/stamps_epilds.log ;;
     gemmtests)
       timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_comm_gpu.py "tests/test_kernels_gpu.py::test_drain_acc" \
         -x -q --timeout 150 --timeout-method thread > gpurun_out/gemmtests.log 2>&1 || { tail -30 gpurun_out/gemmtests.log; exit 1; }
@@ -34,6 +39,15 @@ while [ $# -gt 0 ]; do
       for i in $(seq 1 "$n"); do
         timeout -k 10 300 python bench.py --model bert_base --steps 30 --warmup 5 > gpurun_out/bertx_$i.log 2>&1 || { tail -20 gpurun_out/bertx_$i.log; exit 1; }
         tail -1 gpurun_out/bertx_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print("bert run", d["value"], d.get("gemm_plan"), d.get("phases_ms"))'
+      done ;;
+    arms)
+      # native and stock PyTorch-ROCm arms of all four BASELINE workloads, same box, one call
+      for m in resnet50 bert_base vit_b16 bert_large; do
+        for arm in auto stock; do
+          timeout -k 10 400 python bench.py --model $m --native $arm --steps 15 --warmup 4 > gpurun_out/arm_${m}_$arm.log 2>&1 \
+            || { tail -20 gpurun_out/arm_${m}_$arm.log; exit 1; }
+          tail -1 gpurun_out/arm_${m}_$arm.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); c=d["config"]; print("arm", c["model"], c["native_kernels"], d["value"], d["unit"], "batch", c["per_gpu_batch"], "accum", c.get("grad_accum"), "ms", d["ms_per_step"])'
+        done
       done ;;
     both)
       timeout -k 10 500 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_both.log 2>&1 || { tail -20 gpurun_out/bench_both.log; exit 1; }
