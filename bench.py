@@ -111,21 +111,23 @@ def run_one(model: str, args, world: int):
                       zero_optimizer=args.zero, sync_bn=args.sync_bn,
                       eager_optimizer=os.environ.get("DDL_EAGER_OPTIMIZER", "0") == "1",
                       phase_timing=os.environ.get("DDL_PHASE_TIMING", "1") != "0")
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm
+    before = set(_native_gemm.tuned_choices())
     tr = Trainer(cfg)
     s = tr.run()
     tr.close()
     del tr
-    s["gemm_plan"] = gemm_plan_digest(model)
+    s["gemm_plan"] = gemm_plan_digest(model, exclude=before)
     return s
 
 
-def gemm_plan_digest(model: str) -> str:
-    """Hash of the tuned GEMM kernel plan this process ran (every signature -> (kernel, splits));
-    the full plan goes to stderr.  Two bench processes whose step times differ can then be told
+def gemm_plan_digest(model: str, exclude=()) -> str:
+    """Hash of the tuned GEMM kernel plan this model ran (every signature it tuned -> (kernel,
+    splits); ``exclude``: signatures an earlier model of this process tuned); the full plan goes to stderr.  Two bench processes whose step times differ can then be told
     apart by plan (tuner picks) or not (same plan: the cause is elsewhere)."""
     import hashlib
     from databricks_distributed_deep_learning_amd.ops import _native_gemm
-    plan = {k: list(v) for k, v in sorted(_native_gemm.tuned_choices().items())}
+    plan = {k: list(v) for k, v in sorted(_native_gemm.tuned_choices().items()) if k not in exclude}
     if not plan:
         return ""
     text = json.dumps(plan, sort_keys=True)

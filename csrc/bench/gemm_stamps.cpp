@@ -66,8 +66,9 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> h(nst);
     for (const Case& c : cases) {
         const int M = c.M, N = c.N, K = c.K;
-        const long lda = c.mode == 2 ? M : K;
-        const long ldb = c.mode == 0 ? K : N;
+        const int lay = c.mode & 31;       // | 32: 256 x 192 tiles (NT / NN)
+        const long lda = lay == 2 ? M : K;
+        const long ldb = lay == 0 ? K : N;
         auto run = [&] {
             int r = ddl_gemm_big2(c.mode, A, lda, B, ldb, C, N, M, N, K, nullptr, 0, 0, nullptr, 0, 1, nullptr, 0,
                                   nullptr, 0, nullptr, 0, Z, nullptr, 0);
@@ -103,8 +104,8 @@ int main(int argc, char** argv) {
                 const int n = (int)((r >> 8) % (uint32_t)N);
                 double ref = 0;
                 for (int k = 0; k < K; ++k) {
-                    const double a = f(hA[(c.mode == 2 ? (size_t)k * M + m : (size_t)m * K + k)]);
-                    const double b = f(hA[(c.mode == 0 ? (size_t)n * K + k : (size_t)k * N + n)]);
+                    const double a = f(hA[(lay == 2 ? (size_t)k * M + m : (size_t)m * K + k)]);
+                    const double b = f(hA[(lay == 0 ? (size_t)n * K + k : (size_t)k * N + n)]);
                     ref += a * b;
                 }
                 const double got = f(hc[(size_t)m * N + n]);
@@ -114,7 +115,8 @@ int main(int argc, char** argv) {
             }
             printf("   check: %d / 512 sampled outputs off (worst err / tol %.3f)%s\n", bad, worst, bad ? "  *** MISMATCH ***" : "");
         }
-        const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+        const int tbn = (c.mode & 32) ? 192 : 256;
+        const int tiles = ((M + 255) / 256) * ((N + tbn - 1) / tbn);
         const int grid = std::min(tiles, 256);
         // phases per wave group (0: waves 0-3, 1: waves 4-7)
         double sum[2][2][3] = {}, cnt[2][2] = {};

@@ -44,12 +44,13 @@ namespace {
 #ifndef DDL_GROUP_M
 #define DDL_GROUP_M 8      // tile rows per L2 group (tile order inside an XCD's share)
 #endif
-// Deep retire (default): each half-tile is waited for in the phase right before its first
-// read, not with the whole tile at phases 4 / 8 -- five half-tiles (80 KB) stay in flight
-// instead of three, and the tightest DMA gets five phases to land instead of three (the
-// short-K GEMMs' main loop was DMA-latency bound: csrc/bench/gemm_stamps.cpp).
+// Retire depth of the operand DMA (A/B variants, csrc/bench/gemm_stamps.cpp):
+//   0: the whole E / O tile is waited for at phases 4 / 8 (three half-tiles in flight);
+//   1: each half-tile is waited for in the phase right before its first read (five in flight,
+//      runtime-counted waits);
+//   2: phases 4 / 8 retire three halves, the fourth (staged last) one phase-pair later.
 #ifndef DDL_DEEP_RETIRE
-#define DDL_DEEP_RETIRE 1
+#define DDL_DEEP_RETIRE 0
 #endif
 constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
 constexpr int TB = 256, BK = 64, NTH = 512;
@@ -325,11 +326,16 @@ constexpr int STAMP_TILES = 16;
         }                                                                                                   \
     } while (0)
 __device__ unsigned long long* g_kstamps;   // [block][k-tile pair < 32]: first tile only, wave 0
+// (a store in wave 0's vector-memory stream shifts its counted vmcnt waits: off unless asked for)
+#ifdef DDL_GEMM_KSTAMPS
 #define KSTAMP(it)                                                                                          \
     do {                                                                                                    \
         if (threadIdx.x == 0 && stamp_ti == 0 && (it) < 32)                                                 \
             g_kstamps[((long)blockIdx.y * gridDim.x + blockIdx.x) * 32 + (it)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#else
+#define KSTAMP(it) do {} while (0)
+#endif
 #else
 #define STAMP(ev) do {} while (0)
 #define KSTAMP(it) do {} while (0)
@@ -910,7 +916,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         else if (hold == 38) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
         else VM6();
     };
-#if DDL_DEEP_RETIRE
+#if DDL_DEEP_RETIRE == 1
     // Counted waits from the stage-issue history: bit s of `cm` = stage slot s (the DMA of
     // phase s + 1) of this iteration went out, `pm` = the previous iteration's slots (or the
     // prologue's: E -> slots 1-4, O A0 / B0 / B1 -> slots 5-7).  Stage order per iteration:
@@ -970,7 +976,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         BARRIER();
     };
 #else
-    auto phasesE = [&](int kE, bool stO1, bool more, int hold = 0) {
+    auto phasesE = [&](int kE, bool stO1, bool more, int hold = 0, bool w2 = false) {
         // phase 1: E (0,0)
         readA(0, 0);
         readB(0, 0, fb0);
@@ -981,6 +987,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         // phase 2: E (0,1)
         readB(0, 1, fb1);
         if (more) sa.stage(p, smem, 0, 0, kE + 2);
+#if DDL_DEEP_RETIRE == 2
+        // E-A1 (staged at the previous pair's phase 5) retired here, read in phase 3
+        if (w2) { if (more) VMN(10); else VMN(8); }
+#else
+        (void)w2;
+#endif
         READS_DONE_BARRIER();
         mma(0, 1, fb1);
         BARRIER();
@@ -991,7 +1003,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         mma(1, 1, fb1);
         BARRIER();
         // phase 4: E (1,0); retire O(kE+1)
+#if DDL_DEEP_RETIRE == 2
+        // O-A0 / B0 / B1 only: O-A1 (staged at phase 1) is retired at phase 6
+        if (more) { sb.stage(p, smem, 0, 1, kE + 2); if (hold) vm_retire_o(hold); else VMN(8); } else { VM0(); }
+#else
         if (more) { sb.stage(p, smem, 0, 1, kE + 2); vm_retire_o(hold); } else { VM0(); }
+#endif
         BARRIER();
         mma(1, 0, fb0);
         BARRIER();
@@ -1012,7 +1029,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             sa.stage(p, smem, 1, 0, kt0 + 1);
             sb.stage(p, smem, 1, 0, kt0 + 1);
             sb.stage(p, smem, 1, 1, kt0 + 1);
-#if DDL_DEEP_RETIRE
+#if DDL_DEEP_RETIRE == 1
             VMN(10);      // E-A0 / E-B0 only: E-B1 / E-A1 are retired at phases 1 / 2 (vm_younger)
 #else
             VM6();
@@ -1038,7 +1055,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     for (;;) {
         if (nK > 0) {
             const int pairs = nK / 2;
-#if DDL_DEEP_RETIRE
+#if DDL_DEEP_RETIRE == 1
             unsigned pm = nK > 1 ? 0xFEu : 0x1Eu, cm = 0u;    // the prologue's slots (see vm_younger)
             for (int it = 0; it < pairs; ++it) {
                 KSTAMP(it);
@@ -1087,8 +1104,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 const bool more = kE + 2 < kt_end;
                 const bool moreO = kO + 2 < kt_end;
                 // first pair after a store-behind epilogue: O is already staged whole
-                if constexpr (BNB) phasesE(kE, true, more);
-                else phasesE(kE, !(it == 0 && hold_o), more, it == 0 ? hold_o : 0);
+                if constexpr (BNB) phasesE(kE, true, more, 0, it > 0);
+                else phasesE(kE, !(it == 0 && hold_o), more, it == 0 ? hold_o : 0, it > 0);
                 // phase 5: O (0,0)
                 readA(1, 0);
                 readB(1, 0, fb0);
@@ -1099,6 +1116,13 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 // phase 6: O (0,1)
                 readB(1, 1, fb1);
                 if (moreO) sa.stage(p, smem, 1, 0, kO + 2);
+#if DDL_DEEP_RETIRE == 2
+                if (BNB || !(it == 0 && hold_o)) {        // O-A1 (phase 1), read in phase 7
+                    if (moreO) VMN(10);
+                    else if (more) VMN(8);
+                    else VM0();
+                }
+#endif
                 READS_DONE_BARRIER();
                 mma(0, 1, fb1);
                 BARRIER();
@@ -1109,7 +1133,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 mma(1, 1, fb1);
                 BARRIER();
                 // phase 8: O (1,0); retire E(kE+2)
+#if DDL_DEEP_RETIRE == 2
+                // E-A0 / B0 / B1 only: E-A1 (phase 5) is retired at the next pair's phase 2
+                if (moreO) { sb.stage(p, smem, 1, 1, kO + 2); VMN(8); } else { VM0(); }
+#else
                 if (moreO) { sb.stage(p, smem, 1, 1, kO + 2); VM6(); } else { VM0(); }
+#endif
                 BARRIER();
                 mma(1, 0, fb0);
                 BARRIER();

@@ -9,12 +9,12 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-SHAPES="0 16384 768 768 0 16384 3072 768 0 16384 2304 768 0 16384 768 3072 1 16384 768 768 1 16384 3072 768 1 16384 768 3072 0 8192 8192 8192 0 1000 1000 1000 1 4100 300 520"
+SHAPES="0 16384 768 768 32 16384 768 768 0 16384 3072 768 0 16384 2304 768 32 16384 2304 768 0 16384 768 3072 32 16384 768 3072 1 16384 768 768 33 16384 768 768 1 16384 3072 768 1 16384 768 3072 0 8192 8192 8192 0 1000 1000 1000 1 4100 300 520"
 while [ $# -gt 0 ]; do
   s=$1; shift
   case $s in
     stamps)
-      for v in d1 d0; do
+      for v in d0 d1 d2; do
         [ -x build/gemm_stamps_$v ] || continue
         timeout -k 10 150 build/gemm_stamps_$v $SHAPES > gpurun_out/stamps_$v.log 2>&1 || { tail -5 gpurun_out/stamps_$v.log; exit 1; }
         echo "== $v"; grep -E "^mode|check|k-pair|waves 0-3" gpurun_out/stamps_$v.log
@@ -33,6 +33,16 @@ while [ $# -gt 0 ]; do
       timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_comm_gpu.py "tests/test_kernels_gpu.py::test_drain_acc" \
         -x -q --timeout 150 --timeout-method thread > gpurun_out/gemmtests.log 2>&1 || { tail -30 gpurun_out/gemmtests.log; exit 1; }
       tail -2 gpurun_out/gemmtests.log ;;
+    abdr)
+      # same-box BERT-base A/B: the library's retire depth vs libddl_dr2.so (DDL_DEEP_RETIRE=2), alternating
+      for i in 1 2; do
+        for arm in base dr2; do
+          if [ $arm = dr2 ]; then export DDL_NATIVE_LIB=$PWD/databricks_distributed_deep_learning_amd/_native/ab/libddl_dr2.so; else unset DDL_NATIVE_LIB; fi
+          timeout -k 10 300 python bench.py --model bert_base --steps 30 --warmup 5 > gpurun_out/abdr_${arm}_$i.log 2>&1 || { tail -20 gpurun_out/abdr_${arm}_$i.log; exit 1; }
+          tail -1 gpurun_out/abdr_${arm}_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print("abdr", "'$arm'", d["value"], d.get("phases_ms"))'
+        done
+      done
+      unset DDL_NATIVE_LIB ;;
     bertx)
       n=3
       if [[ ${1:-} =~ ^[0-9]+$ ]]; then n=$1; shift; fi
