@@ -169,7 +169,7 @@ class DataParallel(nn.Module):
 
     # ------------------------------------------------------------------
     def _build_buckets(self, bucket_mb: float, first_bucket_mb: float) -> List[Bucket]:
-        """Whole tensors per bucket, in arena order; a single tensor larger than two buckets
+        """Whole tensors per bucket, in arena order; a single tensor larger than a bucket
         (BERT's 47 MB word embedding) is cut into bucket-sized pieces of its own
         (``split_tensors``): they all launch when its gradient lands, and the per-bucket
         optimizer starts on the first piece while the later ones are still on the wire.
@@ -184,7 +184,7 @@ class DataParallel(nn.Module):
         ents = self.arena.entries
         for ei, e in enumerate(ents):
             nxt = ents[ei + 1].offset if ei + 1 < len(ents) else self.arena.numel
-            if self.split_tensors and e.numel > 2 * full:
+            if self.split_tensors and e.numel > full:
                 if cur:                            # close the bucket in progress first
                     buckets.append(Bucket(len(buckets), start, e.offset, cur))
                     cur, start = [], e.offset

@@ -26,9 +26,11 @@ while [ $# -gt 0 ]; do
       echo "== direct0"; grep -E "^mode|check|waves 0-3" gpurun_out/stamps_direct0.log ;;
     stampsepilds)
       # whole-row stores through LDS for plain bf16 tiles (DDL_GEMM_EPI_LDS=1) vs the register epilogue
-      DDL_GEMM_EPI_LDS=1 timeout -k 10 150 build/gemm_stamps_d1 $SHAPES > gpurun_out/stamps_epilds.log 2>&1 \
-        || { tail -5 gpurun_out/stamps_epilds.log; exit 1; }
-      echo "== epilds"; grep -E "^mode|check|waves 0-3" gpurun_out/stamps_epilds.log ;;
+      for v in d0 d2; do
+        DDL_GEMM_EPI_LDS=1 timeout -k 10 150 build/gemm_stamps_$v 0 16384 768 768 0 16384 3072 768 0 16384 2304 768 \
+          > gpurun_out/stamps_epilds_$v.log 2>&1 || { tail -5 gpurun_out/stamps_epilds_$v.log; exit 1; }
+        echo "== epilds $v"; grep -E "^mode|check|waves 0-3" gpurun_out/stamps_epilds_$v.log
+      done ;;
     gemmtests)
       timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_comm_gpu.py "tests/test_kernels_gpu.py::test_drain_acc" \
         -x -q --timeout 150 --timeout-method thread > gpurun_out/gemmtests.log 2>&1 || { tail -30 gpurun_out/gemmtests.log; exit 1; }

@@ -441,7 +441,7 @@ def test_watchdog_fails_engine_within_seconds():
 
 
 def _split_bucket_equivalence(opt_name):
-    """A tensor larger than two buckets is cut into bucket-sized pieces (BERT's word embedding):
+    """A tensor larger than a bucket is cut into bucket-sized pieces (BERT's word embedding):
     the pieces all-reduce separately and the per-bucket optimizer ranges still give the same
     update as replicated full-batch training."""
     import torch.distributed as dist
