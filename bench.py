@@ -133,6 +133,9 @@ def gemm_plan_digest(model: str, exclude=()) -> str:
     text = json.dumps(plan, sort_keys=True)
     digest = hashlib.sha1(text.encode()).hexdigest()[:12]
     log(f"[bench] {model} gemm plan {digest} ({len(plan)} signatures): {text}")
+    tim = {k: {f"{c[0]}:{c[1]}": round(t * 1000.0, 1) for c, t in v.items()}
+           for k, v in sorted(_native_gemm._timings.items()) if k in plan}
+    log(f"[bench] {model} gemm candidate us ({_native_gemm.online_stats()}): {json.dumps(tim)}")
     return digest
 
 

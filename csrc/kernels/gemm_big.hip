@@ -44,13 +44,17 @@ namespace {
 #ifndef DDL_GROUP_M
 #define DDL_GROUP_M 8      // tile rows per L2 group (tile order inside an XCD's share)
 #endif
-// Retire depth of the operand DMA (A/B variants, csrc/bench/gemm_stamps.cpp):
+// Retire depth of the operand DMA (A/B variants, csrc/bench/gemm_stamps.cpp, profiles/gemm_stamps_dr*.log):
 //   0: the whole E / O tile is waited for at phases 4 / 8 (three half-tiles in flight);
 //   1: each half-tile is waited for in the phase right before its first read (five in flight,
-//      runtime-counted waits);
-//   2: phases 4 / 8 retire three halves, the fourth (staged last) one phase-pair later.
+//      runtime-counted waits) -- measured 1.5-2.2x SLOWER (the counted-wait branches), kept for A/B;
+//   2 (default): phases 4 / 8 retire three halves, the fourth (staged last) two phases later --
+//      constant waits; neutral on 256-wide tiles, 10-15 % faster on 256 x 192 ones.
 #ifndef DDL_DEEP_RETIRE
-#define DDL_DEEP_RETIRE 0
+#define DDL_DEEP_RETIRE 2
+#endif
+#ifndef DDL_GEMM_EPI_LDS_CODE
+#define DDL_GEMM_EPI_LDS_CODE 0   // whole-row LDS epilogue experiment (epi_lds_bf16): not compiled in
 #endif
 constexpr int EP_LD = 132;   // epilogue LDS row stride (floats)
 constexpr int TB = 256, BK = 64, NTH = 512;
@@ -1172,7 +1176,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             // below stay upper bounds)
             // (not with 192-wide tiles: the store counts its vmcnt waits assume are the 256-wide ones)
             // whole-row stores through LDS (buffer O's 64 KB; the next prologue is issued after them)
-            const bool lds_epi = !N192 && !BNB && p.epi_lds && interior && p.ek == EK_BF16 && !p.res && !p.colstats;
+            // (compiled in only with -DDDL_GEMM_EPI_LDS_CODE=1: its second prologue site raised the
+            // register pressure enough to spill the KO operand loaders' row offsets inside the main
+            // loop -- TN / NN 2x slower, profiles/gemm_spills_r04.md)
+            const bool lds_epi = DDL_GEMM_EPI_LDS_CODE && !N192 && !BNB && p.epi_lds && interior && p.ek == EK_BF16 && !p.res && !p.colstats;
             const bool behind = !N192 && !lds_epi && next && nK > 0 && interior &&
                 ((p.ek == EK_BF16 && (!p.bias || (p.behind_mask & BEHIND_BIAS)) &&
                   (!p.res || (p.behind_mask & BEHIND_RES))) ||

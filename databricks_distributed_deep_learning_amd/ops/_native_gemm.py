@@ -104,11 +104,12 @@ def pick_splits(M: int, N: int, K: int, force: Optional[int] = None) -> int:
 
 
 _HYBRID = os.environ.get("DDL_GEMM_HYBRID", "1") != "0"   # tuner candidate (A/B: 0 = never)
-# tuner candidate "big192" (256 x 192 tiles), off by default: never the tuner's pick on BERT-base's
-# shapes (same-box A/B neutral, ViT -0.5 %): its quadrant-1 phases run 8 MFMAs per wave instead of 16
-# with the same barrier / fragment-read / DMA-issue cost, so a tile costs about as much as a 256-wide
-# one and the whole-round grid buys nothing.  DDL_GEMM_192=1 offers it (forcing: kernel="big192").
-_BIG192 = os.environ.get("DDL_GEMM_192", "0") == "1"
+# tuner candidate "big192" (256 x 192 tiles; DDL_GEMM_192=0 drops it): whole rounds where 256-wide
+# tiles leave a partial one (N = 768 / 2304 at M = 16384: 256 / 768 tiles instead of 192 / 576).  With
+# the retire depth 2 main loop (gemm_big.hip DDL_DEEP_RETIRE) its half-filled quadrant-1 phases no
+# longer cost as much as full ones: 16384x768x768 NT 27.2 vs 34.6 us, 16384x2304x768 72.1 vs 95.1 us
+# (profiles/gemm_stamps_dr2.log); forcing: kernel="big192".
+_BIG192 = os.environ.get("DDL_GEMM_192", "1") == "1"
 _DIRECT = os.environ.get("DDL_GEMM_DIRECT", "1") != "0"    # gemm_big.hip register epilogue (big192 needs it)
 def hybrid_rows(M: int, N: int, K: int):
     """Row split of a 256x256-tile GEMM whose tile grid ends in a partial round, or None.
@@ -227,6 +228,8 @@ _timings: dict = {}
 _NARROW_STATS = os.environ.get("DDL_TUNE_NARROW_STATS", "0") != "0"   # same-box A/B neutral: off
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
 _TUNE_ROUNDS = max(1, int(os.environ.get("DDL_GEMM_TUNE_ROUNDS", "5")))   # interleaved timing rounds per candidate
+_TUNE_COLD = os.environ.get("DDL_GEMM_TUNE_COLD", "1") != "0"             # time candidates from evicted caches
+_ONLINE = os.environ.get("DDL_GEMM_TUNE_ONLINE", "1") != "0"              # in-model tuning during warm-up
 # optional persistent cache (JSON): later processes skip the timing runs
 _CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
 
@@ -301,31 +304,70 @@ def agree_across_ranks(group=None) -> int:
     return changed
 
 
-def _time_runs(run, reps: int) -> float:
-    """Mean milliseconds per call over ``reps`` back-to-back launches."""
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+_flush_bufs: dict = {}
+
+
+def _flush_buf(device) -> torch.Tensor:
+    """A 640 MB scratch buffer whose fill evicts the L2s and the 256 MB Infinity Cache."""
+    b = _flush_bufs.get(device)
+    if b is None:
+        b = _flush_bufs[device] = torch.empty(640 << 20, dtype=torch.uint8, device=device)
+    return b
+
+
+def _time_runs(run, reps: int, cold: bool = False) -> float:
+    """Milliseconds per call over ``reps`` launches, in DEVICE time.
+
+    A spin kernel (``torch.cuda._sleep``) goes first so the host has queued every launch
+    before the first timing event is reached: otherwise a kernel shorter than the ~40-60 us
+    the Python launch path takes is timed at the HOST's launch rate -- the same for every
+    candidate -- and the tuner's pick among fast kernels was noise.  ``cold``: every launch is
+    preceded by a cache-evicting fill and timed alone (events around the launch only): a
+    training step's GEMM reads operands that were written long before (saved activations,
+    weights), and with every operand cache-hot the 128x128 kernels won the weight-gradient
+    GEMMs they lose in the model (BERT-base backward +1.7 ms/step when they were picked)."""
+    if hasattr(torch.cuda, "_sleep"):
+        torch.cuda._sleep(int(min(4e8, (4.0e5 if cold else 2.5e5) * (reps + 1))))   # ~120-190 us host time per launch
+    if not cold:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+    buf = _flush_buf(torch.cuda.current_device())
+    evs = []
     for _ in range(reps):
+        buf.fill_(1)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
         run()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps
+        b.record()
+        evs.append((a, b))
+    evs[-1][1].synchronize()
+    return sum(a.elapsed_time(b) for a, b in evs) / reps
 
 
-def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap, residual,
-          colstats=None, bnb=None):
+def _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats):
+    """The (kernel, splits) candidates a call of this signature can run."""
     plain = bias is None and act is None and residual is None and aux is None and not row_remap
     cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain)
     if act not in (None, "relu", "gelu", "dgelu") or (act == "dgelu" and aux is None):
         cands = [c for c in cands if c[0] != "big192"]     # LDS-staged epilogue: 256-wide tiles only
-    cs_s = None
     if colstats is not None:   # statistics epilogue: whole-K tiles only
         cands = [c for c in cands if c[1] == 1 and not c[0].startswith("t")]
         # 128x64 tiles (three blocks per CU) for the epilogue-heavy statistics / BN-backward
         # tiles even where N is a multiple of 128 (more blocks in flight per CU)
         if _NARROW_STATS and N % 64 == 0 and ("narrow", 1) not in cands:
             cands.append(("narrow", 1))
-        cs_s = torch.empty_like(colstats)
+    return cands
+
+
+def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap, residual,
+          colstats=None, bnb=None):
+    cands = _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats)
+    cs_s = torch.empty_like(colstats) if colstats is not None else None
     if len(cands) == 1:
         _timings[key] = {cands[0]: 0.0}
         return cands[0]
@@ -343,19 +385,85 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     # sequential timing let clock / cache drift between candidates decide close calls, so
     # fresh processes could tune different plans for the same shapes.
     est = [_time_runs(r, 1) for r in runs]
-    reps = max(1, min(24, int(0.5 / max(min(est), 1e-3))))
+    reps = max(2, min(8, int(0.3 / max(min(est), 1e-3))))
     rounds = [[] for _ in runs]
     for _ in range(_TUNE_ROUNDS):
         for ci, r in enumerate(runs):
-            rounds[ci].append(_time_runs(r, reps))
+            rounds[ci].append(_time_runs(r, reps, cold=_TUNE_COLD))
     med = [sorted(v)[len(v) // 2] for v in rounds]
     _timings[key] = {c: t for c, t in zip(cands, med)}
     best = min(range(len(cands)), key=lambda i: med[i])
     return cands[best]
 
 
+# ------------------------------------------------------------------ in-model (online) tuning
+# Timing candidates in isolation -- back to back on the same operands, even from evicted caches --
+# did not rank them the way the training step does: the BERT-base weight-gradient GEMMs went to
+# the 128x128 kernel, which won in isolation and ran ~30 % slower in the model (+1.7 ms/step,
+# profiles/kernels_bert_r04_hottuner.md).  During a trainer's warm-up steps an untuned signature
+# therefore cycles through its candidates on its REAL calls (every layer's call is a sample,
+# timed with events on the compute stream, read back once per step) and keeps the one with the
+# lowest median in-model time.  Results are identical whichever candidate runs a call.
+_online_active = False
+_online: dict = {}          # key -> {"cands": [...], "n": calls, "pending": [(cand, e0, e1)], "samples": {}}
+_online_last = None         # (key, cand) of the call _choose just routed online
+_online_count = {"tuned": 0, "samples": 0}
+
+
+def online_stats() -> dict:
+    """How many signatures in-model tuning committed, from how many timed calls (this process)."""
+    return dict(_online_count)
+
+
+@contextlib.contextmanager
+def online_tuning(enabled: bool = True):
+    """Tune untuned GEMM signatures from their in-model calls inside the block (the trainer's
+    warm-up steps); call :func:`online_collect` after each step.  On exit every signature seen
+    gets its in-model argmin (:func:`online_finish`)."""
+    global _online_active
+    prev = _online_active
+    _online_active = bool(enabled) and _TUNE and _ONLINE and torch.cuda.is_available()
+    try:
+        yield
+    finally:
+        if _online_active:
+            online_finish()
+        _online_active = prev
+
+
+def online_collect() -> None:
+    """Read back the events of the calls timed since the last collect (one host sync)."""
+    pend = [(st, c, a, b) for st in _online.values() for c, a, b in st["pending"]]
+    if not pend:
+        return
+    pend[-1][3].synchronize()
+    torch.cuda.synchronize()
+    for st, c, a, b in pend:
+        st["samples"].setdefault(c, []).append(a.elapsed_time(b))
+    for st in _online.values():
+        st["pending"] = []
+
+
+def online_finish() -> int:
+    """Commit the in-model choice of every signature tuned online; returns how many."""
+    online_collect()
+    done = 0
+    for key, st in list(_online.items()):
+        med = {c: sorted(v)[len(v) // 2] for c, v in st["samples"].items() if v}
+        if med:
+            _timings[key] = med
+            _tuned[key] = min(med, key=med.get)
+            done += 1
+            _online_count["samples"] += sum(len(v) for v in st["samples"].values())
+        del _online[key]
+    _online_count["tuned"] += done
+    if done:
+        _save_cache()
+    return done
+
+
 def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap, residual,
-            kernel, colstats, bnb=None):
+            kernel, colstats, bnb=None, online_ok: bool = False):
     """(kernel kind, splits) for one GEMM call: forced, explicit, tuned (cached) or heuristic."""
     kernel = kernel or _forced
     if kernel == "big192" and not (mode in (MODE_NT, MODE_NN) and not row_remap and _DIRECT and
@@ -390,6 +498,15 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
         key = f"{mode}|{M}|{N}|{K}|{lda}|{ldb}|{ldc}|{tuple(conv) if conv is not None else ''}|{int(row_remap)}|" \
               f"{act}|{C.dtype}|{int(bias is not None)}|{int(colstats is not None)}|{int(residual is not None)}"
         choice = _tuned.get(key)
+        if choice is None and online_ok and _online_active and not torch.cuda.is_current_stream_capturing():
+            global _online_last
+            st = _online.get(key)
+            if st is None:
+                cands = _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats)
+                st = _online[key] = {"cands": cands, "n": 0, "pending": [], "samples": {}}
+            choice = st["cands"][st["n"] % len(st["cands"])]
+            st["n"] += 1
+            _online_last = (key, choice)
         if choice is None:
             if torch.cuda.is_current_stream_capturing():   # cannot time inside a graph capture
                 choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
@@ -439,13 +556,20 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
     conv_arr = None
     if conv is not None:
         conv_arr = (ctypes.c_int * len(conv))(*[int(v) for v in conv])
+    global _online_last
+    _online_last = None
     choice = _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv, conv_arr, row_remap,
-                     residual, kernel, colstats, bnb)
-    if _trace is not None:
+                     residual, kernel, colstats, bnb, online_ok=True)
+    online = _online_last
+    _online_last = None
+    if _trace is not None or online is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
     _launch(choice[0], choice[1], mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap,
             residual, accumulate, colstats, bnb)
+    if online is not None:
+        e1.record()
+        _online[online[0]]["pending"].append((online[1], e0, e1))
     if _trace is not None:
         e1.record()
         _trace.append(((mode, M, N, K, tuple(conv) if conv is not None else None, act, bias is not None,

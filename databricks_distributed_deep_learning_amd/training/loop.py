@@ -259,8 +259,13 @@ class Trainer:
         steps = c.steps if steps is None else steps
         warmup = c.warmup_steps if warmup is None else warmup
         self.model.train()
-        for _ in range(warmup):
-            self.train_step()
+        # untuned GEMM signatures pick their kernels from their own calls in these warm-up
+        # steps (ops/_native_gemm.py online_tuning: in-model timing, not isolated benchmarks)
+        from ..ops import _native_gemm
+        with _native_gemm.online_tuning(enabled=self.device.type == "cuda"):
+            for _ in range(warmup):
+                self.train_step()
+                _native_gemm.online_collect()
         if warmup:
             self.agree_kernel_plans()
         self.phases.summary(reset=True)          # warm-up (and tuning) steps are not reported

@@ -45,6 +45,20 @@ while [ $# -gt 0 ]; do
         done
       done
       unset DDL_NATIVE_LIB ;;
+    plans)
+      # same-box BERT-base A/B of fixed GEMM plans (tune cache pre-filled from scripts/plans/*.json) and
+      # the retire-depth-0 library, alternating: ARM = plan[:lib]
+      for i in 1 2; do
+        for arm in bert_cur bert_bigtn bert_bigtn:dr0 bert_bigtn_b256; do
+          pl=${arm%%:*}; lib=${arm#*:}
+          if [ "$lib" = dr0 ]; then export DDL_NATIVE_LIB=$PWD/databricks_distributed_deep_learning_amd/_native/ab/libddl_dr0.so; else unset DDL_NATIVE_LIB; fi
+          cp scripts/plans/$pl.json gpurun_out/plan_cache.json
+          DDL_GEMM_TUNE_CACHE=$PWD/gpurun_out/plan_cache.json timeout -k 10 300 python bench.py --model bert_base --steps 30 --warmup 5 \
+            > gpurun_out/plans_${arm/:/_}_$i.log 2>&1 || { tail -20 gpurun_out/plans_${arm/:/_}_$i.log; exit 1; }
+          tail -1 gpurun_out/plans_${arm/:/_}_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print("plan", "'$arm'", d["value"], d.get("phases_ms"))'
+        done
+      done
+      unset DDL_NATIVE_LIB ;;
     bertx)
       n=3
       if [[ ${1:-} =~ ^[0-9]+$ ]]; then n=$1; shift; fi

@@ -41,7 +41,9 @@ def test_candidates_offer_hybrid_only_for_partial_rounds():
     assert not any(c[0] == "hybrid" for c in NG._candidates(NG.MODE_NT, 25216, 768, 3072, True, 3072, 3072))
 
 
-def test_big192_is_opt_in(monkeypatch):
+def test_big192_candidate(monkeypatch):
+    """256 x 192 tiles are offered for N % 192 == 0 NT / NN GEMMs (DDL_GEMM_192=0 drops them)."""
+    monkeypatch.setattr(NG, "_BIG192", False)
     assert not any(c[0] == "big192" for c in NG._candidates(NG.MODE_NT, 16384, 768, 768, False, 768, 768))
     monkeypatch.setattr(NG, "_BIG192", True)
     assert ("big192", 1) in NG._candidates(NG.MODE_NT, 16384, 768, 768, False, 768, 768)
@@ -55,3 +57,41 @@ def test_no_vendor_gemm_kind():
     assert "blas" not in NG._KINDS and not hasattr(NG, "_blas")
     for mode in (NG.MODE_NT, NG.MODE_NN, NG.MODE_TN):
         assert all(k in NG._KINDS for k, _ in NG._candidates(mode, 16384, 768, 768, False, 768, 768, plain=True))
+
+
+def test_online_tuning_commits_in_model_argmin(monkeypatch):
+    """In-model tuning: calls of an untuned signature cycle through its candidates while the
+    session is open; the committed choice is the candidate with the lowest median sample."""
+    import contextlib
+
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+        def synchronize(self):
+            pass
+
+    monkeypatch.setattr(NG, "_TUNE", True)
+    monkeypatch.setattr(NG, "_ONLINE", True)
+    monkeypatch.setattr(NG.torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(NG.torch.cuda, "synchronize", lambda *a: None)
+    NG._online.clear()
+    key = "k-online"
+    cands = [("big", 1), ("small", 2), ("big192", 1)]
+    times = {("big", 1): [5.0, 5.2, 4.9], ("small", 2): [6.0, 3.0, 6.5], ("big192", 1): [4.0, 4.1, 9.0]}
+    with NG.online_tuning(True):
+        assert NG._online_active
+        st = NG._online[key] = {"cands": cands, "n": 0, "pending": [], "samples": {}}
+        for i in range(9):
+            c = st["cands"][st["n"] % 3]
+            st["n"] += 1
+            t = times[c][i // 3]
+            st["pending"].append((c, Ev(0.0), Ev(t)))
+        NG.online_collect()
+        assert st["samples"][("small", 2)] == [6.0, 3.0, 6.5] and not st["pending"]
+    assert not NG._online_active and key not in NG._online
+    assert NG._tuned.pop(key) == ("big192", 1)          # medians 5.0 / 6.0 / 4.1
+    assert NG._timings.pop(key)[("small", 2)] == 6.0
