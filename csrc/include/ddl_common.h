@@ -263,11 +263,16 @@ __device__ __forceinline__ float colsum64(const float* __restrict__ part, int nr
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     if (ok) {
         int r = grp;
-        for (; r + 48 < nrows; r += 64) {
-            a0 += part[(long)r * ld + col];
-            a1 += part[(long)(r + 16) * ld + col];
-            a2 += part[(long)(r + 32) * ld + col];
-            a3 += part[(long)(r + 48) * ld + col];
+        // eight rows in flight per thread (the partial rows were just written: L2 latency,
+        // not bandwidth, bounds this loop -- a few hundred rows take 2-4 round trips)
+        for (; r + 112 < nrows; r += 128) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = part[(long)(r + 16 * i) * ld + col];
+            a0 += v[0] + v[4];
+            a1 += v[1] + v[5];
+            a2 += v[2] + v[6];
+            a3 += v[3] + v[7];
         }
         for (; r < nrows; r += 16) a0 += part[(long)r * ld + col];
     }

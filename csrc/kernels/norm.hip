@@ -793,15 +793,19 @@ __global__ __launch_bounds__(256) void bn_partials_collapse_k(const float* __res
 // Partial rows beyond this are first collapsed 32:1 (a single finalize block per
 // 64 columns is too little parallelism for ~1000 rows).  The caller allocates
 // `part` with room for the collapsed rows behind the nblk partial rows.
-// DDL_BN_COLLAPSE_MIN overrides both thresholds (this one and ddl_bn_partials_ws's 256)
+// DDL_BN_COLLAPSE_MIN overrides the threshold (collapse_partials and ddl_bn_partials_ws)
 static int collapse_env() {
     static const int v = [] { const char* e = getenv("DDL_BN_COLLAPSE_MIN"); return e ? atoi(e) : 0; }();
     return v;
 }
-constexpr int COLLAPSE_OVER = 64;
+// Up to COLLAPSE_OVER rows the single column-sum kernel reads every row itself (colsum64: 8 rows
+// in flight per thread, <= 4 round trips): the collapse launch cost more than it saved there
+// (BERT-base: 49 collapse launches of ~5 us per step for 128- and 512-row partials).
+constexpr int COLLAPSE_OVER = 512;
+static bool needs_collapse(int nblk) { return nblk > (collapse_env() > 0 ? collapse_env() : COLLAPSE_OVER); }
 static const float* collapse_partials(const float* part, int& nblk, int width, hipStream_t st,
                                       float* ws = nullptr) {
-    if (nblk <= (collapse_env() > 0 ? collapse_env() : COLLAPSE_OVER)) return part;
+    if (!needs_collapse(nblk)) return part;
     if (!ws) ws = const_cast<float*>(part) + (long)nblk * width;
     const int chunks = (nblk + PC_ROWS - 1) / PC_ROWS;
     bn_partials_collapse_k<<<dim3((width + 255) / 256, chunks), 256, 0, st>>>(part, nblk, width, ws);
@@ -810,7 +814,7 @@ static const float* collapse_partials(const float* part, int& nblk, int width, h
 }
 
 DDL_API long ddl_bn_partials_ws(int nblk, int C) {
-    return nblk > (collapse_env() > 0 ? collapse_env() : 256) ? (long)((nblk + PC_ROWS - 1) / PC_ROWS) * 2 * C : 0;
+    return needs_collapse(nblk) ? (long)((nblk + PC_ROWS - 1) / PC_ROWS) * 2 * C : 0;
 }
 
 DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, long M, int C, const void* gamma,

@@ -229,7 +229,7 @@ _NARROW_STATS = os.environ.get("DDL_TUNE_NARROW_STATS", "0") != "0"   # same-box
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
 _TUNE_ROUNDS = max(1, int(os.environ.get("DDL_GEMM_TUNE_ROUNDS", "5")))   # interleaved timing rounds per candidate
 _TUNE_COLD = os.environ.get("DDL_GEMM_TUNE_COLD", "1") != "0"             # time candidates from evicted caches
-_ONLINE = os.environ.get("DDL_GEMM_TUNE_ONLINE", "1") != "0"              # in-model tuning during warm-up
+_ONLINE = os.environ.get("DDL_GEMM_TUNE_ONLINE", "0") == "1"              # in-model tuning during warm-up (opt-in)
 # optional persistent cache (JSON): later processes skip the timing runs
 _CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
 
@@ -397,13 +397,14 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
 
 
 # ------------------------------------------------------------------ in-model (online) tuning
-# Timing candidates in isolation -- back to back on the same operands, even from evicted caches --
-# did not rank them the way the training step does: the BERT-base weight-gradient GEMMs went to
-# the 128x128 kernel, which won in isolation and ran ~30 % slower in the model (+1.7 ms/step,
-# profiles/kernels_bert_r04_hottuner.md).  During a trainer's warm-up steps an untuned signature
-# therefore cycles through its candidates on its REAL calls (every layer's call is a sample,
-# timed with events on the compute stream, read back once per step) and keeps the one with the
-# lowest median in-model time.  Results are identical whichever candidate runs a call.
+# Opt-in (DDL_GEMM_TUNE_ONLINE=1): during a trainer's warm-up steps an untuned signature cycles
+# through its candidates on its REAL calls (every layer's call is a sample, timed with events on the
+# compute stream, read back once per step) and keeps the one with the lowest median in-model time.
+# It was built when the isolated tuner kept the BERT-base weight-gradient GEMMs on the 128x128
+# kernel; the cause turned out to be register spills in the 256x256 kernel's TN loop
+# (profiles/gemm_spills_r04.md), and with those fixed both tuners pick the same plan.  It stays off
+# by default because the candidates differ in split-K summation order: warm-up steps then round
+# differently than in a process whose tune cache is already warm (runs are not bit-reproducible).
 _online_active = False
 _online: dict = {}          # key -> {"cands": [...], "n": calls, "pending": [(cand, e0, e1)], "samples": {}}
 _online_last = None         # (key, cand) of the call _choose just routed online

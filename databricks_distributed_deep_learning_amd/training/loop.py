@@ -259,8 +259,8 @@ class Trainer:
         steps = c.steps if steps is None else steps
         warmup = c.warmup_steps if warmup is None else warmup
         self.model.train()
-        # untuned GEMM signatures pick their kernels from their own calls in these warm-up
-        # steps (ops/_native_gemm.py online_tuning: in-model timing, not isolated benchmarks)
+        # DDL_GEMM_TUNE_ONLINE=1: untuned GEMM signatures pick their kernels from their own calls
+        # in these warm-up steps (ops/_native_gemm.py online_tuning); otherwise a no-op
         from ..ops import _native_gemm
         with _native_gemm.online_tuning(enabled=self.device.type == "cuda"):
             for _ in range(warmup):
