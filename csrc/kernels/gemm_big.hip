@@ -501,7 +501,8 @@ __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const 
 //   EK_BF16: interior tile, bf16 out, optional bf16 bias / residual -- one 16-byte store per
 //            two sites (N, ldc % 8 == 0)
 //   EK_GELU: interior tile, bf16 out = GELU(acc + bf16 bias), pre-activation to aux (likewise)
-//   EK_DGELU: interior tile, bf16 out = acc * GELU'(aux) (+ column sums for the bias gradient)
+//   EK_DGELU: interior tile, bf16 out = acc * GELU'(aux) (+ column sums for the bias gradient), pair
+//             stores like EK_BF16 (N, ldc % 8 == 0)
 //   EK_F32 : interior tile, fp32 split-K partial or fp32 out (+accumulate) -- one 16-byte store
 //   EK_GEN : anything direct4 covers, with bounds checks (edge tiles)
 // With colstats (EK_BF16 / EK_GEN) the BatchNorm statistics of the bf16 output --
@@ -515,7 +516,9 @@ __device__ __forceinline__ int col_base(int n0, int qn, int wn, int j) {
     return n0 + qn * 128 + ((N192 && qn) ? wn * 16 : wn * 32 + j * 16);
 }
 
-template <int EK, bool N192 = false>
+// HOIST: the residual / pre-activation loads of all column groups up front (off in the weight-gradient
+// kernels, whose only bf16 tiles are rare unsplit ones: the extra registers spilled their main loop)
+template <int EK, bool N192 = false, bool HOIST = true>
 __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
                                            int wm, int wn, int lane, int split) {
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
@@ -533,6 +536,29 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                 bpre[qn][j] = (N192 && qn && j) ? make_uint2(0u, 0u)
                                                 : *reinterpret_cast<const uint2*>((const bf16_t*)p.bias +
                                                                                   col_base<N192>(n0, qn, wn, j) + g4);
+    }
+    // residual (bf16 tiles) / saved pre-activation (dGELU): ALL column groups' loads go out before
+    // the first store -- per group they cost one exposed load latency each (p.C may alias them, so
+    // no load can move above an earlier group's stores); 16 / 32 extra VGPRs, free after the loop
+    const bf16_t* pre = EK == EK_BF16 ? p.res : (EK == EK_DGELU ? (const bf16_t*)p.aux : nullptr);
+    uint2 rball[2][2][2][4];
+    auto load_pre = [&](int qn, int j) {
+        const int n = col_base<N192>(n0, qn, wn, j) + g4;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                rball[qn][j][qm][i] = *reinterpret_cast<const uint2*>(
+                    pre + (long)(m0 + qm * 128 + wm * 64 + i * 16 + r16) * p.ldc + n);
+    };
+    if (HOIST && (EK == EK_BF16 || EK == EK_DGELU) && pre) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (N192 && qn && j) continue;
+                load_pre(qn, j);
+            }
     }
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
@@ -597,20 +623,10 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         }
                     }
             } else {
-            // bf16 residual: the column group's 8 sites load together before any store
-            // (p.C may alias p.res for all the compiler knows, so it would otherwise wait
-            // out one load latency per site -- residual-adding dgrads ran at ~2-3 TB/s)
-            // (dGELU: the saved pre-activation likewise)
-            uint2 rb[2][4];
-            const bf16_t* pre = EK == EK_BF16 ? p.res : (EK == EK_DGELU ? (const bf16_t*)p.aux : nullptr);
-            if ((EK == EK_BF16 || EK == EK_DGELU) && pre) {
-#pragma unroll
-                for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        rb[qm][i] = *reinterpret_cast<const uint2*>(
-                            pre + (long)(m0 + qm * 128 + wm * 64 + i * 16 + r16) * p.ldc + n);
-            }
+            // (the residual / pre-activation sites of this group were loaded above, rball; without
+            // HOIST the group's 8 sites load together here, before any of its stores)
+            if (!HOIST && (EK == EK_BF16 || EK == EK_DGELU) && pre) load_pre(qn, j);
+            uint2 (&rb)[2][4] = rball[qn][j];
             // EK_BF16 / EK_GELU store two sites (row blocks i, i + 1) per lane as ONE 16-byte
             // store: v_permlane16_swap hands the odd lane rows (g = 1, 3) the even rows' quads
             // of row block i + 1 in exchange for theirs of row block i, so each lane holds 8
@@ -673,7 +689,9 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         const f32x2_t d0 = f32x2_t{a[0], a[1]} * gelu_erf_grad2(f32x2_t{z[0], z[1]});
                         const f32x2_t d1 = f32x2_t{a[2], a[3]} * gelu_erf_grad2(f32x2_t{z[2], z[3]});
                         const uint32_t lo = pack2bf(d0.x, d0.y), hi = pack2bf(d1.x, d1.y);
-                        *reinterpret_cast<uint2*>((bf16_t*)p.C + o) = make_uint2(lo, hi);
+                        (void)o;
+                        if ((i & 1) == 0) { plo = lo; phi = hi; }
+                        else store_pair(p.C, plo, phi, lo, hi, m);
                         if (stats) {
                             const float t[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                                 __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
@@ -803,6 +821,7 @@ template <int LA, int LB, bool KTAIL, bool DIRECT, bool BNB = false, bool EDGE =
 __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     static_assert(!N192 || (DIRECT && !BNB), "192-wide tiles: register epilogue only");
     constexpr int TBN = N192 ? 192 : TB;
+    constexpr bool WGRAD = LA == KO && LB == KO;   // TN: weight gradients (split-K fp32 / accumulate)
     // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
     // makes the compiler's LDS-DMA alias tracking wait vmcnt(0) before fragment reads)
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF + 16];
@@ -1211,12 +1230,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                     if (nK > 0) prologueE();
                 }
             } else if (interior && p.ek == EK_BF16)
-                epi_direct<EK_BF16, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_BF16, N192, !WGRAD>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_F32)
                 epi_direct<EK_F32, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_GELU)
                 epi_direct<EK_GELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
-            else if (interior && p.ek == EK_DGELU)
+            else if (!WGRAD && interior && p.ek == EK_DGELU)   // (never a weight gradient's)
                 epi_direct<EK_DGELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if constexpr (EDGE)
                 epi_direct<EK_GEN, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
@@ -1532,7 +1551,8 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_GELU && (!p.bias || p.bias_bf16) && !p.row_remap && !p.res)
         p.ek = (p.N % 8 == 0 && p.ldc % 8 == 0) ? EK_GELU : EK_GEN;
     else if (!p.out_f32 && !p.accumulate && p.act == ACT_DGELU && p.aux && !p.bias && !p.row_remap && !p.res)
-        p.ek = (p.N % 4 == 0 && p.ldc % 4 == 0) ? EK_DGELU : EK_GEN;
+        p.ek = (p.N % 8 == 0 && p.ldc % 8 == 0 && !(LA == KO && LB == KO)) ? EK_DGELU : EK_GEN;   // 16-byte pair
+        // stores; the weight-gradient (TN) kernels carry no dGELU epilogue (gemm_big_k WGRAD)
     else
         p.ek = EK_GEN;
     kp.ek = p.ek;
