@@ -53,6 +53,14 @@ namespace {
 #ifndef DDL_DEEP_RETIRE
 #define DDL_DEEP_RETIRE 2
 #endif
+// Phases 1 / 5 issue the B fragments of phases 2 / 6 (quadrant (0,1)) right after their own reads
+// complete, so they land under that phase's MFMAs: the halves they read (E-B1 / O-B1) were retired
+// two phases earlier and are restaged only at phases 4 / 8; fb1 is free from phase 7 / 3 on.
+// Phases 2 / 6 then issue no fragment reads.  (DR 0 / 2 main loops, B k-contiguous only: PF_B1 in
+// gemm_big_k; 0 = read in phases 2 / 6)
+#ifndef DDL_PREFETCH_B1
+#define DDL_PREFETCH_B1 1
+#endif
 #ifndef DDL_GEMM_EPI_LDS_CODE
 #define DDL_GEMM_EPI_LDS_CODE 0   // whole-row LDS epilogue experiment (epi_lds_bf16): not compiled in
 #endif
@@ -822,6 +830,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     static_assert(!N192 || (DIRECT && !BNB), "192-wide tiles: register epilogue only");
     constexpr int TBN = N192 ? 192 : TB;
     constexpr bool WGRAD = LA == KO && LB == KO;   // TN: weight gradients (split-K fp32 / accumulate)
+    // B-fragment prefetch (DDL_PREFETCH_B1) where B is k-contiguous (NT, implicit-GEMM conv forward):
+    // 8192^3 NT -32 % cycles, 4096^3 -20 %; with transposed B reads (NN / TN) it measured slower
+    // (TN: the extra live range spilled its main loop)
+    constexpr bool PF_B1 = DDL_PREFETCH_B1 && LB == KC;
     // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
     // makes the compiler's LDS-DMA alias tracking wait vmcnt(0) before fragment reads)
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF + 16];
@@ -1005,10 +1017,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
         readB(0, 0, fb0);
         if (stO1) sa.stage(p, smem, 1, 1, kE + 1);
         READS_DONE_BARRIER();
+        if (PF_B1) readB(0, 1, fb1);   // phase 2's B fragments, under this phase's MFMAs
         mma(0, 0, fb0);
         BARRIER();
         // phase 2: E (0,1)
-        readB(0, 1, fb1);
+        if (!PF_B1) readB(0, 1, fb1);
         if (more) sa.stage(p, smem, 0, 0, kE + 2);
 #if DDL_DEEP_RETIRE == 2
         // E-A1 (staged at the previous pair's phase 5) retired here, read in phase 3
@@ -1134,10 +1147,11 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 readB(1, 0, fb0);
                 if (more) sa.stage(p, smem, 0, 1, kE + 2);
                 READS_DONE_BARRIER();
+                if (PF_B1) readB(1, 1, fb1);   // O-B1 landed at phase 4
                 mma(0, 0, fb0);
                 BARRIER();
                 // phase 6: O (0,1)
-                readB(1, 1, fb1);
+                if (!PF_B1) readB(1, 1, fb1);
                 if (moreO) sa.stage(p, smem, 1, 0, kO + 2);
 #if DDL_DEEP_RETIRE == 2
                 if (BNB || !(it == 0 && hold_o)) {        // O-A1 (phase 1), read in phase 7
