@@ -915,7 +915,14 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag<LA>(hb, wm * 64 + i * 16, kk);
+            for (int kk = 0; kk < 2; ++kk) {
+#ifdef DDL_DIAG_A_ROWREADS
+                // diagnostic builds only (wrong results): A fragments by row reads whatever the layout
+                fa[i][kk] = frag<KC>(hb, wm * 64 + i * 16, kk);
+#else
+                fa[i][kk] = frag<LA>(hb, wm * 64 + i * 16, kk);
+#endif
+            }
     };
     auto readB = [&](int buf, int qn, bf16x8 (&fb)[2][2]) {
         const char* hb = smem + half_off(buf, 1, qn);
