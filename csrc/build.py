@@ -52,9 +52,15 @@ def needs(src, obj, hdr_mtime):
     return os.path.getmtime(src) > m or hdr_mtime > m
 
 
+# per-source extra flags: gemm_big.hip's 4-wave weight-gradient kernel needs the VGPR form of the
+# MFMA instructions (its AGPR-form accumulators were shuffled around every MFMA; the other kernels'
+# code is identical with it -- profiles/gemm_spills_r04.md)
+EXTRA = {"gemm_big.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def compile_one(src, debug=False):
     obj = obj_for(src)
-    flags = list(COMMON)
+    flags = list(COMMON) + EXTRA.get(os.path.basename(src), [])
     if debug:
         flags = [f for f in flags if f != "-O3"] + ["-O1", "-g"]
     if src.endswith(".cpp"):

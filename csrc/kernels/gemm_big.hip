@@ -111,6 +111,7 @@ struct BigParams {
     const float* bn_mean;
     const float* bn_istd;
     int* sched;               // persistent grid: per-XCD tile tickets (null: static tile striding)
+    int xsplit;               // split-K on a 1-D grid whose XCDs run contiguous (split, tile) runs
 };
 // tile-ticket slot layout: 8 per-XCD counters + one exit counter, 128 B apart
 constexpr int SCHED_STRIDE = 32;
@@ -841,9 +842,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     int tm, tn, m0, n0;
     // XCD-aware bijective remap: an XCD (blockIdx & 7) owns a contiguous range of
     // tile ids; a persistent block's later tiles keep its XCD (gridDim.x % 8 == 0)
-    auto coords = [&](int bid) {
+    auto coords = [&](int bid, bool remap = true) {
         const int xcd = bid & 7, qn_ = nwg >> 3, rn = nwg & 7;
-        const int wg = (xcd < rn ? xcd * (qn_ + 1) : rn * (qn_ + 1) + (xcd - rn) * qn_) + (bid >> 3);
+        const int wg = remap ? (xcd < rn ? xcd * (qn_ + 1) : rn * (qn_ + 1) + (xcd - rn) * qn_) + (bid >> 3) : bid;
         // grouped order: consecutive tiles (the ones an XCD runs together) cover a
         // GROUP_M x k block of tiles instead of one long row, so the A and B panels
         // they stream stay L2-resident at large M, N
@@ -876,16 +877,29 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     auto publish = [&]() {
         if (DYN && p.sched && threadIdx.x == 0) s_tick = tick;
     };
-    int vt = blockIdx.x;
+    int vt = blockIdx.x, split = blockIdx.y;
 #ifdef DDL_GEMM_STAMPS
     int stamp_ti = 0;
 #endif
-    coords(vt);
+    if (p.xsplit) {
+        // split-K (one block per (tile, split), a 1-D grid): workgroups go to the XCDs round-robin,
+        // so XCD x gets blocks x, x + 8, ...; they are given a CONTIGUOUS run of the split-major
+        // (split, tile) order -- mostly one split's k-range over neighbouring tiles, whose A / B
+        // panel rows then come from HBM once into that XCD's L2 and serve every tile that reads
+        // them (with blockIdx.y = split, an XCD's blocks spread over all splits: the TN weight
+        // gradients streamed ~5x their unique bytes at the HBM rate)
+        const int n = nwg * p.splits, xcd = blockIdx.x & 7, qn_ = n >> 3, rn = n & 7;
+        const int q = (xcd < rn ? xcd * (qn_ + 1) : rn * (qn_ + 1) + (xcd - rn) * qn_) + (int)(blockIdx.x >> 3);
+        split = q / nwg;
+        vt = q - split * nwg;
+        coords(vt, false);
+    } else {
+        coords(vt);
+    }
     ask();
     STAMP(0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = w >> 2, wn = w & 3;
-    const int split = blockIdx.y;
     const int nK_total = (p.K + BK - 1) / BK;
     const int kt0 = split * p.kt_per_split;
     const int kt_end = min(nK_total, kt0 + p.kt_per_split);
@@ -1442,6 +1456,132 @@ __global__ __launch_bounds__(256) void big_reduce_k(BigParams p, const float* __
     }
 }
 
+// ------------------------------------------------------------------ weight-gradient kernel ("wg")
+// C[M, N] (+)= A^T B with A = [K][M] and B = [K][N] both k-outer: the TN weight gradients
+// (dW = dY^T X over K = tokens / pixels).  The 8-wave kernel above reads a k-outer A operand with
+// twice the transposed LDS reads of a row operand and, at two waves per SIMD (256 registers), has
+// no registers to read ahead: each phase waits for its reads before its MFMAs
+// (profiles/pmc_gemm_modes_r04.md: TN 5.0 K cycles per 64-deep k-tile vs NN 3.1 K).  Here 4 waves
+// (one per SIMD, 512 registers each) own 128 x 64 of a 256 x 128 tile (acc 128 registers) and never
+// wait for a read they just issued: tile t+1's fragments replace tile t's as soon as the MFMAs
+// reading them have issued.  (128 x 128 per wave needs the
+// whole 256-AGPR file for its accumulators and spilled them.)  Operands arrive by LDS-DMA in 32-deep
+// k-tiles through a 4-stage ring (3 tiles in flight), in the swizzled k-outer image of the 8-wave
+// kernel (frag<KO>).  Output: fp32 split-K partials; big_reduce_k sums them and applies accumulate
+// and the output dtype (also for one split).
+// Needs M % 256 == 0, N % 128 == 0, K % 32 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-byte aligned operands.
+constexpr int WG_NTH = 256, WG_BK = 32, WG_ST = 4, WG_TN = 128;
+constexpr int WG_HALF = WG_BK * 256;     // bytes: 32 k-rows x 128 columns x 2 B
+constexpr int WG_DMA = 6;                // DMA instructions per wave per k-tile (A: 2 halves x 2, B: 2)
+// stage s: A half 0, A half 1, B
+__device__ __forceinline__ int wg_off(int s, int x, int h) { return (s * 3 + x * 2 + h) * WG_HALF; }
+
+// (This file is compiled with -mllvm -amdgpu-mfma-vgpr-form, csrc/build.py: with the AGPR form the
+// allocator gave each MFMA a destination other than its accumulator input and shuffled the
+// accumulators through v_accvgpr moves around every MFMA of this kernel -- 2.7x its MFMA time.
+// The 8-wave kernels' code is identical either way.)
+__global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[WG_ST * 3 * WG_HALF];   // 96 KB, one LDS object
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int wm = w >> 1, wn = w & 1;
+    // 1-D grid of (split, tile) blocks; XCD x (blocks x, x + 8, ...) runs a contiguous run of the
+    // split-major order, so its blocks share k-rows of the A / B panels in its L2 (gemm_big_k xsplit)
+    const int nwg = p.tiles_m * p.tiles_n;
+    const int n = nwg * p.splits, xcd = blockIdx.x & 7, qn = n >> 3, rn = n & 7;
+    const int q = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (int)(blockIdx.x >> 3);
+    const int split = q / nwg, tile = q - split * nwg;
+    const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+    const int m0 = tm * 256, n0 = tn * WG_TN;
+    const int nkt = p.K / WG_BK;
+    const int kt0 = split * p.kt_per_split;
+    const int nt = min(nkt, kt0 + p.kt_per_split) - kt0;      // >= 1 (host)
+    // DMA lanes: k-row krow0 (+4 for j = 1) of a 32-row half, 16-byte chunk c of its 128 columns,
+    // stored at the swizzled slot l & 15 (swz_ko ignores bit 2: the same c for both j)
+    const int krow0 = (w * 2) * 4 + (l >> 4);
+    const int c = (l & 15) ^ swz_ko(krow0);
+    const bf16_t* ga = p.A + (long)krow0 * p.lda + m0 + 8 * c;
+    const bf16_t* gb = p.B + (long)krow0 * p.ldb + n0 + 8 * c;
+    auto stage = [&](int kt, int st) {
+        const long ka = (long)kt * WG_BK;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            glds(ga + (ka + j * 4) * p.lda, smem + wg_off(st, 0, 0) + (w * 2 + j) * 1024);
+            glds(ga + (ka + j * 4) * p.lda + 128, smem + wg_off(st, 0, 1) + (w * 2 + j) * 1024);
+            glds(gb + (ka + j * 4) * p.ldb, smem + wg_off(st, 1, 0) + (w * 2 + j) * 1024);
+        }
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // one set of fragments in registers (A: 8 row blocks, B: 4 column blocks); tile t+1's overwrite
+    // tile t's as soon as the MFMAs that read them have issued: A rows 0-3 under the MFMAs of rows
+    // 4-7, A rows 4-7 and B at the end of the tile, landing under the next tile's barrier
+    bf16x8 fa[8], fb[4];
+    auto readA = [&](int st, int i0) {
+        const char* ha = smem + wg_off(st, 0, wm);
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i) fa[i] = frag<KO>(ha, i * 16, 0);
+    };
+    auto readB = [&](int st) {
+        const char* hb = smem + wg_off(st, 1, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag<KO>(hb, wn * 64 + j * 16, 0);
+    };
+    auto mma4 = [&](int i0) {
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    };
+    // Branch-free steady state: every iteration stages a tile (past the last one it re-stages the
+    // last, into the slot no longer read), waits, syncs and reads the next tile's fragments (past
+    // the end: a stale slot, never used) -- accumulators crossing a branch were copied between
+    // AGPRs and VGPRs (64 v_accvgpr_write + hazard nops per 16 MFMAs).
+    const int ktl = kt0 + nt - 1;
+    // prologue: tiles 0..2 in flight (8 - 2 of them possibly re-stages of the last), tile 0 landed
+    stage(kt0, 0);
+    stage(min(kt0 + 1, ktl), 1);
+    stage(min(kt0 + 2, ktl), 2);
+    VMN(12);
+    BARRIER();
+    readB(0);
+    readA(0, 0);
+    readA(0, 4);
+    // one k-tile per iteration: tile t+1 landed (tile t+2 may still be in flight) and made visible by
+    // the barrier -- which also orders every wave's reads of tile t-1 (issued in the iteration before,
+    // consumed by its MFMAs) before slot (t+3) % 4 = (t-1) % 4 is restaged.  One loop body, no
+    // unrolling, no register copies (two alternating fragment sets made the allocator rotate the
+    // accumulators through VGPR copies).
+#pragma unroll 1
+    for (int t = 0; t < nt; ++t) {
+#ifndef DDL_DIAG_WG_NODMA   // diagnostic builds only (wrong results): no operand DMA after the prologue
+        VMN(6);
+#endif
+        BARRIER();
+        mma4(0);
+        readA((t + 1) & 3, 0);
+#ifndef DDL_DIAG_WG_NODMA
+        stage(min(kt0 + t + 3, ktl), (t + 3) & 3);
+#endif
+        mma4(4);
+        readA((t + 1) & 3, 4);
+        readB((t + 1) & 3);
+    }
+    VM0();      // no LDS-DMA may outlive the workgroup's LDS
+    // fp32 partial tile: lane holds C[m][n .. n+3] of each 16 x 16 block (the MFMA layout)
+    float* out = (float*)p.C + (long)split * p.split_stride;
+    const int r16 = l & 15, g4 = (l >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            *reinterpret_cast<f32x4*>(out + (long)(m0 + wm * 128 + i * 16 + r16) * p.ldc + n0 + wn * 64 + j * 16 + g4) =
+                acc[i][j];
+}
+
 void fill_conv(ConvDesc& cd, const int* d) {
     cd.N = d[0]; cd.H = d[1]; cd.W = d[2]; cd.C = d[3]; cd.P = d[4]; cd.Q = d[5];
     cd.stride = d[6]; cd.h_off = d[7]; cd.w_off = d[8]; cd.h_step = d[9]; cd.w_step = d[10];
@@ -1481,6 +1621,15 @@ bool edge_split_enabled() {
     static const bool on = [] {
         const char* e = getenv("DDL_GEMM_LEAN");
         return e && e[0] == '1';
+    }();
+    return on;
+}
+
+// DDL_GEMM_XSPLIT=0: split-K grids as (tiles, splits) with blockIdx.y = split (A/B timing)
+bool xsplit_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_XSPLIT");
+        return !(e && e[0] == '0');
     }();
     return on;
 }
@@ -1591,7 +1740,9 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
         gx = std::min(nwg, cap);
         if (gx < nwg && p.act != ACT_BNB && dynamic_enabled()) kp.sched = sched_slot(st);
     }
-    const dim3 grid(gx, splits);
+    // split-K: a 1-D grid whose XCDs each run a contiguous (split, tile) range (gemm_big_k xsplit)
+    kp.xsplit = splits > 1 && xsplit_enabled();
+    const dim3 grid(kp.xsplit ? gx * splits : gx, kp.xsplit ? 1 : splits);
     if (direct) {
         if constexpr (LB == KC && (LA == KC || LA == CONV)) {   // dgrad operand layouts
             if (p.act == ACT_BNB) {
@@ -1673,4 +1824,36 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
         case 3: return launch_big<CONV, KC>(p, workspace, ws_elems, splits, st);
         default: return -1;   // conv wgrad (CONVW) stays on the 128x128 kernel (gemm.hip)
     }
+}
+
+// TN weight gradient on the 4-wave kernel (gemm_wg_k): C[M, N] (+)= A^T B, A = [K][M] (lda), B = [K][N]
+// (ldb); fp32 partials in `workspace` (splits x M x ldc floats, also for one split), then the reduce
+// applies accumulate / the output dtype.  Returns -1 when the shape is outside the kernel's contract.
+DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                           int out_f32, int splits, float* workspace, long ws_elems, int accumulate, hipStream_t st) {
+    if (M <= 0 || N <= 0) return 0;
+    if (M % 256 || N % WG_TN || K <= 0 || K % WG_BK || lda % 8 || ldb % 8 || ldc % 4 || ldc < N ||
+        ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+        return -1;
+    BigParams p{};
+    p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
+    p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+    p.act = ACT_NONE; p.accumulate = accumulate; p.out_f32 = out_f32;
+    p.tiles_m = M / 256;
+    p.tiles_n = N / WG_TN;
+    const int nkt = K / WG_BK;
+    if (splits < 1) splits = 1;
+    if (splits > nkt) splits = nkt;
+    p.kt_per_split = (nkt + splits - 1) / splits;
+    splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
+    p.splits = splits;
+    p.split_stride = (long)M * ldc;
+    if (!workspace || ws_elems < p.split_stride * splits) return -2;
+    BigParams kp = p;
+    kp.C = workspace;
+    hipLaunchKernelGGL(gemm_wg_k, dim3(p.tiles_m * p.tiles_n * splits), dim3(WG_NTH), 0, st, kp);
+    const long total = (long)M * ((N + 3) / 4);
+    const int g = (int)std::min<long>(16384, (total + 255) / 256);
+    big_reduce_k<<<g, 256, 0, st>>>(p, workspace);
+    return (int)hipGetLastError();
 }

@@ -15,6 +15,7 @@ from ._lib import I, L, P
 _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_n64": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
+               "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -36,7 +37,7 @@ def set_big_gemm(enabled: bool) -> None:
 
 
 _forced: Optional[str] = None
-_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow")
+_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg")
 # per-call device timing for diagnostics (scripts/debug/gemm_trace.py): list of
 # (signature, (kernel, splits), start event, end event) while enabled
 _trace: Optional[list] = None
@@ -159,6 +160,17 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
         A, lda, B, ldb, M, N = B, ldb, A, lda, N, M
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
     out_f32 = 1 if C.dtype == torch.float32 else 0
+    if kind == "wg":
+        if (mode == MODE_TN and bias is None and act is None and residual is None and colstats is None
+                and not row_remap and wg_ok(M, N, K, lda, ldb) and ldc % 4 == 0
+                and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0):
+            ws = torch.empty(max(1, s) * M * ldc, dtype=torch.float32, device=C.device)
+            rc = _lib.fn("ddl_gemm_wgrad")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, out_f32,
+                                           s, ws.data_ptr(), ws.numel(), int(accumulate), _lib.stream())
+            if rc != 0:
+                raise RuntimeError(f"ddl_gemm_wgrad(M={M}, N={N}, K={K}, splits={s}) failed: {rc}")
+            return
+        kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
     ws = torch.empty(s * M * (N if mode & TRANS_OUT else ldc), dtype=torch.float32, device=C.device) \
         if s > 1 else None
     args = (mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, _lib.p(bias), bias_bf16,
@@ -197,6 +209,10 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
     if N <= 192 or N % 128 == 64:     # 128x64 tiles: no half-empty column tile
         ns = 1 if row_remap else pick_splits(M, 2 * N, K)   # 128x64 tiles = 128x128 tiles on 2N
         out += [("narrow", s) for s in sorted({1, max(1, ns // 2), ns})]
+    if _WG and mode == MODE_TN and plain and wg_ok(M, N, K, lda, ldb):
+        # 4-wave weight-gradient kernel (gemm_big.hip gemm_wg_k): 256x128 tiles, fp32 partials + reduce
+        ws_ = big_splits(M, 2 * N, K)      # 256x128 tiles = 256x256 tiles on 2N
+        out += [("wg", s) for s in sorted({max(1, ws_ // 2), ws_, 2 * ws_})]
     if mode in (MODE_TN, MODE_CONVW) and plain and (M <= 192 or M % 128 == 64):
         ts = pick_splits(N, 2 * M, K)     # transposed: N' = M (output channels) on 64-wide tiles
         out += [("tnarrow", s) for s in sorted({1, max(1, ts // 2), ts})]
@@ -210,6 +226,14 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
         if hy is not None:                # a partial last round of 256x256 tiles
             out += [("hybrid", s) for s in sorted({2, max(2, hy[1] // 2), hy[1]})]
     return out
+
+
+_WG = os.environ.get("DDL_GEMM_WG", "1") != "0"   # tuner candidate "wg" (A/B: 0 = never)
+
+
+def wg_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
+    """Shapes the 4-wave weight-gradient kernel takes (ddl_gemm_wgrad's contract: 256x128 tiles)."""
+    return M % 256 == 0 and N % 128 == 0 and K % 32 == 0 and K > 0 and lda % 8 == 0 and ldb % 8 == 0
 
 
 def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):
@@ -486,6 +510,9 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
         elif kernel == "narrow":
             choice = ("narrow", 1 if row_remap else pick_splits(M, 2 * N, K, splits))
+        elif kernel == "wg" and mode == MODE_TN and bias is None and act is None and residual is None \
+                and not row_remap and colstats is None and wg_ok(M, N, K, lda, ldb):
+            choice = ("wg", splits or big_splits(M, N, K))
         elif kernel == "tnarrow" and mode in (MODE_TN, MODE_CONVW) and bias is None and act is None \
                 and residual is None and not row_remap and colstats is None:
             choice = ("tnarrow", pick_splits(N, 2 * M, K, splits))
@@ -543,7 +570,8 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
     """C = op(A) op(B) (+ epilogue).  ``kernel`` forces "big" (256x256), "small" (128x128),
     "narrow" (128x64), "tnarrow" (weight gradient computed transposed on 128x64 tiles), "big192"
     (256x192 tiles of the 256x256 kernel: NT / NN, register epilogue) or
-    "hybrid" (256x256 tiles, the rows past the last whole round split-K: ``hybrid_rows``).  Every
+    "hybrid" (256x256 tiles, the rows past the last whole round split-K: ``hybrid_rows``) or "wg" (TN weight
+    gradients on the 4-wave 256x256 kernel, fp32 partials + reduce: ``wg_ok`` shapes).  Every
     kind is a hand-written kernel of this library (no vendor GEMM library is ever called).
 
     ``colstats`` (fp32, >= ceil(M/128) * 2N elements): the epilogue also writes BatchNorm

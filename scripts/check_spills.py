@@ -1,7 +1,7 @@
 """Register-spill check for the hand-written GEMM kernels (profiles/gemm_spills_r04.md).
 
 Emits the gfx950 device assembly of a kernel source (``hipcc --cuda-device-only -S``, ~4 min for
-gemm_big.hip) or reads an existing ``.s`` and reports, per ``gemm_big_k`` instantiation, the scratch
+gemm_big.hip) or reads an existing ``.s`` and reports, per ``gemm_big_k`` instantiation and for ``gemm_wg_k``, the scratch
 (spill) instructions in the whole body and inside its MFMA main loop (the span between the first and
 last ``v_mfma`` of the densest cluster).  Exits 1 if any main loop holds more than ``--max-loop``.
 
@@ -16,7 +16,7 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PAT = re.compile(r"\n(_ZN\w*gemm_big_k\w+):[^\n]*\n(.*?)\.Lfunc_end", re.S)
+PAT = re.compile(r"\n(_ZN\w*gemm_(?:big|wg)_k\w*):[^\n]*\n(.*?)\.Lfunc_end", re.S)
 TPL = re.compile(r"gemm_big_kILi(\d)ELi(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E")
 
 
@@ -24,6 +24,8 @@ def emit(src: str, out: str, defines) -> None:
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I",
            os.path.join(ROOT, "csrc", "include"), "-ffp-contract=fast", "-munsafe-fp-atomics", "-x", "hip",
            "--cuda-device-only", "-S", src, "-o", out] + [f"-D{d}" for d in defines]
+    if os.path.basename(src) == "gemm_big.hip":     # the library's flags for it (csrc/build.py EXTRA)
+        cmd += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
     subprocess.run(cmd, check=True)
 
 
@@ -32,7 +34,7 @@ def scan(text: str):
     for m in PAT.finditer(text):
         name, body = m.group(1), m.group(2)
         t = TPL.search(name)
-        tag = "".join(t.groups()) if t else name[-40:]
+        tag = "".join(t.groups()) if t else "wg" if "gemm_wg_k" in name else name[-40:]
         lines = body.split("\n")
         mf = [i for i, ln in enumerate(lines) if "v_mfma" in ln]
         sc = [i for i, ln in enumerate(lines) if "scratch_" in ln]

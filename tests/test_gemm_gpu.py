@@ -51,6 +51,42 @@ def test_gemm_modes(M, N, K, kernel):
     assert _rel_err(dw32, dy.float().t() @ a.float()) < 1e-3
 
 
+@pytest.mark.parametrize("Mo,No,Kr", [(256, 128, 32), (512, 384, 1056), (768, 256, 4096), (2304, 768, 1024)])
+@pytest.mark.parametrize("splits", [1, 2, 5])
+def test_wgrad_kernel(Mo, No, Kr, splits):
+    """4-wave weight-gradient kernel ("wg", gemm_big.hip gemm_wg_k): dW = dY^T X over the reduction,
+    fp32 partials + reduce; bf16 / fp32 outputs, plain and accumulating, vs an fp32 reference."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops._native_gemm import MODE_TN, gemm
+    torch.manual_seed(Mo + No + Kr + splits)
+    dy = torch.randn(Kr, Mo, device=dev).to(torch.bfloat16)
+    x = torch.randn(Kr, No, device=dev).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    dw = torch.empty(Mo, No, device=dev, dtype=torch.bfloat16)
+    gemm(MODE_TN, dy, Mo, x, No, dw, No, Mo, No, Kr, kernel="wg", splits=splits)
+    assert _rel_err(dw, ref) < 1e-2
+    prev = torch.randn(Mo, No, device=dev)
+    acc32 = prev.clone()
+    gemm(MODE_TN, dy, Mo, x, No, acc32, No, Mo, No, Kr, kernel="wg", splits=splits, accumulate=True)
+    assert _rel_err(acc32, prev + ref) < 1e-3
+    acc16 = prev.to(torch.bfloat16)
+    gemm(MODE_TN, dy, Mo, x, No, acc16, No, Mo, No, Kr, kernel="wg", splits=splits, accumulate=True)
+    assert _rel_err(acc16, prev + ref) < 1e-2
+
+
+def test_wgrad_kernel_contract():
+    """Shapes outside the 4-wave kernel's contract (M % 256, N % 128, K % 32) run another kernel."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    assert NG.wg_ok(768, 2304, 16384, 768, 2304) and not NG.wg_ok(200, 256, 64, 200, 256)
+    assert not NG.wg_ok(256, 256, 48, 256, 256)
+    dy = torch.randn(96, 200, device=dev).to(torch.bfloat16)
+    x = torch.randn(96, 256, device=dev).to(torch.bfloat16)
+    dw = torch.empty(200, 256, device=dev, dtype=torch.bfloat16)
+    NG.gemm(NG.MODE_TN, dy, 200, x, 256, dw, 256, 200, 256, 96, kernel="wg")
+    assert _rel_err(dw, dy.float().t() @ x.float()) < 1e-2
+
+
 @pytest.mark.parametrize("act", [None, "gelu", "relu", "tanh"])
 def test_linear_autograd(act):
     dev = gpu_device()

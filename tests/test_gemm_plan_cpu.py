@@ -95,3 +95,19 @@ def test_online_tuning_commits_in_model_argmin(monkeypatch):
     assert not NG._online_active and key not in NG._online
     assert NG._tuned.pop(key) == ("big192", 1)          # medians 5.0 / 6.0 / 4.1
     assert NG._timings.pop(key)[("small", 2)] == 6.0
+
+
+def test_wg_candidate(monkeypatch):
+    """The 4-wave weight-gradient kernel is offered for plain TN GEMMs inside its contract
+    (M % 256, N % 128, K % 32) -- BERT-base's four weight gradients -- and nowhere else."""
+    monkeypatch.setattr(NG, "_WG", True)
+    for M, N in [(2304, 768), (768, 3072), (3072, 768), (768, 768)]:
+        c = NG._candidates(NG.MODE_TN, M, N, 16384, False, M, N, plain=True)
+        assert any(k == "wg" for k, _ in c), (M, N)
+        assert all(s >= 1 for k, s in c if k == "wg")
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_TN, 200, 256, 16384, False, 200, 256, plain=True))
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_TN, 256, 256, 16400, False, 256, 256, plain=True))
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_TN, 768, 768, 16384, False, 768, 768, plain=False))
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_NT, 768, 768, 16384, False, 768, 768, plain=True))
+    monkeypatch.setattr(NG, "_WG", False)
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_TN, 768, 768, 16384, False, 768, 768, plain=True))
