@@ -1469,7 +1469,7 @@ __global__ __launch_bounds__(256) void big_reduce_k(BigParams p, const float* __
 // k-tiles through a 4-stage ring (3 tiles in flight), in the swizzled k-outer image of the 8-wave
 // kernel (frag<KO>).  Output: fp32 split-K partials; big_reduce_k sums them and applies accumulate
 // and the output dtype (also for one split).
-// Needs M % 256 == 0, N % 128 == 0, K % 32 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-byte aligned operands.
+// Needs M % 256 == 0, N % 128 == 0, K % 128 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-byte aligned operands.
 constexpr int WG_NTH = 256, WG_BK = 32, WG_ST = 4, WG_TN = 128;
 constexpr int WG_HALF = WG_BK * 256;     // bytes: 32 k-rows x 128 columns x 2 B
 constexpr int WG_DMA = 6;                // DMA instructions per wave per k-tile (A: 2 halves x 2, B: 2)
@@ -1555,20 +1555,29 @@ __global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
     // consumed by its MFMAs) before slot (t+3) % 4 = (t-1) % 4 is restaged.  One loop body, no
     // unrolling, no register copies (two alternating fragment sets made the allocator rotate the
     // accumulators through VGPR copies).
-#pragma unroll 1
-    for (int t = 0; t < nt; ++t) {
+    // (unrolled by the 4 ring slots, nt % 4 == 0 by the host's split sizes: every LDS address is a
+    // loop-invariant lane offset plus an immediate -- with a run-time slot each fragment read cost
+    // a VALU add, and the loop's VALU overflowed the issue slots between MFMAs)
+    auto iter = [&](int t, int sl) {
 #ifndef DDL_DIAG_WG_NODMA   // diagnostic builds only (wrong results): no operand DMA after the prologue
         VMN(6);
 #endif
         BARRIER();
         mma4(0);
-        readA((t + 1) & 3, 0);
+        readA((sl + 1) & 3, 0);
 #ifndef DDL_DIAG_WG_NODMA
-        stage(min(kt0 + t + 3, ktl), (t + 3) & 3);
+        stage(min(kt0 + t + 3, ktl), (sl + 3) & 3);
 #endif
         mma4(4);
-        readA((t + 1) & 3, 4);
-        readB((t + 1) & 3);
+        readA((sl + 1) & 3, 4);
+        readB((sl + 1) & 3);
+    };
+#pragma unroll 1
+    for (int t = 0; t < nt; t += 4) {
+        iter(t, 0);
+        iter(t + 1, 1);
+        iter(t + 2, 2);
+        iter(t + 3, 3);
     }
     VM0();      // no LDS-DMA may outlive the workgroup's LDS
     // fp32 partial tile: lane holds C[m][n .. n+3] of each 16 x 16 block (the MFMA layout)
@@ -1832,7 +1841,7 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
 DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                            int out_f32, int splits, float* workspace, long ws_elems, int accumulate, hipStream_t st) {
     if (M <= 0 || N <= 0) return 0;
-    if (M % 256 || N % WG_TN || K <= 0 || K % WG_BK || lda % 8 || ldb % 8 || ldc % 4 || ldc < N ||
+    if (M % 256 || N % WG_TN || K <= 0 || K % (4 * WG_BK) || lda % 8 || ldb % 8 || ldc % 4 || ldc < N ||
         ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
         return -1;
     BigParams p{};
@@ -1841,10 +1850,10 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
     p.act = ACT_NONE; p.accumulate = accumulate; p.out_f32 = out_f32;
     p.tiles_m = M / 256;
     p.tiles_n = N / WG_TN;
-    const int nkt = K / WG_BK;
+    const int nkt = K / WG_BK;                    // a multiple of 4 (K % 128 == 0)
     if (splits < 1) splits = 1;
-    if (splits > nkt) splits = nkt;
-    p.kt_per_split = (nkt + splits - 1) / splits;
+    if (splits > nkt / 4) splits = nkt / 4;
+    p.kt_per_split = ((nkt + splits - 1) / splits + 3) & ~3;   // whole 4-tile rounds of the ring
     splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
     p.splits = splits;
     p.split_stride = (long)M * ldc;

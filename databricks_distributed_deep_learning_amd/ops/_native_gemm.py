@@ -233,7 +233,7 @@ _WG = os.environ.get("DDL_GEMM_WG", "1") != "0"   # tuner candidate "wg" (A/B: 0
 
 def wg_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
     """Shapes the 4-wave weight-gradient kernel takes (ddl_gemm_wgrad's contract: 256x128 tiles)."""
-    return M % 256 == 0 and N % 128 == 0 and K % 32 == 0 and K > 0 and lda % 8 == 0 and ldb % 8 == 0
+    return M % 256 == 0 and N % 128 == 0 and K % 128 == 0 and K > 0 and lda % 8 == 0 and ldb % 8 == 0
 
 
 def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):

@@ -49,7 +49,7 @@ while [ $# -gt 0 ]; do
       # same-box BERT-base A/B of fixed GEMM plans (tune cache pre-filled from scripts/plans/*.json) and
       # the retire-depth-0 library, alternating: ARM = plan[:lib]
       for i in 1 2; do
-        for arm in bert_cur bert_bigtn bert_bigtn:dr0 bert_bigtn_b256; do
+        for arm in ${PLAN_ARMS:-bert_cur bert_bigtn bert_bigtn:dr0 bert_bigtn_b256}; do
           pl=${arm%%:*}; lib=${arm#*:}
           if [ "$lib" = dr0 ]; then export DDL_NATIVE_LIB=$PWD/databricks_distributed_deep_learning_amd/_native/ab/libddl_dr0.so; else unset DDL_NATIVE_LIB; fi
           cp scripts/plans/$pl.json gpurun_out/plan_cache.json

@@ -51,7 +51,7 @@ def test_gemm_modes(M, N, K, kernel):
     assert _rel_err(dw32, dy.float().t() @ a.float()) < 1e-3
 
 
-@pytest.mark.parametrize("Mo,No,Kr", [(256, 128, 32), (512, 384, 1056), (768, 256, 4096), (2304, 768, 1024)])
+@pytest.mark.parametrize("Mo,No,Kr", [(256, 128, 128), (512, 384, 1152), (768, 256, 4096), (2304, 768, 1024)])
 @pytest.mark.parametrize("splits", [1, 2, 5])
 def test_wgrad_kernel(Mo, No, Kr, splits):
     """4-wave weight-gradient kernel ("wg", gemm_big.hip gemm_wg_k): dW = dY^T X over the reduction,
@@ -75,11 +75,11 @@ def test_wgrad_kernel(Mo, No, Kr, splits):
 
 
 def test_wgrad_kernel_contract():
-    """Shapes outside the 4-wave kernel's contract (M % 256, N % 128, K % 32) run another kernel."""
+    """Shapes outside the 4-wave kernel's contract (M % 256, N % 128, K % 128) run another kernel."""
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
     assert NG.wg_ok(768, 2304, 16384, 768, 2304) and not NG.wg_ok(200, 256, 64, 200, 256)
-    assert not NG.wg_ok(256, 256, 48, 256, 256)
+    assert not NG.wg_ok(256, 256, 48, 256, 256) and not NG.wg_ok(256, 256, 96, 256, 256)
     dy = torch.randn(96, 200, device=dev).to(torch.bfloat16)
     x = torch.randn(96, 256, device=dev).to(torch.bfloat16)
     dw = torch.empty(200, 256, device=dev, dtype=torch.bfloat16)

@@ -99,7 +99,7 @@ def test_online_tuning_commits_in_model_argmin(monkeypatch):
 
 def test_wg_candidate(monkeypatch):
     """The 4-wave weight-gradient kernel is offered for plain TN GEMMs inside its contract
-    (M % 256, N % 128, K % 32) -- BERT-base's four weight gradients -- and nowhere else."""
+    (M % 256, N % 128, K % 128) -- BERT-base's four weight gradients -- and nowhere else."""
     monkeypatch.setattr(NG, "_WG", True)
     for M, N in [(2304, 768), (768, 3072), (3072, 768), (768, 768)]:
         c = NG._candidates(NG.MODE_TN, M, N, 16384, False, M, N, plain=True)
