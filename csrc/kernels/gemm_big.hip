@@ -1480,6 +1480,10 @@ __device__ __forceinline__ int wg_off(int s, int x, int h) { return (s * 3 + x *
 // allocator gave each MFMA a destination other than its accumulator input and shuffled the
 // accumulators through v_accvgpr moves around every MFMA of this kernel -- 2.7x its MFMA time.
 // The 8-wave kernels' code is identical either way.)
+// CW: B is the implicit im2col of an NHWC input (conv weight gradient, CONVW): reduction rows are
+// output pixels, columns (tap, channel); a lane's 8 columns are one tap's 8 channels (C % 8 == 0),
+// fixed for the whole reduction, so only the pixel is decomposed per DMA (padding: the zero page)
+template <bool CW>
 __global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
     __shared__ __attribute__((aligned(16))) char smem[WG_ST * 3 * WG_HALF];   // 96 KB, one LDS object
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -1501,13 +1505,23 @@ __global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
     const int c = (l & 15) ^ swz_ko(krow0);
     const bf16_t* ga = p.A + (long)krow0 * p.lda + m0 + 8 * c;
     const bf16_t* gb = p.B + (long)krow0 * p.ldb + n0 + 8 * c;
+    int cdh = 0, cdw = 0, cci = 0;
+    if (CW) tap_of(p.cd, n0 + 8 * c, cdh, cdw, cci);
     auto stage = [&](int kt, int st) {
         const long ka = (long)kt * WG_BK;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             glds(ga + (ka + j * 4) * p.lda, smem + wg_off(st, 0, 0) + (w * 2 + j) * 1024);
             glds(ga + (ka + j * 4) * p.lda + 128, smem + wg_off(st, 0, 1) + (w * 2 + j) * 1024);
-            glds(gb + (ka + j * 4) * p.ldb, smem + wg_off(st, 1, 0) + (w * 2 + j) * 1024);
+            if (CW) {
+                const Pix x = decompose(p.cd, p.B, (int)ka + krow0 + j * 4, p.K);
+                const int hh = x.hb + cdh, ww = x.wb + cdw;
+                const bool ok = (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W;
+                glds(ok ? x.img + ((long)hh * p.cd.W + ww) * p.cd.C + cci : p.zero,
+                     smem + wg_off(st, 1, 0) + (w * 2 + j) * 1024);
+            } else {
+                glds(gb + (ka + j * 4) * p.ldb, smem + wg_off(st, 1, 0) + (w * 2 + j) * 1024);
+            }
         }
     };
     f32x4 acc[8][4];
@@ -1838,13 +1852,18 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
 // TN weight gradient on the 4-wave kernel (gemm_wg_k): C[M, N] (+)= A^T B, A = [K][M] (lda), B = [K][N]
 // (ldb); fp32 partials in `workspace` (splits x M x ldc floats, also for one split), then the reduce
 // applies accumulate / the output dtype.  Returns -1 when the shape is outside the kernel's contract.
+// conv (nullable): the CONVW descriptor (as ddl_gemm_big2) -- B is then the NHWC input and C the
+// weight gradient [Cout][R * S * Cin] (channel count % 8 == 0); zero: >= 16 zero bytes (padding taps)
 DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                           int out_f32, int splits, float* workspace, long ws_elems, int accumulate, hipStream_t st) {
+                           int out_f32, int splits, float* workspace, long ws_elems, int accumulate,
+                           const int* conv, const void* zero, hipStream_t st) {
     if (M <= 0 || N <= 0) return 0;
     if (M % 256 || N % WG_TN || K <= 0 || K % (4 * WG_BK) || lda % 8 || ldb % 8 || ldc % 4 || ldc < N ||
-        ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+        ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || (conv && (conv[3] % 8 || !zero)))
         return -1;
     BigParams p{};
+    if (conv) fill_conv(p.cd, conv);
+    p.zero = (const bf16_t*)zero;
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.act = ACT_NONE; p.accumulate = accumulate; p.out_f32 = out_f32;
@@ -1860,7 +1879,8 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
     if (!workspace || ws_elems < p.split_stride * splits) return -2;
     BigParams kp = p;
     kp.C = workspace;
-    hipLaunchKernelGGL(gemm_wg_k, dim3(p.tiles_m * p.tiles_n * splits), dim3(WG_NTH), 0, st, kp);
+    if (conv) hipLaunchKernelGGL(gemm_wg_k<true>, dim3(p.tiles_m * p.tiles_n * splits), dim3(WG_NTH), 0, st, kp);
+    else hipLaunchKernelGGL(gemm_wg_k<false>, dim3(p.tiles_m * p.tiles_n * splits), dim3(WG_NTH), 0, st, kp);
     const long total = (long)M * ((N + 3) / 4);
     const int g = (int)std::min<long>(16384, (total + 255) / 256);
     big_reduce_k<<<g, 256, 0, st>>>(p, workspace);

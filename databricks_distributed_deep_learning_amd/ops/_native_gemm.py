@@ -15,7 +15,7 @@ from ._lib import I, L, P
 _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_n64": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
-               "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P],
+               "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -161,12 +161,14 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
     out_f32 = 1 if C.dtype == torch.float32 else 0
     if kind == "wg":
-        if (mode == MODE_TN and bias is None and act is None and residual is None and colstats is None
+        cw = mode == MODE_CONVW and conv_arr is not None and conv_arr[3] % 8 == 0
+        if ((mode == MODE_TN or cw) and bias is None and act is None and residual is None and colstats is None
                 and not row_remap and wg_ok(M, N, K, lda, ldb) and ldc % 4 == 0
                 and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0):
             ws = torch.empty(max(1, s) * M * ldc, dtype=torch.float32, device=C.device)
             rc = _lib.fn("ddl_gemm_wgrad")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, out_f32,
-                                           s, ws.data_ptr(), ws.numel(), int(accumulate), _lib.stream())
+                                           s, ws.data_ptr(), ws.numel(), int(accumulate),
+                                           conv_arr if cw else None, _zero_page(C.device).data_ptr(), _lib.stream())
             if rc != 0:
                 raise RuntimeError(f"ddl_gemm_wgrad(M={M}, N={N}, K={K}, splits={s}) failed: {rc}")
             return
@@ -196,7 +198,8 @@ def _big_allowed(mode: int, K: int, lda: int = 8, ldb: int = 8) -> bool:
     return not _force_small and mode != MODE_CONVW and K % 8 == 0 and K >= 64 and lda % 8 == 0 and ldb % 8 == 0
 
 
-def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int, plain: bool = False):
+def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int, plain: bool = False,
+                conv_c: Optional[int] = None):
     """(kernel, splits) variants worth timing for one GEMM shape: each kernel at
     no split, its heuristic split and half of it (split-K trades parallelism
     against fp32 partial-slab traffic, which the heuristic cannot price)."""
@@ -209,7 +212,8 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
     if N <= 192 or N % 128 == 64:     # 128x64 tiles: no half-empty column tile
         ns = 1 if row_remap else pick_splits(M, 2 * N, K)   # 128x64 tiles = 128x128 tiles on 2N
         out += [("narrow", s) for s in sorted({1, max(1, ns // 2), ns})]
-    if _WG and mode == MODE_TN and plain and wg_ok(M, N, K, lda, ldb):
+    if _WG and plain and wg_ok(M, N, K, lda, ldb) and (
+            mode == MODE_TN or (mode == MODE_CONVW and conv_c is not None and conv_c % 8 == 0)):
         # 4-wave weight-gradient kernel (gemm_big.hip gemm_wg_k): 256x128 tiles, fp32 partials + reduce
         ws_ = big_splits(M, 2 * N, K)      # 256x128 tiles = 256x256 tiles on 2N
         out += [("wg", s) for s in sorted({max(1, ws_ // 2), ws_, 2 * ws_})]
@@ -373,10 +377,11 @@ def _time_runs(run, reps: int, cold: bool = False) -> float:
     return sum(a.elapsed_time(b) for a, b in evs) / reps
 
 
-def _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats):
-    """The (kernel, splits) candidates a call of this signature can run."""
+def _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats, conv_c=None):
+    """The (kernel, splits) candidates a call of this signature can run (``conv_c``: a convolution's
+    input channel count)."""
     plain = bias is None and act is None and residual is None and aux is None and not row_remap
-    cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain)
+    cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain, conv_c)
     if act not in (None, "relu", "gelu", "dgelu") or (act == "dgelu" and aux is None):
         cands = [c for c in cands if c[0] != "big192"]     # LDS-staged epilogue: 256-wide tiles only
     if colstats is not None:   # statistics epilogue: whole-K tiles only
@@ -390,7 +395,8 @@ def _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residua
 
 def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, row_remap, residual,
           colstats=None, bnb=None):
-    cands = _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats)
+    cands = _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats,
+                             None if conv_arr is None else int(conv_arr[3]))
     cs_s = torch.empty_like(colstats) if colstats is not None else None
     if len(cands) == 1:
         _timings[key] = {cands[0]: 0.0}
@@ -510,8 +516,9 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
         elif kernel == "narrow":
             choice = ("narrow", 1 if row_remap else pick_splits(M, 2 * N, K, splits))
-        elif kernel == "wg" and mode == MODE_TN and bias is None and act is None and residual is None \
-                and not row_remap and colstats is None and wg_ok(M, N, K, lda, ldb):
+        elif kernel == "wg" and (mode == MODE_TN or (mode == MODE_CONVW and conv is not None and conv[3] % 8 == 0)) \
+                and bias is None and act is None and residual is None and not row_remap and colstats is None \
+                and wg_ok(M, N, K, lda, ldb):
             choice = ("wg", splits or big_splits(M, N, K))
         elif kernel == "tnarrow" and mode in (MODE_TN, MODE_CONVW) and bias is None and act is None \
                 and residual is None and not row_remap and colstats is None:
@@ -530,7 +537,8 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
             global _online_last
             st = _online.get(key)
             if st is None:
-                cands = _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats)
+                cands = _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residual, colstats,
+                                         None if conv is None else int(conv[3]))
                 st = _online[key] = {"cands": cands, "n": 0, "pending": [], "samples": {}}
             choice = st["cands"][st["n"] % len(st["cands"])]
             st["n"] += 1

@@ -214,6 +214,28 @@ def test_conv_wgrad_transposed(N, H, W, C, K, R, stride, pad):
     assert _rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,K,R,stride,pad", [(2, 16, 16, 128, 256, 3, 1, 1), (2, 32, 32, 128, 256, 3, 2, 1),
+                                                    (2, 16, 16, 256, 512, 3, 2, 1)])
+def test_conv_wgrad_wg(N, H, W, C, K, R, stride, pad):
+    """Conv weight gradient on the 4-wave kernel with an implicit-im2col B operand ("wg", CONVW):
+    padding taps from the zero page, stride 2, vs the fp32 reference."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    from databricks_distributed_deep_learning_amd.ops.conv import conv2d_reference
+    torch.manual_seed(10)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(K, R, R, C, device=dev).to(torch.bfloat16)
+    P = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, P, P, K, device=dev).to(torch.bfloat16)
+    assert NG.wg_ok(K, R * R * C, N * P * P, K, 0)
+    wr = w.float().requires_grad_(True)
+    conv2d_reference(x.float(), wr, stride, pad).backward(dy.float())
+    with NG.force_kernel("wg"):
+        dw = NC._wgrad(dy, x, w.shape, stride, pad)
+    assert _rel_err(dw, wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("path", ["serial", "multi", "multi_narrow"])
 @pytest.mark.parametrize("N,H,W,C,K,R,pad", [(2, 15, 13, 64, 128, 3, 1), (4, 28, 28, 128, 128, 3, 1),
                                              (2, 9, 9, 64, 64, 5, 2)])

@@ -111,3 +111,14 @@ def test_wg_candidate(monkeypatch):
     assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_NT, 768, 768, 16384, False, 768, 768, plain=True))
     monkeypatch.setattr(NG, "_WG", False)
     assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_TN, 768, 768, 16384, False, 768, 768, plain=True))
+
+
+def test_wg_candidate_conv_wgrad(monkeypatch):
+    """Conv weight gradients (CONVW) get the 4-wave kernel when the input channel count keeps each
+    8-channel chunk inside one tap (C % 8 == 0) and the GEMM is inside its contract."""
+    monkeypatch.setattr(NG, "_WG", True)
+    c = NG._candidates(NG.MODE_CONVW, 256, 2304, 50176, False, 256, 0, plain=True, conv_c=256)
+    assert any(k == "wg" for k, _ in c)
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_CONVW, 256, 2304, 50176, False, 256, 0, plain=True))
+    assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_CONVW, 256, 1152, 50176, False, 256, 0, plain=True,
+                                                         conv_c=4))
