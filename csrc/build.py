@@ -52,10 +52,12 @@ def needs(src, obj, hdr_mtime):
     return os.path.getmtime(src) > m or hdr_mtime > m
 
 
-# per-source extra flags: gemm_big.hip's 4-wave weight-gradient kernel needs the VGPR form of the
-# MFMA instructions (its AGPR-form accumulators were shuffled around every MFMA; the other kernels'
-# code is identical with it -- profiles/gemm_spills_r04.md)
-EXTRA = {"gemm_big.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# per-source extra flags: the VGPR form of the MFMA instructions.  With AGPR-form accumulators the
+# allocator shuffled them through v_accvgpr moves around the MFMAs: gemm_big.hip's 4-wave weight-
+# gradient kernel (2.7x its MFMA time), conv3x3_wgrad_k (620 moves per 144 MFMAs, 414 registers ->
+# 260), the skinny GEMMs.  gemm_big.hip's 8-wave kernels compile identically either way.
+_VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+EXTRA = {"gemm_big.hip": _VGPR_FORM, "conv3x3.hip": _VGPR_FORM, "skinny_gemm.hip": _VGPR_FORM}
 
 
 def compile_one(src, debug=False):
