@@ -832,9 +832,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     constexpr int TBN = N192 ? 192 : TB;
     constexpr bool WGRAD = LA == KO && LB == KO;   // TN: weight gradients (split-K fp32 / accumulate)
     // B-fragment prefetch (DDL_PREFETCH_B1) where B is k-contiguous (NT, implicit-GEMM conv forward):
-    // 8192^3 NT -32 % cycles, 4096^3 -20 %; with transposed B reads (NN / TN) it measured slower
-    // (TN: the extra live range spilled its main loop)
-    constexpr bool PF_B1 = DDL_PREFETCH_B1 && LB == KC;
+    // 8192^3 NT -32 % cycles, 4096^3 -20 %; NN (transposed B reads): 4096^3 +9 % in isolation but
+    // +0.3 % on the BERT-base step (DDL_PREFETCH_B1_NN); never TN (the extra live range spilled its loop)
+#ifndef DDL_PREFETCH_B1_NN
+#define DDL_PREFETCH_B1_NN 1   // NN too: BERT-base same-box +0.3 % (9,024 vs 8,997 / 9,000, two pairs)
+#endif
+    constexpr bool PF_B1 = DDL_PREFETCH_B1 && (LB == KC || (DDL_PREFETCH_B1_NN && LA == KC && LB == KO));
     // (+16 bytes: the tile ticket.  One LDS object only: a second __shared__ variable
     // makes the compiler's LDS-DMA alias tracking wait vmcnt(0) before fragment reads)
     __shared__ __attribute__((aligned(16))) char smem[8 * HALF + 16];
