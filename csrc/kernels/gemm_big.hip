@@ -1473,11 +1473,8 @@ __global__ __launch_bounds__(256) void big_reduce_k(BigParams p, const float* __
 // kernel (frag<KO>).  Output: fp32 split-K partials; big_reduce_k sums them and applies accumulate
 // and the output dtype (also for one split).
 // Needs M % 256 == 0, N % 128 == 0, K % 128 == 0, lda / ldb % 8 == 0, ldc % 4 == 0, 16-byte aligned operands.
-constexpr int WG_NTH = 256, WG_BK = 32, WG_ST = 4, WG_TN = 128;
+constexpr int WG_BK = 32, WG_ST = 4;
 constexpr int WG_HALF = WG_BK * 256;     // bytes: 32 k-rows x 128 columns x 2 B
-constexpr int WG_DMA = 6;                // DMA instructions per wave per k-tile (A: 2 halves x 2, B: 2)
-// stage s: A half 0, A half 1, B
-__device__ __forceinline__ int wg_off(int s, int x, int h) { return (s * 3 + x * 2 + h) * WG_HALF; }
 
 // (This file is compiled with -mllvm -amdgpu-mfma-vgpr-form, csrc/build.py: with the AGPR form the
 // allocator gave each MFMA a destination other than its accumulator input and shuffled the
@@ -1486,11 +1483,19 @@ __device__ __forceinline__ int wg_off(int s, int x, int h) { return (s * 3 + x *
 // CW: B is the implicit im2col of an NHWC input (conv weight gradient, CONVW): reduction rows are
 // output pixels, columns (tap, channel); a lane's 8 columns are one tap's 8 channels (C % 8 == 0),
 // fixed for the whole reduction, so only the pixel is decomposed per DMA (padding: the zero page)
-template <bool CW>
-__global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[WG_ST * 3 * WG_HALF];   // 96 KB, one LDS object
+// NW: 4 waves (one per SIMD, 256 x 128 tiles, "wg") or 8 waves (two per SIMD, 256 x 256 tiles,
+// "wg2": the 256 x 256 kernel's operand bytes per output, the second wave on each SIMD filling the
+// first one's read / barrier gaps).  Every wave owns 128 x 64 (acc 128 registers).
+template <bool CW, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void gemm_wg_k(BigParams p) {
+    constexpr int WN = NW / 2, TNW = 64 * WN, BH = TNW / 128;   // waves along N, tile N, B halves
+    constexpr int JW = 8 / NW;                                   // DMA instructions per wave per half
+    constexpr int DMA = JW * (2 + BH);                           // ... per k-tile
+    __shared__ __attribute__((aligned(16))) char smem[WG_ST * (2 + BH) * WG_HALF];   // 96 / 128 KB, one LDS object
+    // stage s: A half 0, A half 1, B half 0 (, B half 1)
+    auto wg_off = [](int s, int x, int h) { return (s * (2 + BH) + (x ? 2 + h : h)) * WG_HALF; };
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int wm = w >> 1, wn = w & 1;
+    const int wm = w / WN, wn = w % WN;
     // 1-D grid of (split, tile) blocks; XCD x (blocks x, x + 8, ...) runs a contiguous run of the
     // split-major order, so its blocks share k-rows of the A / B panels in its L2 (gemm_big_k xsplit)
     const int nwg = p.tiles_m * p.tiles_n;
@@ -1498,32 +1503,39 @@ __global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
     const int q = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (int)(blockIdx.x >> 3);
     const int split = q / nwg, tile = q - split * nwg;
     const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
-    const int m0 = tm * 256, n0 = tn * WG_TN;
+    const int m0 = tm * 256, n0 = tn * TNW;
     const int nkt = p.K / WG_BK;
     const int kt0 = split * p.kt_per_split;
     const int nt = min(nkt, kt0 + p.kt_per_split) - kt0;      // >= 1 (host)
-    // DMA lanes: k-row krow0 (+4 for j = 1) of a 32-row half, 16-byte chunk c of its 128 columns,
-    // stored at the swizzled slot l & 15 (swz_ko ignores bit 2: the same c for both j)
-    const int krow0 = (w * 2) * 4 + (l >> 4);
+    // DMA lanes: k-row krow0 (+4 j) of a 32-row half, 16-byte chunk c of its 128 columns, stored at
+    // the swizzled slot l & 15 (for JW = 2, swz_ko ignores bit 2: the same c for both j)
+    const int krow0 = (w * JW) * 4 + (l >> 4);
     const int c = (l & 15) ^ swz_ko(krow0);
     const bf16_t* ga = p.A + (long)krow0 * p.lda + m0 + 8 * c;
     const bf16_t* gb = p.B + (long)krow0 * p.ldb + n0 + 8 * c;
-    int cdh = 0, cdw = 0, cci = 0;
-    if (CW) tap_of(p.cd, n0 + 8 * c, cdh, cdw, cci);
+    int cdh[BH], cdw[BH], cci[BH];
+#pragma unroll
+    for (int h = 0; h < BH; ++h) {
+        cdh[h] = cdw[h] = cci[h] = 0;
+        if (CW) tap_of(p.cd, n0 + h * 128 + 8 * c, cdh[h], cdw[h], cci[h]);
+    }
     auto stage = [&](int kt, int st) {
         const long ka = (long)kt * WG_BK;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            glds(ga + (ka + j * 4) * p.lda, smem + wg_off(st, 0, 0) + (w * 2 + j) * 1024);
-            glds(ga + (ka + j * 4) * p.lda + 128, smem + wg_off(st, 0, 1) + (w * 2 + j) * 1024);
-            if (CW) {
-                const Pix x = decompose(p.cd, p.B, (int)ka + krow0 + j * 4, p.K);
-                const int hh = x.hb + cdh, ww = x.wb + cdw;
-                const bool ok = (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W;
-                glds(ok ? x.img + ((long)hh * p.cd.W + ww) * p.cd.C + cci : p.zero,
-                     smem + wg_off(st, 1, 0) + (w * 2 + j) * 1024);
-            } else {
-                glds(gb + (ka + j * 4) * p.ldb, smem + wg_off(st, 1, 0) + (w * 2 + j) * 1024);
+        for (int j = 0; j < JW; ++j) {
+            glds(ga + (ka + j * 4) * p.lda, smem + wg_off(st, 0, 0) + (w * JW + j) * 1024);
+            glds(ga + (ka + j * 4) * p.lda + 128, smem + wg_off(st, 0, 1) + (w * JW + j) * 1024);
+#pragma unroll
+            for (int h = 0; h < BH; ++h) {
+                if (CW) {
+                    const Pix x = decompose(p.cd, p.B, (int)ka + krow0 + j * 4, p.K);
+                    const int hh = x.hb + cdh[h], ww = x.wb + cdw[h];
+                    const bool ok = (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W;
+                    glds(ok ? x.img + ((long)hh * p.cd.W + ww) * p.cd.C + cci[h] : p.zero,
+                         smem + wg_off(st, 1, h) + (w * JW + j) * 1024);
+                } else {
+                    glds(gb + (ka + j * 4) * p.ldb + h * 128, smem + wg_off(st, 1, h) + (w * JW + j) * 1024);
+                }
             }
         }
     };
@@ -1542,9 +1554,9 @@ __global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
         for (int i = i0; i < i0 + 4; ++i) fa[i] = frag<KO>(ha, i * 16, 0);
     };
     auto readB = [&](int st) {
-        const char* hb = smem + wg_off(st, 1, 0);
+        const char* hb = smem + wg_off(st, 1, wn >> 1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = frag<KO>(hb, wn * 64 + j * 16, 0);
+        for (int j = 0; j < 4; ++j) fb[j] = frag<KO>(hb, (wn & 1) * 64 + j * 16, 0);
     };
     auto mma4 = [&](int i0) {
 #pragma unroll
@@ -1558,26 +1570,26 @@ __global__ __launch_bounds__(WG_NTH, 1) void gemm_wg_k(BigParams p) {
     // the end: a stale slot, never used) -- accumulators crossing a branch were copied between
     // AGPRs and VGPRs (64 v_accvgpr_write + hazard nops per 16 MFMAs).
     const int ktl = kt0 + nt - 1;
-    // prologue: tiles 0..2 in flight (8 - 2 of them possibly re-stages of the last), tile 0 landed
+    // prologue: tiles 0..2 in flight (two of them possibly re-stages of the last), tile 0 landed
     stage(kt0, 0);
     stage(min(kt0 + 1, ktl), 1);
     stage(min(kt0 + 2, ktl), 2);
-    VMN(12);
+    if constexpr (DMA == 6) VMN(12);
+    else VMN(8);
     BARRIER();
     readB(0);
     readA(0, 0);
     readA(0, 4);
     // one k-tile per iteration: tile t+1 landed (tile t+2 may still be in flight) and made visible by
     // the barrier -- which also orders every wave's reads of tile t-1 (issued in the iteration before,
-    // consumed by its MFMAs) before slot (t+3) % 4 = (t-1) % 4 is restaged.  One loop body, no
-    // unrolling, no register copies (two alternating fragment sets made the allocator rotate the
-    // accumulators through VGPR copies).
-    // (unrolled by the 4 ring slots, nt % 4 == 0 by the host's split sizes: every LDS address is a
-    // loop-invariant lane offset plus an immediate -- with a run-time slot each fragment read cost
-    // a VALU add, and the loop's VALU overflowed the issue slots between MFMAs)
+    // consumed by its MFMAs) before slot (t+3) % 4 = (t-1) % 4 is restaged.  One loop body, unrolled
+    // by the 4 ring slots (nt % 4 == 0 by the host's split sizes): every LDS address is a loop-
+    // invariant lane offset plus an immediate -- with a run-time slot each fragment read cost a VALU
+    // add, and the loop's VALU overflowed the issue slots between MFMAs.
     auto iter = [&](int t, int sl) {
 #ifndef DDL_DIAG_WG_NODMA   // diagnostic builds only (wrong results): no operand DMA after the prologue
-        VMN(6);
+        if constexpr (DMA == 6) VMN(6);
+        else VMN(4);
 #endif
         BARRIER();
         mma4(0);
@@ -1857,11 +1869,13 @@ DDL_API int ddl_gemm_big2(int mode, const void* A, long lda, const void* B, long
 // applies accumulate / the output dtype.  Returns -1 when the shape is outside the kernel's contract.
 // conv (nullable): the CONVW descriptor (as ddl_gemm_big2) -- B is then the NHWC input and C the
 // weight gradient [Cout][R * S * Cin] (channel count % 8 == 0); zero: >= 16 zero bytes (padding taps)
+// wide: 8 waves on 256 x 256 tiles ("wg2", N % 256 == 0) instead of 4 on 256 x 128 ("wg")
 DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                            int out_f32, int splits, float* workspace, long ws_elems, int accumulate,
-                           const int* conv, const void* zero, hipStream_t st) {
+                           const int* conv, const void* zero, int wide, hipStream_t st) {
     if (M <= 0 || N <= 0) return 0;
-    if (M % 256 || N % WG_TN || K <= 0 || K % (4 * WG_BK) || lda % 8 || ldb % 8 || ldc % 4 || ldc < N ||
+    const int tnw = wide ? 256 : 128;
+    if (M % 256 || N % tnw || K <= 0 || K % (4 * WG_BK) || lda % 8 || ldb % 8 || ldc % 4 || ldc < N ||
         ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || (conv && (conv[3] % 8 || !zero)))
         return -1;
     BigParams p{};
@@ -1871,7 +1885,7 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
     p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.act = ACT_NONE; p.accumulate = accumulate; p.out_f32 = out_f32;
     p.tiles_m = M / 256;
-    p.tiles_n = N / WG_TN;
+    p.tiles_n = N / tnw;
     const int nkt = K / WG_BK;                    // a multiple of 4 (K % 128 == 0)
     if (splits < 1) splits = 1;
     if (splits > nkt / 4) splits = nkt / 4;
@@ -1882,8 +1896,14 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
     if (!workspace || ws_elems < p.split_stride * splits) return -2;
     BigParams kp = p;
     kp.C = workspace;
-    if (conv) hipLaunchKernelGGL(gemm_wg_k<true>, dim3(p.tiles_m * p.tiles_n * splits), dim3(WG_NTH), 0, st, kp);
-    else hipLaunchKernelGGL(gemm_wg_k<false>, dim3(p.tiles_m * p.tiles_n * splits), dim3(WG_NTH), 0, st, kp);
+    const dim3 grid(p.tiles_m * p.tiles_n * splits);
+    if (wide) {
+        if (conv) hipLaunchKernelGGL((gemm_wg_k<true, 8>), grid, dim3(512), 0, st, kp);
+        else hipLaunchKernelGGL((gemm_wg_k<false, 8>), grid, dim3(512), 0, st, kp);
+    } else {
+        if (conv) hipLaunchKernelGGL((gemm_wg_k<true, 4>), grid, dim3(256), 0, st, kp);
+        else hipLaunchKernelGGL((gemm_wg_k<false, 4>), grid, dim3(256), 0, st, kp);
+    }
     const long total = (long)M * ((N + 3) / 4);
     const int g = (int)std::min<long>(16384, (total + 255) / 256);
     big_reduce_k<<<g, 256, 0, st>>>(p, workspace);

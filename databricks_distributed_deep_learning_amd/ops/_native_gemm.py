@@ -15,7 +15,7 @@ from ._lib import I, L, P
 _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_n64": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
-               "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, P],
+               "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, I, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -37,7 +37,7 @@ def set_big_gemm(enabled: bool) -> None:
 
 
 _forced: Optional[str] = None
-_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg")
+_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg", "wg2")
 # per-call device timing for diagnostics (scripts/debug/gemm_trace.py): list of
 # (signature, (kernel, splits), start event, end event) while enabled
 _trace: Optional[list] = None
@@ -160,15 +160,17 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
         A, lda, B, ldb, M, N = B, ldb, A, lda, N, M
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
     out_f32 = 1 if C.dtype == torch.float32 else 0
-    if kind == "wg":
+    if kind in ("wg", "wg2"):
         cw = mode == MODE_CONVW and conv_arr is not None and conv_arr[3] % 8 == 0
+        wide = kind == "wg2"
         if ((mode == MODE_TN or cw) and bias is None and act is None and residual is None and colstats is None
-                and not row_remap and wg_ok(M, N, K, lda, ldb) and ldc % 4 == 0
+                and not row_remap and wg_ok(M, N, K, lda, ldb, wide) and ldc % 4 == 0
                 and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0):
             ws = torch.empty(max(1, s) * M * ldc, dtype=torch.float32, device=C.device)
             rc = _lib.fn("ddl_gemm_wgrad")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, out_f32,
                                            s, ws.data_ptr(), ws.numel(), int(accumulate),
-                                           conv_arr if cw else None, _zero_page(C.device).data_ptr(), _lib.stream())
+                                           conv_arr if cw else None, _zero_page(C.device).data_ptr(), int(wide),
+                                           _lib.stream())
             if rc != 0:
                 raise RuntimeError(f"ddl_gemm_wgrad(M={M}, N={N}, K={K}, splits={s}) failed: {rc}")
             return
@@ -214,9 +216,13 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
         out += [("narrow", s) for s in sorted({1, max(1, ns // 2), ns})]
     if _WG and plain and wg_ok(M, N, K, lda, ldb) and (
             mode == MODE_TN or (mode == MODE_CONVW and conv_c is not None and conv_c % 8 == 0)):
-        # 4-wave weight-gradient kernel (gemm_big.hip gemm_wg_k): 256x128 tiles, fp32 partials + reduce
+        # weight-gradient kernel (gemm_big.hip gemm_wg_k): 4 waves on 256x128 tiles ("wg") and 8 waves on
+        # 256x256 tiles ("wg2"); fp32 partials + reduce
         ws_ = big_splits(M, 2 * N, K)      # 256x128 tiles = 256x256 tiles on 2N
         out += [("wg", s) for s in sorted({max(1, ws_ // 2), ws_, 2 * ws_})]
+        if _WG2 and N % 256 == 0:
+            w2 = big_splits(M, N, K)
+            out += [("wg2", s) for s in sorted({max(1, w2 // 2), w2, 2 * w2})]
     if mode in (MODE_TN, MODE_CONVW) and plain and (M <= 192 or M % 128 == 64):
         ts = pick_splits(N, 2 * M, K)     # transposed: N' = M (output channels) on 64-wide tiles
         out += [("tnarrow", s) for s in sorted({1, max(1, ts // 2), ts})]
@@ -233,11 +239,17 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
 
 
 _WG = os.environ.get("DDL_GEMM_WG", "1") != "0"   # tuner candidate "wg" (A/B: 0 = never)
+# "wg2" (8 waves, 256x256 tiles) is opt-in: at two waves per SIMD its 128x64 wave tiles plus fragments
+# exceed the 256-register budget and spill in the loop -- slower than both "wg" and the 256x256 kernel
+# on every BERT-base weight gradient (profiles/tn_kinds_r04_wg2.log)
+_WG2 = os.environ.get("DDL_GEMM_WG2", "0") == "1"
 
 
-def wg_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
-    """Shapes the 4-wave weight-gradient kernel takes (ddl_gemm_wgrad's contract: 256x128 tiles)."""
-    return M % 256 == 0 and N % 128 == 0 and K % 128 == 0 and K > 0 and lda % 8 == 0 and ldb % 8 == 0
+def wg_ok(M: int, N: int, K: int, lda: int, ldb: int, wide: bool = False) -> bool:
+    """Shapes the weight-gradient kernel takes (ddl_gemm_wgrad's contract: 256x128 tiles, or 256x256
+    for the 8-wave ``wide`` variant "wg2")."""
+    return M % 256 == 0 and N % (256 if wide else 128) == 0 and K % 128 == 0 and K > 0 and lda % 8 == 0 \
+        and ldb % 8 == 0
 
 
 def _heuristic(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ldb: int):
@@ -516,10 +528,11 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
             choice = ("big", 1 if row_remap else (splits or big_splits(M, N, K)))
         elif kernel == "narrow":
             choice = ("narrow", 1 if row_remap else pick_splits(M, 2 * N, K, splits))
-        elif kernel == "wg" and (mode == MODE_TN or (mode == MODE_CONVW and conv is not None and conv[3] % 8 == 0)) \
+        elif kernel in ("wg", "wg2") \
+                and (mode == MODE_TN or (mode == MODE_CONVW and conv is not None and conv[3] % 8 == 0)) \
                 and bias is None and act is None and residual is None and not row_remap and colstats is None \
-                and wg_ok(M, N, K, lda, ldb):
-            choice = ("wg", splits or big_splits(M, N, K))
+                and wg_ok(M, N, K, lda, ldb, kernel == "wg2"):
+            choice = (kernel, splits or big_splits(M, N, K))
         elif kernel == "tnarrow" and mode in (MODE_TN, MODE_CONVW) and bias is None and act is None \
                 and residual is None and not row_remap and colstats is None:
             choice = ("tnarrow", pick_splits(N, 2 * M, K, splits))

@@ -51,9 +51,11 @@ def test_gemm_modes(M, N, K, kernel):
     assert _rel_err(dw32, dy.float().t() @ a.float()) < 1e-3
 
 
-@pytest.mark.parametrize("Mo,No,Kr", [(256, 128, 128), (512, 384, 1152), (768, 256, 4096), (2304, 768, 1024)])
+@pytest.mark.parametrize("kind", ["wg", "wg2"])
+@pytest.mark.parametrize("Mo,No,Kr", [(256, 256, 128), (512, 512, 1152), (768, 256, 4096), (2304, 768, 1024),
+                                      (512, 384, 512)])
 @pytest.mark.parametrize("splits", [1, 2, 5])
-def test_wgrad_kernel(Mo, No, Kr, splits):
+def test_wgrad_kernel(Mo, No, Kr, splits, kind):
     """4-wave weight-gradient kernel ("wg", gemm_big.hip gemm_wg_k): dW = dY^T X over the reduction,
     fp32 partials + reduce; bf16 / fp32 outputs, plain and accumulating, vs an fp32 reference."""
     dev = gpu_device()
@@ -63,14 +65,14 @@ def test_wgrad_kernel(Mo, No, Kr, splits):
     x = torch.randn(Kr, No, device=dev).to(torch.bfloat16)
     ref = dy.float().t() @ x.float()
     dw = torch.empty(Mo, No, device=dev, dtype=torch.bfloat16)
-    gemm(MODE_TN, dy, Mo, x, No, dw, No, Mo, No, Kr, kernel="wg", splits=splits)
+    gemm(MODE_TN, dy, Mo, x, No, dw, No, Mo, No, Kr, kernel=kind, splits=splits)
     assert _rel_err(dw, ref) < 1e-2
     prev = torch.randn(Mo, No, device=dev)
     acc32 = prev.clone()
-    gemm(MODE_TN, dy, Mo, x, No, acc32, No, Mo, No, Kr, kernel="wg", splits=splits, accumulate=True)
+    gemm(MODE_TN, dy, Mo, x, No, acc32, No, Mo, No, Kr, kernel=kind, splits=splits, accumulate=True)
     assert _rel_err(acc32, prev + ref) < 1e-3
     acc16 = prev.to(torch.bfloat16)
-    gemm(MODE_TN, dy, Mo, x, No, acc16, No, Mo, No, Kr, kernel="wg", splits=splits, accumulate=True)
+    gemm(MODE_TN, dy, Mo, x, No, acc16, No, Mo, No, Kr, kernel=kind, splits=splits, accumulate=True)
     assert _rel_err(acc16, prev + ref) < 1e-2
 
 
@@ -216,7 +218,8 @@ def test_conv_wgrad_transposed(N, H, W, C, K, R, stride, pad):
 
 @pytest.mark.parametrize("N,H,W,C,K,R,stride,pad", [(2, 16, 16, 128, 256, 3, 1, 1), (2, 32, 32, 128, 256, 3, 2, 1),
                                                     (2, 16, 16, 256, 512, 3, 2, 1)])
-def test_conv_wgrad_wg(N, H, W, C, K, R, stride, pad):
+@pytest.mark.parametrize("kind", ["wg", "wg2"])
+def test_conv_wgrad_wg(N, H, W, C, K, R, stride, pad, kind):
     """Conv weight gradient on the 4-wave kernel with an implicit-im2col B operand ("wg", CONVW):
     padding taps from the zero page, stride 2, vs the fp32 reference."""
     dev = gpu_device()
@@ -231,7 +234,7 @@ def test_conv_wgrad_wg(N, H, W, C, K, R, stride, pad):
     assert NG.wg_ok(K, R * R * C, N * P * P, K, 0)
     wr = w.float().requires_grad_(True)
     conv2d_reference(x.float(), wr, stride, pad).backward(dy.float())
-    with NG.force_kernel("wg"):
+    with NG.force_kernel(kind):
         dw = NC._wgrad(dy, x, w.shape, stride, pad)
     assert _rel_err(dw, wr.grad) < 1e-2
 
