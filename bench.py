@@ -108,7 +108,7 @@ def run_one(model: str, args, world: int):
                          pad_fraction=args.bert_pad_fraction)
     cfg = cfg.replace(steps=args.steps, warmup_steps=args.warmup, native=args.native, log_every=0,
                       bucket_mb=args.bucket_mb, backend=args.backend,
-                      zero_optimizer=args.zero, sync_bn=args.sync_bn,
+                      zero_optimizer=args.zero, sync_bn=args.sync_bn, dp_rehearsal=args.dp_rehearsal,
                       eager_optimizer=os.environ.get("DDL_EAGER_OPTIMIZER", "0") == "1",
                       phase_timing=os.environ.get("DDL_PHASE_TIMING", "1") != "0")
     from databricks_distributed_deep_learning_amd.ops import _native_gemm
@@ -153,8 +153,12 @@ def main() -> int:
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off", "stock"],
                     help="auto/on: HIP kernels; stock: plain PyTorch-ROCm + torch DDP arm; "
                          "off: the framework's CPU-oracle ops (correctness reference, not a baseline)")
-    ap.add_argument("--bucket-mb", default="25",
-                    help="gradient bucket MB, or 'auto' (sized from the startup all-reduce probe at N > 1)")
+    ap.add_argument("--bucket-mb", default="auto",
+                    help="gradient bucket MB, or 'auto' (default: sized from the startup all-reduce probe at "
+                         "N > 1; 4 / 25 MB without a probe -- bucket_policy.source in the output says which)")
+    ap.add_argument("--dp-rehearsal", action="store_true",
+                    help="N = 1: run the N > 1 step form anyway (native RCCL engine, per-bucket all-reduces, "
+                         "per-bucket range optimizer) so its cost shows in phases_ms")
     ap.add_argument("--zero", action="store_true", help="ZeRO-1: shard fp32 master + optimizer state over ranks")
     ap.add_argument("--sync-bn", action="store_true", help="SyncBatchNorm (CV models)")
     ap.add_argument("--backend", default=os.environ.get("DDL_BACKEND", "auto"),
@@ -219,6 +223,9 @@ def main() -> int:
         line["comm_probe"] = head["comm_probe"]          # startup all-reduce probe (N > 1, native engine)
     if head.get("comm_buckets"):
         line["comm_buckets"] = head["comm_buckets"]      # last step: per-bucket ring time / bus GB/s
+    for k in ("rccl", "rank_devices", "dp_rehearsal"):    # RCCL's nranks / device; every rank's device
+        if head.get(k):
+            line[k] = head[k]
     if "bert_base" in results and is_r50:
         b = results["bert_base"]
         line["extra"] = {

@@ -24,6 +24,15 @@
 // fails or a collective exceeds its timeout; every later call then fails with the reason.
 // ddl_comm_collective_ms() reads a finished collective's device time (per-bucket timing).
 //
+// Locking: the watchdog's three calls never take the lock an API call holds while it is inside
+// RCCL.  `api` serialises the API callers among themselves (collective enqueue order); `book`
+// guards the launch bookkeeping (counters, event slots, launch times) and is held only around
+// event records and counter updates, never across an RCCL call; the communicator pointer and
+// the abort flag are atomics, so ddl_comm_abort() swaps the communicator out and calls
+// ncclCommAbort() even while another thread is blocked inside an enqueue (RCCL sets up peer
+// connections on a communicator's first collective: with a dead peer that enqueue can block).
+// A blocked enqueue counts as pending for ddl_comm_oldest_pending_ms() from the moment it began.
+//
 // The reference has no communication layer at all; BASELINE.json
 // mandates "data-parallel all-reduce ... RCCL ring/tree over xGMI ... overlapped
 // with backward on HIP streams".
@@ -31,7 +40,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -117,7 +128,7 @@ constexpr int RING = 64;
 using Clock = std::chrono::steady_clock;
 
 struct Engine {
-    ncclComm_t comm = nullptr;
+    std::atomic<ncclComm_t> comm{nullptr};
     hipStream_t stream = nullptr;    // collectives run here, concurrent with compute
     hipEvent_t produced = nullptr;   // compute -> comm ordering
     hipEvent_t drained = nullptr;    // comm -> compute ordering
@@ -125,28 +136,62 @@ struct Engine {
     hipEvent_t done[RING] = {};
     Clock::time_point t_launch[RING];
     int rank = 0, world = 1, device = 0;
-    long launched = 0;
-    long finished = 0;               // every collective numbered <= finished is known complete
-    long bytes = 0;
-    int injected = 0;                // test hook: reported as the async error
-    bool aborted = false;
-    std::mutex mu;                   // API calls vs the watchdog thread's abort
+    long launched = 0;               // (book)
+    long finished = 0;               // (book) every collective numbered <= finished is known complete
+    long bytes = 0;                  // (book)
+    // an enqueue in progress (host time it began; in_enqueue false otherwise) (book)
+    bool in_enqueue = false;
+    Clock::time_point t_enqueue;
+    std::atomic<int> injected{0};    // test hook: reported as the async error
+    std::atomic<int> stall_ms{0};    // test hook: the next enqueue blocks this long (a dead peer)
+    std::atomic<bool> aborted{false};
+    std::mutex api;                  // API callers among themselves; never taken by the watchdog
+    std::mutex book;                 // bookkeeping only; never held across an RCCL call
 };
 
 // collective number e->launched + 1 is about to go onto the comm stream
 bool mark_start(Engine* e) {
+    std::lock_guard<std::mutex> lk(e->book);
     const long i = e->launched % RING;
     e->t_launch[i] = Clock::now();
     return hok(hipEventRecord(e->start[i], e->stream), "hipEventRecord");
 }
 
-// all-reduce number e->launched just went onto the comm stream: mark its completion
-bool mark_done(Engine* e) {
+// a collective just went onto the comm stream: count it, mark its completion
+bool mark_done(Engine* e, long nbytes) {
+    std::lock_guard<std::mutex> lk(e->book);
+    e->launched += 1;
+    e->bytes += nbytes;
     return hok(hipEventRecord(e->done[(e->launched - 1) % RING], e->stream), "hipEventRecord");
 }
 
+// The communicator for an enqueue (null once aborted).  The enqueue counts as pending from
+// here until end_enqueue(), so a call that blocks inside RCCL is seen by the watchdog.
+ncclComm_t begin_enqueue(Engine* e) {
+    {
+        std::lock_guard<std::mutex> lk(e->book);
+        e->in_enqueue = true;
+        e->t_enqueue = Clock::now();
+    }
+    const int stall = e->stall_ms.exchange(0);
+    if (stall > 0) std::this_thread::sleep_for(std::chrono::milliseconds(stall));
+    ncclComm_t c = e->comm.load();
+    if (!c || e->aborted.load()) {
+        set_err("comm", "communicator aborted");
+        std::lock_guard<std::mutex> lk(e->book);
+        e->in_enqueue = false;
+        return nullptr;
+    }
+    return c;
+}
+
+void end_enqueue(Engine* e) {
+    std::lock_guard<std::mutex> lk(e->book);
+    e->in_enqueue = false;
+}
+
 bool usable(Engine* e) {
-    if (e->aborted || !e->comm) {
+    if (e->aborted.load() || !e->comm.load()) {
         set_err("comm", "communicator aborted");
         return false;
     }
@@ -159,6 +204,8 @@ bool order_after(Engine* e, hipStream_t compute) {
     return hok(hipEventRecord(e->produced, compute), "hipEventRecord") &&
            hok(hipStreamWaitEvent(e->stream, e->produced, 0), "hipStreamWaitEvent");
 }
+
+long esize(int dtype) { return dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2; }
 
 }  // namespace
 
@@ -195,26 +242,29 @@ DDL_API void* ddl_comm_create(const char* rccl_path, const char* id_bytes, int w
         }
     ncclUniqueId id;
     std::memcpy(id.internal, id_bytes, NCCL_UNIQUE_ID_BYTES);
-    if (!ok(g_rccl.commInitRank(&e->comm, world, id, rank), "ncclCommInitRank")) {
+    ncclComm_t c = nullptr;
+    if (!ok(g_rccl.commInitRank(&c, world, id, rank), "ncclCommInitRank")) {
         hipStreamDestroy(e->stream);
         delete e;
         return nullptr;
     }
+    e->comm.store(c);
     return e;
 }
 
 DDL_API int ddl_comm_allreduce(void* h, void* buf, long count, int dtype, int avg, hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
     if (!e || count <= 0) return count == 0 ? 0 : -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    if (!ok(g_rccl.allReduce(buf, buf, (size_t)count, dtype_of(dtype), avg ? ncclAvg : ncclSum, e->comm, e->stream),
-            "ncclAllReduce"))
-        return -2;
-    e->launched += 1;
-    e->bytes += count * (dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2);
-    return mark_done(e) ? 0 : -3;
+    ncclComm_t c = begin_enqueue(e);
+    if (!c) return -4;
+    const bool good = ok(g_rccl.allReduce(buf, buf, (size_t)count, dtype_of(dtype), avg ? ncclAvg : ncclSum, c,
+                                          e->stream), "ncclAllReduce");
+    end_enqueue(e);
+    if (!good) return -2;
+    return mark_done(e, count * esize(dtype)) ? 0 : -3;
 }
 
 // several buckets that became ready together: one fused RCCL group launch
@@ -222,44 +272,59 @@ DDL_API int ddl_comm_allreduce_many(void* h, void** bufs, const long* counts, in
                                     hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute)) return -3;
-    const long before = e->launched;
-    // one start mark per member, all at the group's stream position
-    for (int i = 0, k = 0; i < n; ++i) {
-        if (counts[i] <= 0) continue;
-        const long slot = (before + k++) % RING;
-        e->t_launch[slot] = Clock::now();
-        if (!hok(hipEventRecord(e->start[slot], e->stream), "hipEventRecord")) return -3;
-    }
-    if (!ok(g_rccl.groupStart(), "ncclGroupStart")) return -2;
-    for (int i = 0; i < n; ++i) {
-        if (counts[i] <= 0) continue;
-        if (!ok(g_rccl.allReduce(bufs[i], bufs[i], (size_t)counts[i], dtype_of(dtype), avg ? ncclAvg : ncclSum,
-                                 e->comm, e->stream),
-                "ncclAllReduce")) {
-            g_rccl.groupEnd();
-            return -2;
+    long before;
+    int members = 0;
+    long nbytes = 0;
+    {
+        // one start mark per member, all at the group's stream position
+        std::lock_guard<std::mutex> bk(e->book);
+        before = e->launched;
+        for (int i = 0; i < n; ++i) {
+            if (counts[i] <= 0) continue;
+            const long slot = (before + members++) % RING;
+            e->t_launch[slot] = Clock::now();
+            nbytes += counts[i] * esize(dtype);
+            if (!hok(hipEventRecord(e->start[slot], e->stream), "hipEventRecord")) return -3;
         }
-        e->launched += 1;
     }
-    if (!ok(g_rccl.groupEnd(), "ncclGroupEnd")) return -2;
+    if (!members) return 0;
+    ncclComm_t c = begin_enqueue(e);
+    if (!c) return -4;
+    bool good = ok(g_rccl.groupStart(), "ncclGroupStart");
+    for (int i = 0; good && i < n; ++i) {
+        if (counts[i] <= 0) continue;
+        good = ok(g_rccl.allReduce(bufs[i], bufs[i], (size_t)counts[i], dtype_of(dtype), avg ? ncclAvg : ncclSum, c,
+                                   e->stream), "ncclAllReduce");
+    }
+    good = ok(g_rccl.groupEnd(), "ncclGroupEnd") && good;
+    end_enqueue(e);
+    if (!good) return -2;
     // every number of the group completes at the same point of the comm stream
+    std::lock_guard<std::mutex> bk(e->book);
+    e->launched = before + members;
+    e->bytes += nbytes;
     for (long k = before; k < e->launched; ++k)
         if (!hok(hipEventRecord(e->done[k % RING], e->stream), "hipEventRecord")) return -3;
     return 0;
 }
 
+// (numbered and timed like the reductions, so a hung broadcast is covered by the watchdog too)
 DDL_API int ddl_comm_broadcast(void* h, void* buf, long count, int dtype, int root, hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
-    if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e || count <= 0) return count == 0 ? 0 : -1;
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
-    if (!order_after(e, compute)) return -3;
-    if (!ok(g_rccl.broadcast(buf, buf, (size_t)count, dtype_of(dtype), root, e->comm, e->stream), "ncclBroadcast"))
-        return -2;
-    return 0;
+    if (!order_after(e, compute) || !mark_start(e)) return -3;
+    ncclComm_t c = begin_enqueue(e);
+    if (!c) return -4;
+    const bool good = ok(g_rccl.broadcast(buf, buf, (size_t)count, dtype_of(dtype), root, c, e->stream),
+                         "ncclBroadcast");
+    end_enqueue(e);
+    if (!good) return -2;
+    return mark_done(e, count * esize(dtype)) ? 0 : -3;
 }
 
 // reduce-scatter / all-gather (ZeRO-1 buckets) are numbered with the all-reduces, so
@@ -269,37 +334,39 @@ DDL_API int ddl_comm_reduce_scatter(void* h, const void* send, void* recv, long 
                                     hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
     if (!e || recv_count <= 0) return recv_count == 0 ? 0 : -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    if (!ok(g_rccl.reduceScatter(send, recv, (size_t)recv_count, dtype_of(dtype), avg ? ncclAvg : ncclSum, e->comm,
-                                 e->stream),
-            "ncclReduceScatter"))
-        return -2;
-    e->launched += 1;
-    e->bytes += recv_count * e->world * (dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2);
-    return mark_done(e) ? 0 : -3;
+    ncclComm_t c = begin_enqueue(e);
+    if (!c) return -4;
+    const bool good = ok(g_rccl.reduceScatter(send, recv, (size_t)recv_count, dtype_of(dtype),
+                                              avg ? ncclAvg : ncclSum, c, e->stream), "ncclReduceScatter");
+    end_enqueue(e);
+    if (!good) return -2;
+    return mark_done(e, recv_count * e->world * esize(dtype)) ? 0 : -3;
 }
 
 DDL_API int ddl_comm_all_gather(void* h, const void* send, void* recv, long send_count, int dtype,
                                 hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
     if (!e || send_count <= 0) return send_count == 0 ? 0 : -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    if (!ok(g_rccl.allGather(send, recv, (size_t)send_count, dtype_of(dtype), e->comm, e->stream), "ncclAllGather"))
-        return -2;
-    e->launched += 1;
-    e->bytes += send_count * e->world * (dtype == 1 || dtype >= 4 ? 4 : dtype == 3 ? 8 : 2);
-    return mark_done(e) ? 0 : -3;
+    ncclComm_t c = begin_enqueue(e);
+    if (!c) return -4;
+    const bool good = ok(g_rccl.allGather(send, recv, (size_t)send_count, dtype_of(dtype), c, e->stream),
+                         "ncclAllGather");
+    end_enqueue(e);
+    if (!good) return -2;
+    return mark_done(e, send_count * e->world * esize(dtype)) ? 0 : -3;
 }
 
 // compute stream waits for every collective issued so far
 DDL_API int ddl_comm_wait(void* h, hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     return hok(hipEventRecord(e->drained, e->stream), "hipEventRecord") &&
                    hok(hipStreamWaitEvent(compute, e->drained, 0), "hipStreamWaitEvent")
@@ -307,14 +374,16 @@ DDL_API int ddl_comm_wait(void* h, hipStream_t compute) {
                : -3;
 }
 
-// compute stream waits for collective number `seq` (all-reduce / reduce-scatter / all-gather; 1-based, as counted by ddl_comm_stats(h, 0))
-// and, the comm stream being in order, everything issued before it.  A number more than
-// RING behind the newest waits for a later one instead (still correct, just later).
+// compute stream waits for collective number `seq` (all-reduce / reduce-scatter / all-gather /
+// broadcast; 1-based, as counted by ddl_comm_stats(h, 0)) and, the comm stream being in order,
+// everything issued before it.  A number more than RING behind the newest waits for a later one
+// instead (still correct, just later).
 DDL_API int ddl_comm_wait_upto(void* h, long seq, hipStream_t compute) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
+    std::lock_guard<std::mutex> bk(e->book);
     if (seq < 1 || seq > e->launched) return -1;
     if (e->launched - seq >= RING) seq = e->launched;
     return hok(hipStreamWaitEvent(compute, e->done[(seq - 1) % RING], 0), "hipStreamWaitEvent") ? 0 : -3;
@@ -323,45 +392,47 @@ DDL_API int ddl_comm_wait_upto(void* h, long seq, hipStream_t compute) {
 DDL_API int ddl_comm_synchronize(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    {
-        std::lock_guard<std::mutex> lk(e->mu);
-        if (!usable(e)) return -4;
-    }
-    // (not under the lock: the watchdog must be able to abort a synchronize stuck on a dead peer)
+    if (!usable(e)) return -4;
+    // (no lock: the watchdog must be able to abort a synchronize stuck on a dead peer)
     return hok(hipStreamSynchronize(e->stream), "hipStreamSynchronize") ? 0 : -3;
 }
 
 // RCCL's asynchronous error state of the communicator: 0 = fine (ncclInProgress counts as
-// fine), otherwise the ncclResult_t code; -4 after an abort.  Thread-safe (the watchdog).
+// fine), otherwise the ncclResult_t code; -4 after an abort.  Lock-free (the watchdog).
 DDL_API int ddl_comm_async_error(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (e->aborted || !e->comm) return -4;
-    if (e->injected) return e->injected;
+    ncclComm_t c = e->comm.load();
+    if (e->aborted.load() || !c) return -4;
+    if (const int inj = e->injected.load()) return inj;
     if (!g_rccl.getAsyncError) return 0;
     ncclResult_t r = ncclSuccess;
-    if (g_rccl.getAsyncError(e->comm, &r) != ncclSuccess) return (int)ncclInternalError;
+    if (g_rccl.getAsyncError(c, &r) != ncclSuccess) return (int)ncclInternalError;
     return (r == ncclSuccess || r == ncclInProgress) ? 0 : (int)r;
 }
 
-// Milliseconds the oldest collective that has not finished has been on the comm stream
-// (host clock since its launch call), -1 if every collective finished.  Only the RING newest
-// are tracked: older ones count as finished (their events were recycled).
+// Milliseconds the oldest collective that has not finished has been pending (host clock since
+// its launch call; an enqueue still inside RCCL counts from when it began), -1 if every
+// collective finished.  Only the RING newest are tracked: older ones count as finished (their
+// events were recycled).  Takes the bookkeeping lock only (never held across an RCCL call).
 DDL_API double ddl_comm_oldest_pending_ms(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1.0;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> bk(e->book);
+    const auto now = Clock::now();
+    double age = e->in_enqueue ? std::chrono::duration<double, std::milli>(now - e->t_enqueue).count() : -1.0;
     if (e->finished < e->launched - RING) e->finished = e->launched - RING;
     while (e->finished < e->launched) {
         const long slot = e->finished % RING;      // collective number finished + 1
         const hipError_t q = hipEventQuery(e->done[slot]);
-        if (q == hipErrorNotReady)
-            return std::chrono::duration<double, std::milli>(Clock::now() - e->t_launch[slot]).count();
+        if (q == hipErrorNotReady) {
+            const double a = std::chrono::duration<double, std::milli>(now - e->t_launch[slot]).count();
+            return a > age ? a : age;
+        }
         if (q != hipSuccess) return -2.0;
         ++e->finished;
     }
-    return -1.0;
+    return age;
 }
 
 // Device time of finished collective number `seq` (start -> done events), -1 if it has not
@@ -369,7 +440,7 @@ DDL_API double ddl_comm_oldest_pending_ms(void* h) {
 DDL_API double ddl_comm_collective_ms(void* h, long seq) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1.0;
-    std::lock_guard<std::mutex> lk(e->mu);
+    std::lock_guard<std::mutex> bk(e->book);
     if (seq < 1 || seq > e->launched || e->launched - seq >= RING) return -1.0;
     const long slot = (seq - 1) % RING;
     if (hipEventQuery(e->done[slot]) != hipSuccess) return -1.0;
@@ -378,15 +449,15 @@ DDL_API double ddl_comm_collective_ms(void* h, long seq) {
     return ms;
 }
 
-// Failure path from any thread: ncclCommAbort (kernels spinning on a dead peer return, the
-// streams drain) and mark the engine unusable; the stream / events stay for destroy.
+// Failure path from any thread, lock-free: the communicator is swapped out first (later API
+// calls see it gone), then ncclCommAbort (kernels spinning on a dead peer return, the streams
+// drain, an enqueue blocked in connection setup returns); the stream / events stay for destroy.
 DDL_API int ddl_comm_abort(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (e->comm && !e->aborted) g_rccl.commAbort(e->comm);
-    e->comm = nullptr;
-    e->aborted = true;
+    e->aborted.store(true);
+    ncclComm_t c = e->comm.exchange(nullptr);
+    if (c) g_rccl.commAbort(c);
     return 0;
 }
 
@@ -394,14 +465,24 @@ DDL_API int ddl_comm_abort(void* h) {
 DDL_API int ddl_comm_inject_error(void* h, int code) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    std::lock_guard<std::mutex> lk(e->mu);
-    e->injected = code;
+    e->injected.store(code);
+    return 0;
+}
+
+// Test hook: the next collective enqueue blocks `ms` milliseconds inside the engine (holding the
+// API lock, as an RCCL enqueue stuck in connection setup to a dead peer does), then fails with -4
+// if the communicator was aborted meanwhile.
+DDL_API int ddl_comm_test_stall(void* h, int ms) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e) return -1;
+    e->stall_ms.store(ms);
     return 0;
 }
 
 DDL_API long ddl_comm_stats(void* h, int which) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
+    std::lock_guard<std::mutex> bk(e->book);
     return which == 0 ? e->launched : e->bytes;
 }
 
@@ -409,14 +490,15 @@ DDL_API void ddl_comm_destroy(void* h, int abort) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return;
     {
-        std::lock_guard<std::mutex> lk(e->mu);
-        if (e->comm) {
-            if (abort) g_rccl.commAbort(e->comm);
+        std::lock_guard<std::mutex> lk(e->api);     // no API call in flight past this point
+        e->aborted.store(true);
+        ncclComm_t c = e->comm.exchange(nullptr);
+        if (c) {
+            if (abort) g_rccl.commAbort(c);
             else {
                 hipStreamSynchronize(e->stream);
-                g_rccl.commDestroy(e->comm);
+                g_rccl.commDestroy(c);
             }
-            e->comm = nullptr;
         }
     }
     for (int i = 0; i < RING; ++i) {

@@ -44,15 +44,20 @@ class TrainConfig:
     lr_warmup_steps: int = 0
     # ---- distributed ------------------------------------------------------
     backend: str = "auto"            # auto|nccl|gloo  (nccl == RCCL on ROCm)
-    bucket_mb: float = 25.0          # gradient bucket size for the reducer (<= 0: "auto", from the comm probe)
-    first_bucket_mb: float = 4.0     # small first bucket so comm starts early
-    comm_probe: bool = True          # world > 1 with the native engine: time 1/4/16/64 MB all-reduces at start
+    bucket_mb: float = 0.0           # gradient bucket size for the reducer (<= 0: "auto" -- sized from the
+                                     # startup all-reduce probe at world > 1 with the native engine; the
+                                     # 4 / 25 MB constants without a probe; bucket_policy.source says which)
+    first_bucket_mb: float = 4.0     # small first bucket so comm starts early (fixed bucket_mb only)
+    comm_probe: bool = False         # probe even with a fixed bucket_mb (the auto policy always probes)
     comm: str = "auto"               # gradient all-reduce engine: auto|native (C++ RCCL engine)|torch
     grad_reduce_dtype: str = "auto"  # auto|fp32|bf16  all-reduce payload dtype
     broadcast_buffers: bool = False
     sync_bn: bool = False            # SyncBatchNorm: BN statistics summed over all ranks (CV models)
     zero_optimizer: bool = False     # ZeRO-1: fp32 master + optimizer state sharded 1/world per rank
     overlap_optimizer: bool = True   # world > 1: per-bucket optimizer updates as each all-reduce completes
+    dp_rehearsal: bool = False       # world 1 on a GPU: run the N > 1 step's form anyway -- native RCCL
+                                     # engine (1-rank communicator), per-bucket all-reduces, per-bucket
+                                     # range optimizer (overlap_optimizer) -- so its cost shows in phases_ms
     eager_optimizer: bool = False    # GPU: those updates start during backward, on a side stream
                                      # (1 GPU same-box A/B: -0.4 % -- the HBM-bound updates slow the
                                      # concurrent backward GEMMs about as much as they hide)

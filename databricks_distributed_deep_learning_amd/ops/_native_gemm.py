@@ -355,6 +355,13 @@ def _flush_buf(device) -> torch.Tensor:
     return b
 
 
+def release_tuning_buffers() -> None:
+    """Drop the tuner's cache-flush buffers (640 MB each): called once the warm-up has tuned every
+    signature, so that HBM returns to the allocator for the training step (a signature first seen
+    later re-creates its buffer on demand)."""
+    _flush_bufs.clear()
+
+
 def _time_runs(run, reps: int, cold: bool = False) -> float:
     """Milliseconds per call over ``reps`` launches, in DEVICE time.
 

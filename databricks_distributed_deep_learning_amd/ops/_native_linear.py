@@ -28,6 +28,69 @@ def _ok(x, w) -> bool:
             and x.numel() > 0)
 
 
+def _ok_padded(x, w) -> bool:
+    """Output width not a multiple of 8 (a classifier head: num_labels = 2): the GEMMs run on the
+    native kernels over N rounded up to 8 (zero weight rows), see ``_LinearPadN``."""
+    K = x.shape[-1]
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and K % 8 == 0 and w.shape[0] % 8 != 0
+            and x.numel() > 0)
+
+
+class _LinearPadN(torch.autograd.Function):
+    """y = x W^T (+ b) (tanh / relu) for N % 8 != 0 on the native GEMMs: W, b and dy are
+    zero-padded to Np = roundup(N, 8) rows / columns (a few KB for a classifier head), so the
+    forward NT, the dgrad NN (reduction over Np) and the weight-gradient TN are the same
+    MFMA kernels as every other Linear -- no vendor GEMM runs for the head."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        K, N = x.shape[-1], w.shape[0]
+        Np = (N + 7) // 8 * 8
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M = x2.shape[0]
+        wp = torch.zeros(Np, K, dtype=w.dtype, device=w.device)
+        wp[:N] = w
+        bp = None
+        if b is not None:
+            bp = torch.zeros(Np, dtype=b.dtype, device=b.device)
+            bp[:N] = b
+        y = torch.empty(M, Np, dtype=x.dtype, device=x.device)
+        gemm(MODE_NT, x2, K, wp, K, y, Np, M, Np, K, bias=bp, act=act if act in ("tanh", "relu") else None)
+        out = y[:, :N].contiguous()
+        ctx.save_for_backward(x2, wp, out if act in ("tanh", "relu") else None)
+        ctx.act, ctx.has_bias, ctx.xshape, ctx.N = act, b is not None, x.shape, N
+        return out.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wp, y = ctx.saved_tensors
+        M, K = x2.shape
+        N, Np = ctx.N, wp.shape[0]
+        dy2 = dy.reshape(M, N)
+        if ctx.act == "tanh":
+            dy2 = (dy2.float() * (1 - y.float() ** 2)).to(dy2.dtype)
+        elif ctx.act == "relu":
+            dy2 = dy2 * (y > 0)
+        dyp = torch.zeros(M, Np, dtype=dy2.dtype, device=dy2.device)
+        dyp[:, :N] = dy2
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
+            gemm(MODE_NN, dyp, Np, wp, K, dx, K, M, K, Np)
+            dx = dx.view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dwp = torch.empty(Np, K, dtype=wp.dtype, device=wp.device)
+            gemm(MODE_TN, dyp, Np, x2, K, dwp, K, Np, K, M)
+            dw = dwp[:N]
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            dbp = torch.empty(Np, dtype=wp.dtype, device=wp.device)
+            E.colsum(dyp, dbp)
+            db = dbp[:N]
+        return dx, dw, db, None
+
+
 # dgrad as an NT GEMM against a cached W^T (DDL_DGRAD_NT=1) or as NN with W read through
 # transposed LDS reads (default): since the NN kernel's ds_read_b64_tr_b16 no longer waits
 # out the operand prefetch, NN is as fast as NT and needs no per-step W^T copy (the copy
@@ -283,6 +346,9 @@ class _DgeluHandoff:
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], act: Optional[str],
            bridge=None, fuse_dgelu: bool = False, residual: Optional[torch.Tensor] = None,
            residual_grad_to=None) -> torch.Tensor:
+    if (_ok_padded(x, w) and bridge is None and residual is None and act in (None, "tanh", "relu")
+            and (b is None or b.dtype == w.dtype)):
+        return _LinearPadN.apply(x, w, b, act)
     if not _ok(x, w) or (b is not None and b.dtype != w.dtype) or \
             (residual is not None and residual.shape[-1] != w.shape[0]):
         from .bridge import join

@@ -58,6 +58,7 @@ _SIGS = {
     "ddl_comm_collective_ms": ([P, L], ctypes.c_double),
     "ddl_comm_abort": ([P], I),
     "ddl_comm_inject_error": ([P, I], I),
+    "ddl_comm_test_stall": ([P, I], I),
 }
 _DTYPES = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2, torch.int64: 3, torch.int32: 4}
 
@@ -217,6 +218,11 @@ class NativeComm:
     def inject_error(self, code: int) -> None:
         """Test hook: make RCCL's asynchronous error state read ``code`` (the watchdog's input)."""
         _fn("ddl_comm_inject_error")(self._h, int(code))
+
+    def stall_next_enqueue(self, ms: int) -> None:
+        """Test hook: the next collective call blocks ``ms`` inside the engine, as an RCCL enqueue
+        stuck in connection setup to a dead peer does (the watchdog must still see and abort it)."""
+        _fn("ddl_comm_test_stall")(self._h, int(ms))
 
     def collective_ms(self, seq: int) -> float:
         """Device time of finished collective ``seq`` (its start / done events), -1 if unknown."""

@@ -70,9 +70,9 @@ class Bucket:
 def _drain_into(acc32: torch.Tensor, grad: torch.Tensor) -> None:
     """acc32 += grad; grad = 0 -- one native pass over the arena on the GPU (ddl_drain_acc),
     an add + zero fill elsewhere."""
-    if grad.is_cuda and grad.numel() % 8 == 0:
+    if grad.is_cuda and grad.numel() % 8 == 0 and grad.dtype in (torch.bfloat16, torch.float32):
         from ..ops import _lib
-        if _lib.available():
+        if _lib.use_native(grad):      # (False under --native off: the CPU-oracle mode)
             _lib.call("ddl_drain_acc", _lib.dcode(grad), acc32.data_ptr(), grad.data_ptr(), grad.numel())
             return
     acc32.add_(grad)

@@ -85,23 +85,51 @@ def adasum_tree(parts) -> torch.Tensor:
     return parts[0]
 
 
-def _gather_rows(t: torch.Tensor) -> torch.Tensor:
-    """[world, numel] copy of every rank's flat ``t`` (rank order)."""
-    flat = t.reshape(-1).contiguous()
-    out = torch.empty((size(), flat.numel()), dtype=flat.dtype, device=flat.device)
-    dist.all_gather_into_tensor(out, flat) if flat.is_cuda else dist.all_gather(list(out.unbind(0)), flat)
+def _combine_segments(lower: torch.Tensor, upper: torch.Tensor, segments) -> torch.Tensor:
+    """adasum_combine(lower, upper) applied to each (offset, numel) segment independently."""
+    out = torch.empty_like(lower)
+    for off, n in segments:
+        out[off:off + n] = adasum_combine(lower[off:off + n], upper[off:off + n])
     return out
 
 
+def _exchange(send: torch.Tensor, to, recv: torch.Tensor, frm: int) -> None:
+    """Send ``send`` to every rank in ``to`` and receive ``recv`` from ``frm`` (one batch: the
+    RCCL backend needs the pair's send and receive grouped, or both sends block)."""
+    ops = [dist.P2POp(dist.isend, send, q) for q in to] + [dist.P2POp(dist.irecv, recv, frm)]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+
+
 def adasum_allreduce(tensor: torch.Tensor, segments: Optional[Iterable] = None) -> torch.Tensor:
-    """Adasum of ``tensor`` over all ranks, identical on every rank (each rank combines the
-    gathered copies in the same order).  ``segments`` = (offset, numel) ranges combined
-    independently (Horovod applies Adasum per tensor); default: the whole tensor."""
-    rows = _gather_rows(tensor)
-    flat = rows[0].clone()
-    for off, n in (segments or [(0, flat.numel())]):
-        flat[off:off + n] = adasum_tree([rows[r, off:off + n] for r in range(rows.shape[0])])
-    return flat.view_as(tensor)
+    """Adasum of ``tensor`` over all ranks, identical on every rank, by recursive doubling:
+    at level l (stride s = 2^l) rank blocks of s ranks -- each block holding its Adasum so far --
+    pair with the neighbouring block (b, b ^ 1); every rank swaps its vector with one rank of the
+    partner block and both compute ``adasum_combine(lower block, upper block)`` (Horovod's
+    order: (0,1), (2,3), ... then pairs of pairs, = ``adasum_tree``); a block with no partner
+    is carried up unchanged.  Memory is O(numel) per rank (one receive buffer), not
+    world x numel.  ``segments`` = (offset, numel) ranges combined independently (Horovod
+    applies Adasum per tensor); default: the whole tensor."""
+    n, r = size(), rank()
+    cur = tensor.reshape(-1).contiguous().clone()
+    segs = list(segments or [(0, cur.numel())])
+    if n == 1:
+        return cur.view_as(tensor)
+    buf = torch.empty_like(cur)
+    s = 1
+    while s < n:
+        b, nblocks = r // s, -(-n // s)
+        pb = b ^ 1
+        if pb < nblocks:
+            first, bsize = b * s, min(s, n - b * s)
+            pfirst, psize = pb * s, min(s, n - pb * s)
+            frm = pfirst + min(r - first, psize - 1)          # my source in the partner block
+            to = [pfirst + j for j in range(psize) if first + min(j, bsize - 1) == r]
+            _exchange(cur, to, buf, frm)
+            lower, upper = (cur, buf) if b < pb else (buf, cur)
+            cur = _combine_segments(lower, upper, segs)
+        s *= 2
+    return cur.view_as(tensor)
 
 
 def allreduce(tensor: torch.Tensor, average: Optional[bool] = None, name: Optional[str] = None,
@@ -179,6 +207,13 @@ class _DistributedOptimizer:
     Communication is bucketed and overlapped with backward through the same
     hook-driven reducer as :class:`DataParallel` (grads are views into one flat
     arena, all-reduced slice by slice as they become ready).
+
+    ``op=Adasum`` follows Horovod's Adasum optimizer: every rank takes a LOCAL optimizer step
+    on its own gradient, and the parameter deltas (not the raw gradients) are combined with
+    Adasum per tensor (:func:`adasum_allreduce`, recursive doubling); the parameters become
+    ``p_before + adasum(delta)``.  For plain SGD this equals Adasum of the gradients (times
+    -lr); with momentum / Adam the two differ, and this is the one Horovod computes.
+    (Horovod itself is not importable here: the parity is with its documented algorithm.)
     """
 
     def __init__(self, optimizer: torch.optim.Optimizer, named_parameters: Optional[Iterable] = None,
@@ -197,8 +232,7 @@ class _DistributedOptimizer:
         self.op = op
         self.backward_passes_per_step = backward_passes_per_step
         if op == Adasum:
-            # Adasum needs every rank's whole gradient of a tensor at once (its dot products):
-            # gradients accumulate locally in the arena and are combined per tensor at step()
+            # gradients stay local (accumulated in the arena); step() combines the deltas
             self.arena.rebind_grads()
             self._reducer = None
             return
@@ -219,13 +253,8 @@ class _DistributedOptimizer:
             self._reducer.zero_grad()
 
     def synchronize(self) -> None:
-        if self._reducer is None:       # Adasum: per-tensor combination of the gathered gradients
+        if self._reducer is None:       # Adasum: nothing to reduce before the local step
             self.arena.rebind_grads()   # gradients a set_to_none zero_grad detached from the arena
-            if size() > 1:
-                g, moved = _prep(self.arena.grad)
-                segs = [(e.offset, e.numel) for e in self.arena.entries]
-                out = adasum_allreduce(g, segs)
-                self.arena.grad.copy_(out.to(self.arena.grad.device) if moved else out)
             return
         self._reducer.finish()
         if self.op == Average and size() > 1:
@@ -233,7 +262,19 @@ class _DistributedOptimizer:
 
     def step(self, closure=None):
         self.synchronize()
-        return self.optimizer.step(closure)
+        if self._reducer is not None or size() == 1:
+            return self.optimizer.step(closure)
+        # Adasum: local step, then p = p_before + Adasum over ranks of (p_after - p_before)
+        before = self.arena.flat.detach().clone()
+        loss = self.optimizer.step(closure)
+        with torch.no_grad():
+            delta = self.arena.flat - before
+            d, moved = _prep(delta)
+            segs = [(e.offset, e.numel) for e in self.arena.entries]
+            out = adasum_allreduce(d, segs)
+            self.arena.flat.copy_(before + (out.to(before.device) if moved else out))
+        self.arena.bump()
+        return loss
 
     def state_dict(self):
         return self.optimizer.state_dict()

@@ -69,7 +69,8 @@ class Trainer:
             first_mb, bucket_mb = auto_buckets(self.comm_probe, self.arena.numel * esz / 2 ** 20) \
                 if self.comm_probe else (4.0, 25.0)
         self.bucket_policy = {"bucket_mb": bucket_mb, "first_bucket_mb": first_mb,
-                              "source": "probe" if cfg.bucket_mb <= 0 and self.comm_probe else "config"}
+                              "source": ("probe" if self.comm_probe else "default") if cfg.bucket_mb <= 0
+                              else "config"}
         # LAMB's trust ratio needs every tensor whole in one optimizer range: no split tensors
         self.ddp = DataParallel(model, self.arena, bucket_mb=bucket_mb, first_bucket_mb=first_mb,
                                 reduce_dtype=rd, broadcast_buffers=cfg.broadcast_buffers,
@@ -82,8 +83,8 @@ class Trainer:
         if zero:
             self.opt.gather_fn = self.ddp.gather_params
         self.sched = LRSchedule(cfg.lr, cfg.lr_schedule, cfg.lr_warmup_steps, cfg.steps + cfg.warmup_steps)
-        self.overlap_optimizer = (self.world > 1 and cfg.overlap_optimizer and self.opt.supports_ranges()
-                                  and self.ddp.reduce_dtype == self.arena.dtype)
+        self.overlap_optimizer = ((self.world > 1 or self.rehearsal) and cfg.overlap_optimizer
+                                  and self.opt.supports_ranges() and self.ddp.reduce_dtype == self.arena.dtype)
         # on the GPU the per-bucket updates start DURING backward, on a side stream, as soon as a
         # bucket's gradients (and its all-reduce) are done (DataParallel.set_eager)
         self.eager_optimizer = (cfg.overlap_optimizer and cfg.eager_optimizer and self.opt.supports_ranges()
@@ -106,7 +107,12 @@ class Trainer:
         (``parallel.comm.probe_allreduce``: 1 / 4 / 16 / 64 MB all-reduces, bus GB/s) before
         the buckets are laid out -- ``bucket_mb <= 0`` sizes them from the probe."""
         c = self.cfg
-        if self.world == 1 or c.comm not in ("auto", "native") or self.device.type != "cuda":
+        # (the watchdog runs from the engine's construction on, so a peer lost during the probe
+        # aborts the communicator instead of hanging the rank)
+        self.rehearsal = False
+        if c.comm not in ("auto", "native") or self.device.type != "cuda":
+            return c.comm, []
+        if self.world == 1 and not c.dp_rehearsal:
             return c.comm, []
         from ..parallel.comm import CommError, NativeComm, native_available, probe_allreduce
         if not native_available():
@@ -117,8 +123,9 @@ class Trainer:
             if c.comm == "native":
                 raise
             return "torch", []
+        self.rehearsal = self.world == 1
         probe = []
-        if c.comm_probe or c.bucket_mb <= 0:
+        if self.world > 1 and (c.comm_probe or c.bucket_mb <= 0):
             probe = probe_allreduce(eng, self.device, dtype=reduce_dtype or self.arena.dtype, world=self.world)
         return eng, probe
 
@@ -268,6 +275,7 @@ class Trainer:
                 _native_gemm.online_collect()
         if warmup:
             self.agree_kernel_plans()
+        _native_gemm.release_tuning_buffers()     # the tuner's 640 MB flush buffer back to the allocator
         self.phases.summary(reset=True)          # warm-up (and tuning) steps are not reported
         timer = StepTimer(self.device)
         meter = ThroughputMeter(self.samples_per_step)
@@ -323,6 +331,19 @@ class Trainer:
         }
         if self.comm_probe:
             summary["comm_probe"] = self.comm_probe
+        if self.rehearsal:
+            summary["dp_rehearsal"] = True
+        eng = getattr(self.ddp, "native", None)
+        if eng is not None and hasattr(eng, "world"):
+            # the communicator's own view of the job (what RCCL was initialised with)
+            summary["rccl"] = {"nranks": int(eng.world), "rank": int(eng.rank), "device": int(eng.device.index),
+                               "version": ".".join(str(v) for v in torch.cuda.nccl.version())}
+        if self.world > 1 and self.device.type == "cuda":
+            import socket
+            summary["rank_devices"] = ddist.all_gather_object(
+                {"rank": self.rank, "device": self.device.index, "host": socket.gethostname(),
+                 "pci": torch.cuda.get_device_properties(self.device).pci_bus_id
+                 if hasattr(torch.cuda.get_device_properties(self.device), "pci_bus_id") else None})
         timings = self.ddp.bucket_timings()       # the last step's rings (synchronised by the barrier above)
         if timings:
             summary["comm_buckets"] = timings

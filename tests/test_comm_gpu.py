@@ -247,6 +247,42 @@ def test_watchdog_aborts_on_async_error(pg):
     c.close()
 
 
+def test_watchdog_aborts_blocked_enqueue(pg):
+    """An enqueue that blocks inside the engine (held API lock: RCCL connection setup to a dead
+    peer) is seen by the watchdog as a pending collective and aborted: the watchdog's calls never
+    wait for the API lock, the blocked call returns CommError, and close() does not hang."""
+    import threading
+    import time
+    from databricks_distributed_deep_learning_amd.parallel.comm import CommError, NativeComm
+    c = NativeComm(timeout_s=0.5, poll_s=0.05)
+    x = torch.ones(4096, device=pg)
+    c.all_reduce(x)
+    c.wait()
+    torch.cuda.synchronize()
+    c.stall_next_enqueue(4000)
+    err = []
+
+    def enqueue():
+        try:
+            c.all_reduce(x)
+        except CommError as e:
+            err.append(str(e))
+
+    t = threading.Thread(target=enqueue)
+    t0 = time.time()
+    t.start()
+    while c.failed is None and time.time() - t0 < 10:
+        time.sleep(0.02)
+    # aborted while the enqueue was still blocked (it blocks for 4 s)
+    assert c.failed and "unfinished after" in c.failed, c.failed
+    assert time.time() - t0 < 3.5
+    t.join(timeout=10)
+    assert not t.is_alive() and err, err
+    with pytest.raises(CommError):
+        c.broadcast(x)
+    c.close()
+
+
 def test_engine_probe_and_bucket_timings(pg):
     """The startup probe runs on the engine, and the reducer reports per-bucket ring times of
     the last step (world 1: every number exists, bus bandwidth is 0 by the 2(n-1)/n factor)."""

@@ -479,3 +479,71 @@ def test_split_tensor_buckets_match(opt_name):
     assert len(pieces) >= 2, out["layout"]
     assert all((b[0] - pieces[0][0]) % 8192 == 0 for b in pieces), out["layout"]
     assert out["err"] < 1e-6, out
+
+
+# ---------------------------------------------------------------- bf16 vs fp32 gradient payloads
+def _ring_sum_bf16(chunks):
+    """What an n-rank RCCL ring all-reduce computes for a bf16 payload: the reduce-scatter walks
+    each chunk through the ranks in ring order, every hop adding in fp32 and storing the running
+    sum as bf16 (n - 1 roundings), then the all-gather copies the result unchanged."""
+    acc = chunks[0].to(torch.bfloat16)
+    for c in chunks[1:]:
+        acc = (acc.float() + c.to(torch.bfloat16).float()).to(torch.bfloat16)
+    return acc.float()
+
+
+def _bert_grad_reduce_error():
+    """Each of 8 ranks computes real BERT-base-architecture gradients (bf16 model, its own
+    micro-batch; 2 encoder layers to keep 8 CPU processes fast) -- the payload the data-parallel
+    reducer ships.  Rank 0 compares the summed gradient of an fp32 payload, gloo's own bf16
+    all-reduce and an RCCL-ring bf16 emulation against an fp64 sum."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd import ops
+    from databricks_distributed_deep_learning_amd.models.bert import bert_base
+    ops.set_native_mode("off")
+    r, n = dist.get_rank(), dist.get_world_size()
+    torch.manual_seed(0)
+    m = bert_base(num_labels=2, dropout=0.0, num_hidden_layers=2, vocab_size=4096).to(torch.bfloat16)
+    g = torch.Generator().manual_seed(100 + r)
+    ids = torch.randint(0, 4096, (4, 64), generator=g)
+    labels = torch.randint(0, 2, (4,), generator=g)
+    loss, _ = m(ids, None, None, labels)
+    loss.backward()
+    grad = torch.cat([p.grad.reshape(-1) for p in m.parameters() if p.grad is not None])   # bf16
+    # fp32 payload (what grad_reduce_dtype=fp32 ships) and bf16 payload through gloo
+    g32 = grad.float().clone()
+    dist.all_reduce(g32)
+    try:
+        g16 = grad.clone()
+        dist.all_reduce(g16)
+        g16 = g16.float()
+    except RuntimeError:              # gloo without bf16 sums: the ring emulation below only
+        g16 = None
+    every = [torch.empty_like(grad) for _ in range(n)]
+    dist.all_gather(every, grad)
+    if r != 0:
+        return None
+    ref = torch.stack([e.double() for e in every]).sum(0)
+    ring = _ring_sum_bf16([e for e in every])
+
+    def rel(x):
+        return float((x.double() - ref).norm() / ref.norm())
+    once = rel(ref.to(torch.bfloat16))          # the unavoidable part: one rounding of the exact sum
+    return {"fp32": rel(g32), "gloo_bf16": None if g16 is None else rel(g16), "ring_bf16": rel(ring),
+            "round_once": once, "numel": grad.numel()}
+
+
+def test_bf16_gradient_reduce_error_world8():
+    """Gradient-reduce payload precision at world 8.  The default payload is
+    the arena dtype (bf16): an 8-rank ring rounds every running sum to bf16 seven times.  Measured
+    on real BERT gradients: the ring's relative error (L2, whole gradient) is a small multiple of a
+    single bf16 rounding of the exact sum and well under 1 % -- far below the minibatch gradient
+    noise the optimizer sees -- so the bf16 payload (half the xGMI bytes) stays the default;
+    ``grad_reduce_dtype=fp32`` is the switch for anyone who wants the exact sum."""
+    out = Distributor(num_processes=8, use_gpu=False, timeout_s=600).run(_bert_grad_reduce_error)
+    assert out["fp32"] < 1e-6, out
+    assert out["ring_bf16"] < 8 * out["round_once"], out
+    assert out["ring_bf16"] < 0.01, out
+    if out["gloo_bf16"] is not None:
+        assert out["gloo_bf16"] < 0.01, out
+    print("bf16 vs fp32 reduce error (8 ranks):", out)

@@ -109,6 +109,36 @@ def test_linear_autograd(act):
         assert _rel_err(got, want) < 3e-2
 
 
+@pytest.mark.parametrize("N,act", [(2, None), (5, "tanh"), (1000 + 3, None)])
+def test_linear_padded_n_native(N, act, monkeypatch):
+    """N % 8 != 0 (BERT's classifier head, num_labels = 2) runs on the native GEMMs over N padded
+    to 8 (no hipBLASLt): forward and all three gradients against fp32 autograd."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_linear
+    from databricks_distributed_deep_learning_amd.ops.linear import linear_reference
+    called = []
+    orig = torch.nn.functional.linear
+
+    def spy(*a, **k):      # F.linear on GPU tensors = hipBLASLt
+        called.append(1)
+        return orig(*a, **k)
+    monkeypatch.setattr(torch.nn.functional, "linear", spy)
+    torch.manual_seed(2)
+    x = torch.randn(128, 768, device=dev).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(N, 768, device=dev) * 0.05).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(N, device=dev).to(torch.bfloat16).requires_grad_(True)
+    y = _native_linear.linear(x, w, b, act)
+    g = torch.randn(128, N, device=dev)
+    y.backward(g.to(torch.bfloat16))
+    assert not called and y.shape == (128, N)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = linear_reference(xr, wr, br, act)
+    assert _rel_err(y, yr) < 2e-2
+    yr.backward(g.to(torch.bfloat16).float())
+    for got, want in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert got.shape == want.shape and _rel_err(got, want) < 3e-2
+
+
 CONVS = [  # N, H, W, C, K, R, stride, pad
     (2, 14, 14, 64, 64, 3, 1, 1),
     (2, 15, 13, 64, 128, 3, 2, 1),

@@ -228,7 +228,8 @@ def _hvd_adasum():
     g = [torch.randn(7, generator=torch.Generator().manual_seed(40 + k)) for k in range(2)]
     red = hvd.allreduce(g[r], op=hvd.Adasum)
     err_t = (red - adasum_combine(g[0], g[1])).abs().max().item()
-    # DistributedOptimizer(op=Adasum): per-tensor Adasum of the two ranks' gradients
+    # DistributedOptimizer(op=Adasum): local step, per-tensor Adasum of the parameter deltas;
+    # plain SGD: delta = -lr * g, so p = p0 - lr * Adasum(g0, g1) (Adasum is scale invariant)
     torch.manual_seed(3)
     m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 2))
     x = torch.randn(8, 6, generator=torch.Generator().manual_seed(9))
@@ -239,12 +240,33 @@ def _hvd_adasum():
         grads.append([p.grad.clone() for p in m.parameters()])
     opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), named_parameters=m.named_parameters(),
                                    op=hvd.Adasum)
+    p0 = [p.detach().clone() for p in m.parameters()]
     opt.zero_grad()
     m(x[4 * r:4 * r + 4]).square().sum().backward()
-    opt.synchronize()
-    err_o = max((p.grad - adasum_combine(grads[0][i], grads[1][i])).abs().max().item()
+    opt.step()
+    err_o = max((p.detach() - (p0[i] - 0.1 * adasum_combine(grads[0][i], grads[1][i]))).abs().max().item()
                 for i, p in enumerate(m.parameters()))
     return err_t, err_o
+
+
+def _hvd_adasum_tree(n):
+    """Recursive-doubling Adasum over n ranks == adasum_tree of the n inputs (incl. an odd
+    world: a block without a partner is carried up), identical on every rank."""
+    from databricks_distributed_deep_learning_amd.parallel import hvd
+    from databricks_distributed_deep_learning_amd.parallel.horovod import adasum_allreduce, adasum_tree
+    hvd.init()
+    r = hvd.rank()
+    g = [torch.randn(11, generator=torch.Generator().manual_seed(70 + k)) for k in range(n)]
+    segs = [(0, 4), (4, 7)]
+    red = adasum_allreduce(g[r], segs)
+    want = torch.cat([adasum_tree([x[o:o + k] for x in g]) for o, k in segs])
+    return (red - want).abs().max().item()
+
+
+@pytest.mark.parametrize("n", [3, 4])
+def test_horovod_adasum_recursive_doubling(n):
+    res = HorovodRunner(np=n, use_gpu=False).run(_hvd_adasum_tree, n=n)
+    assert res < 1e-6, res
 
 
 def test_horovod_adasum_world2():
