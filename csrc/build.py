@@ -57,7 +57,8 @@ def needs(src, obj, hdr_mtime):
 # gradient kernel (2.7x its MFMA time), conv3x3_wgrad_k (620 moves per 144 MFMAs, 414 registers ->
 # 260), the skinny GEMMs.  gemm_big.hip's 8-wave kernels compile identically either way.
 _VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
-EXTRA = {"gemm_big.hip": _VGPR_FORM, "conv3x3.hip": _VGPR_FORM, "skinny_gemm.hip": _VGPR_FORM}
+EXTRA = {"gemm_big.hip": _VGPR_FORM, "conv3x3.hip": _VGPR_FORM, "skinny_gemm.hip": _VGPR_FORM,
+         "stream_gemm.hip": _VGPR_FORM}
 
 
 def compile_one(src, debug=False):

@@ -232,6 +232,20 @@ __device__ __forceinline__ float row16_sum(float v) {
     v = dpp_add<0x141>(v);   // row_half_mirror
     return dpp_add<0x140>(v);   // row_mirror
 }
+// Whole-wave sum with no LDS traffic: the 16-lane row sums (DPP), then gfx950's
+// v_permlane16_swap / v_permlane32_swap exchange rows (0,1), (2,3) and the two halves -- each
+// lane adds its own value and its partner's, so every lane ends with the wave's sum.  Six
+// dependent VALU steps instead of the six ds_bpermute round trips (and their LDS bank cycles)
+// of the __shfl_xor tree.  All 64 lanes must be active.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v = row16_sum(v);
+    const uint32_t u = __float_as_uint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const uint32_t w = __float_as_uint(v);
+    const auto b = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 
 // Fast unsigned division by a runtime constant (magic multiply), for index math
 // in hot loops: q = umulhi(n, mul) >> shift, exact for n < 2^31.

@@ -112,6 +112,7 @@ struct BigParams {
     const float* bn_istd;
     int* sched;               // persistent grid: per-XCD tile tickets (null: static tile striding)
     int xsplit;               // split-K on a 1-D grid whose XCDs run contiguous (split, tile) runs
+    int part_bf16;            // split-K partial slabs stored as bf16 (DDL_GEMM_PART_BF16, default on)
 };
 // tile-ticket slot layout: 8 per-XCD counters + one exit counter, 128 B apart
 constexpr int SCHED_STRIDE = 32;
@@ -446,13 +447,15 @@ __device__ __forceinline__ void epilogue4(const BigParams& p, long orow, int n, 
 // Covers bias / residual / ReLU / GELU (+pre-activation) / accumulate / fp32 /
 // split-K partial outputs; tanh, dGELU and row remap take the LDS-staged epilogue.
 // `fin` receives the four values as stored (for column statistics of the output)
+template <bool PB = false>
 __device__ __forceinline__ void direct4(const BigParams& p, int m, int n, const f32x4& a, int split, float* fin) {
     if (m >= p.M || n >= p.N) return;
     const bool full = n + 3 < p.N;
     const int nv = p.N - n;
     float v[4] = {a[0], a[1], a[2], a[3]};
     if (p.splits > 1) {
-        store4g((float*)p.C + split * p.split_stride + (long)m * p.ldc + n, full, nv, v);
+        if constexpr (PB) store4g((bf16_t*)p.C + split * p.split_stride + (long)m * p.ldc + n, full, nv, v);
+        else store4g((float*)p.C + split * p.split_stride + (long)m * p.ldc + n, full, nv, v);
         return;
     }
     if (p.bias) {
@@ -527,7 +530,10 @@ __device__ __forceinline__ int col_base(int n0, int qn, int wn, int j) {
 
 // HOIST: the residual / pre-activation loads of all column groups up front (off in the weight-gradient
 // kernels, whose only bf16 tiles are rare unsplit ones: the extra registers spilled their main loop)
-template <int EK, bool N192 = false, bool HOIST = true>
+// PB: the split-K partials are bf16 (the weight-gradient instantiations, compile-time: a run-time
+// choice between two store paths spilled 128 scratch ops into their MFMA main loops, and so did
+// a bf16 path in the other kernels' epilogues -- scripts/check_spills.py)
+template <int EK, bool N192 = false, bool HOIST = true, bool PB = false>
 __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2][4][2], int m0, int n0, int tm,
                                            int wm, int wn, int lane, int split) {
     const int g4 = (lane >> 4) * 4, r16 = lane & 15;
@@ -712,14 +718,18 @@ __device__ __forceinline__ void epi_direct(const BigParams& p, f32x4 (&acc)[2][2
                         }
                     } else if (EK == EK_F32) {
                         if (p.splits > 1) {
-                            *reinterpret_cast<f32x4*>((float*)p.C + split * p.split_stride + (long)m * p.ldc + n) = a;
+                            if constexpr (PB)   // the weight-gradient kernels' partials are always bf16
+                                *reinterpret_cast<uint2*>((bf16_t*)p.C + split * p.split_stride + (long)m * p.ldc + n) =
+                                    make_uint2(pack2bf(a[0], a[1]), pack2bf(a[2], a[3]));
+                            else
+                                *reinterpret_cast<f32x4*>((float*)p.C + split * p.split_stride + (long)m * p.ldc + n) = a;
                         } else {
                             f32x4* cp = reinterpret_cast<f32x4*>((float*)p.C + (long)m * p.ldc + n);
                             *cp = p.accumulate ? a + *cp : a;
                         }
                     } else {
                         float fin[4] = {0.f, 0.f, 0.f, 0.f};
-                        direct4(p, m, n, a, split, fin);
+                        direct4<PB>(p, m, n, a, split, fin);
                         if (stats && m < p.M) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
@@ -1270,13 +1280,13 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
             } else if (interior && p.ek == EK_BF16)
                 epi_direct<EK_BF16, N192, !WGRAD>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_F32)
-                epi_direct<EK_F32, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_F32, N192, true, WGRAD>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (interior && p.ek == EK_GELU)
                 epi_direct<EK_GELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if (!WGRAD && interior && p.ek == EK_DGELU)   // (never a weight gradient's)
                 epi_direct<EK_DGELU, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             else if constexpr (EDGE)
-                epi_direct<EK_GEN, N192>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
+                epi_direct<EK_GEN, N192, true, WGRAD>(p, acc, m0c, n0c, tm_c, wm, wn, lane, split);
             STAMP(3);
 #ifdef DDL_GEMM_STAMPS
             ++stamp_ti;
@@ -1389,9 +1399,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 }
             }
             if (partial) {
-                float* dst = (float*)p.C + split * p.split_stride + (long)m * p.ldc + n;
-                store4g(dst, n + 3 < p.N, p.N - n, v);
-                if (n + 4 < p.N) store4g(dst + 4, n + 7 < p.N, p.N - n - 4, v + 4);
+                if constexpr (WGRAD) {
+                    bf16_t* dst = (bf16_t*)p.C + split * p.split_stride + (long)m * p.ldc + n;
+                    store4g(dst, n + 3 < p.N, p.N - n, v);
+                    if (n + 4 < p.N) store4g(dst + 4, n + 7 < p.N, p.N - n - 4, v + 4);
+                } else {
+                    float* dst = (float*)p.C + split * p.split_stride + (long)m * p.ldc + n;
+                    store4g(dst, n + 3 < p.N, p.N - n, v);
+                    if (n + 4 < p.N) store4g(dst + 4, n + 7 < p.N, p.N - n - 4, v + 4);
+                }
                 continue;
             }
             const long orow = out_row(p, m);
@@ -1439,7 +1455,8 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     }
 }
 
-// Split-K: sum fp32 partial slabs + the epilogue; 4 consecutive columns per thread.
+// Split-K: sum the partial slabs (fp32, or bf16 with p.part_bf16) + the epilogue; 4 consecutive
+// columns per thread.
 __global__ __launch_bounds__(256) void big_reduce_k(BigParams p, const float* __restrict__ part) {
     const long n4 = ((long)p.N + 3) / 4;
     const long total = (long)p.M * n4;
@@ -1451,7 +1468,8 @@ __global__ __launch_bounds__(256) void big_reduce_k(BigParams p, const float* __
         float v[4] = {0.f, 0.f, 0.f, 0.f};
         for (int s = 0; s < p.splits; ++s) {
             float t[4];
-            load4g(part + s * p.split_stride + (long)m * p.ldc + n, full, nv, t);
+            if (p.part_bf16) load4g((const bf16_t*)part + s * p.split_stride + (long)m * p.ldc + n, full, nv, t);
+            else load4g(part + s * p.split_stride + (long)m * p.ldc + n, full, nv, t);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += t[r];
         }
@@ -1609,15 +1627,27 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_wg_k(BigParams p) {
         iter(t + 3, 3);
     }
     VM0();      // no LDS-DMA may outlive the workgroup's LDS
-    // fp32 partial tile: lane holds C[m][n .. n+3] of each 16 x 16 block (the MFMA layout)
-    float* out = (float*)p.C + (long)split * p.split_stride;
+    // partial tile: lane holds C[m][n .. n+3] of each 16 x 16 block (the MFMA layout); fp32, or
+    // bf16 (p.part_bf16: half the slab bytes written here and read by the reduce)
     const int r16 = l & 15, g4 = (l >> 4) * 4;
+    if (p.part_bf16) {
+        bf16_t* out = (bf16_t*)p.C + (long)split * p.split_stride;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            *reinterpret_cast<f32x4*>(out + (long)(m0 + wm * 128 + i * 16 + r16) * p.ldc + n0 + wn * 64 + j * 16 + g4) =
-                acc[i][j];
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<uint2*>(out + (long)(m0 + wm * 128 + i * 16 + r16) * p.ldc + n0 + wn * 64 + j * 16 +
+                                          g4) = make_uint2(pack2bf(acc[i][j][0], acc[i][j][1]),
+                                                           pack2bf(acc[i][j][2], acc[i][j][3]));
+    } else {
+        float* out = (float*)p.C + (long)split * p.split_stride;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<f32x4*>(out + (long)(m0 + wm * 128 + i * 16 + r16) * p.ldc + n0 + wn * 64 + j * 16 + g4) =
+                    acc[i][j];
+    }
 }
 
 void fill_conv(ConvDesc& cd, const int* d) {
@@ -1716,6 +1746,16 @@ int behind_mask() {
     return m;
 }
 
+// DDL_GEMM_PART_BF16=0: split-K partial slabs in fp32 (default bf16: each partial is a fp32 sum of
+// its k-range rounded once; the reduce sums them in fp32 -- half the slab bytes on both sides)
+bool part_bf16_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_PART_BF16");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // DDL_GEMM_EPI_LDS=1: plain bf16 interior tiles store whole rows through LDS (epi_lds_bf16)
 bool epi_lds_enabled() {
     static const bool on = [] {
@@ -1734,10 +1774,15 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     p.tiles_n = (p.N + tbn - 1) / tbn;
     const int nk = (p.K + BK - 1) / BK;
     if (splits < 1) splits = 1;
+    // the weight-gradient kernel's split-K partials are bf16 (compiled in): an fp32 output asks
+    // for more than that, so it runs unsplit
+    if (LA == KO && LB == KO && p.out_f32) splits = 1;
     if (splits > nk) splits = nk > 0 ? nk : 1;
     p.kt_per_split = nk > 0 ? (nk + splits - 1) / splits : 1;
     splits = nk > 0 ? (nk + p.kt_per_split - 1) / p.kt_per_split : 1;
     p.splits = splits;
+    // weight gradients (TN): bf16 partial slabs, compiled in (epi_direct PB); the reduce reads them so
+    p.part_bf16 = LA == KO && LB == KO && splits > 1 ? 1 : 0;
     if (splits > 1) {
         p.split_stride = (long)p.M * p.ldc;
         if (!ws || ws_elems < p.split_stride * splits) return -2;
@@ -1893,6 +1938,7 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
     splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
     p.splits = splits;
     p.split_stride = (long)M * ldc;
+    p.part_bf16 = !out_f32 && part_bf16_enabled() ? 1 : 0;
     if (!workspace || ws_elems < p.split_stride * splits) return -2;
     BigParams kp = p;
     kp.C = workspace;

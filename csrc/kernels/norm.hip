@@ -528,13 +528,13 @@ __global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T
 #pragma unroll
         for (int j = 0; j < 4; ++j) s += v[k][j];
     }
-    const float mean = wave_sum(s) / H;
+    const float mean = wave_sum_dpp(s) / H;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < VPL; ++k)
 #pragma unroll
         for (int j = 0; j < 4; ++j) { const float d = v[k][j] - mean; q += d * d; }
-    const float rstd = rsqrtf(wave_sum(q) / H + eps);
+    const float rstd = rsqrtf(wave_sum_dpp(q) / H + eps);
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
         const int col = 256 * k + 4 * lane;
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
                                                 const T* __restrict__ dadd = nullptr) {
     // part row per block: [dgamma(H) | dbeta(H) | (dxsum) sum of dx (H)] -- the last is the
     // bias gradient of the Linear that produced this LayerNorm's input
-    __shared__ float s_acc[3][4][VPL * 256];
+    __shared__ __attribute__((aligned(16))) float s_acc[3][4][VPL * 256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float dg[VPL][4], db[VPL][4], ds[VPL][4], g[VPL][4];
 #pragma unroll
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
                 dg[k][j] += d[k][j] * xh[k][j];
                 db[k][j] += d[k][j];
             }
-        const float m1 = wave_sum(s1) / H, m2 = wave_sum(s2) / H;
+        const float m1 = wave_sum_dpp(s1) / H, m2 = wave_sum_dpp(s2) / H;
 #pragma unroll
         for (int k = 0; k < VPL; ++k) {
             float o[4];
@@ -687,14 +687,14 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             rb = rd;
         }
     }
+    // 16-byte stores (one ds_write_b128 per lane and column group): four scalar stores of a
+    // 16-byte lane stride put lanes l, l + 8, l + 16, l + 24 on one bank (4-way conflicts)
 #pragma unroll
-    for (int k = 0; k < VPL; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            s_acc[0][w][256 * k + 4 * lane + j] = dg[k][j];
-            s_acc[1][w][256 * k + 4 * lane + j] = db[k][j];
-            s_acc[2][w][256 * k + 4 * lane + j] = ds[k][j];
-        }
+    for (int k = 0; k < VPL; ++k) {
+        *reinterpret_cast<float4*>(&s_acc[0][w][256 * k + 4 * lane]) = make_float4(dg[k][0], dg[k][1], dg[k][2], dg[k][3]);
+        *reinterpret_cast<float4*>(&s_acc[1][w][256 * k + 4 * lane]) = make_float4(db[k][0], db[k][1], db[k][2], db[k][3]);
+        *reinterpret_cast<float4*>(&s_acc[2][w][256 * k + 4 * lane]) = make_float4(ds[k][0], ds[k][1], ds[k][2], ds[k][3]);
+    }
     __syncthreads();
     const int nv = dxsum ? 3 : 2;
     for (int c = threadIdx.x; c < H; c += 256) {
@@ -790,6 +790,235 @@ __global__ __launch_bounds__(256) void bn_partials_collapse_k(const float* __res
     out[(long)blockIdx.y * width + col] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
+// ---------------------------------------------------------------- merged collapse + finalize
+// The BatchNorm statistics / backward-coefficient finalize from thousands of partial rows (one
+// per 128 rows of a GEMM epilogue) used to be two launches: a 32:1 collapse, then ONE workgroup
+// per 64 channels walking every remaining row (latency-bound: each 16-row group of a 1024-thread
+// block is a dependent round trip).  Here one launch: grid (C / 64, S) workgroups of 1024
+// threads, each summing FIN_RPS rows of its 64 channels with all loads in flight (one round trip),
+// writing that slice's sums, then the agent-scope release / arrival-ticket hand-off
+// (cdna_hip_programming.md §5 "In-launch split-K reduction"): the workgroup that draws the last
+// ticket of its channel group acquires, sums the S slice rows (one more round trip) and finishes
+// the channels.  S = 1 (<= FIN_RPS rows) finishes directly.  Deterministic: fixed summation
+// order whichever workgroup arrives last.
+constexpr int FIN_RPS = 128;        // partial rows per slice (16 row lanes x 8 loads in flight)
+constexpr int TICKETS = 8192, TICKET_WIN = 64;
+
+// a window of TICKET_WIN zeroed arrival tickets for one launch (per device; the last arriver of
+// each group re-zeroes its ticket, so a window is reusable once its launch has finished --
+// TICKETS / TICKET_WIN launches later)
+static int* fin_tickets() {
+    static std::mutex mu;
+    static std::unordered_map<int, int*> pools;
+    static unsigned next = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    int*& pool = pools[dev];
+    if (!pool) {
+        if (hipMalloc(&pool, TICKETS * sizeof(int)) != hipSuccess) { pool = nullptr; return nullptr; }
+        if (hipMemset(pool, 0, TICKETS * sizeof(int)) != hipSuccess) return nullptr;
+    }
+    int* w = pool + (next % (TICKETS / TICKET_WIN)) * TICKET_WIN;
+    ++next;
+    return w;
+}
+
+// this workgroup's sums of rows [r0, r1) for column c and C + c (double, thread < 64 holds them)
+__device__ __forceinline__ void fin_slice(const float* __restrict__ part, int r0, int r1, long ld, int C, int c,
+                                          bool ok, float* red, double& s, double& q) {
+    const int rl = threadIdx.x >> 6;
+    float a = 0.f, b = 0.f;
+    if (ok) {
+        float va[8], vb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = r0 + rl + 16 * i;
+            va[i] = r < r1 ? part[(long)r * ld + c] : 0.f;
+            vb[i] = r < r1 ? part[(long)r * ld + C + c] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a += va[i]; b += vb[i]; }
+        for (int r = r0 + rl + 128; r < r1; r += 16) {      // rows beyond one round trip (S capped)
+            a += part[(long)r * ld + c];
+            b += part[(long)r * ld + C + c];
+        }
+    }
+    red[threadIdx.x] = a;
+    red[1024 + threadIdx.x] = b;
+    __syncthreads();
+    s = 0.0;
+    q = 0.0;
+    if (threadIdx.x < 64) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            s += (double)red[i * 64 + threadIdx.x];
+            q += (double)red[1024 + i * 64 + threadIdx.x];
+        }
+    }
+    __syncthreads();
+}
+
+// S > 1: publish this slice's sums, then the last arriver of the channel group returns true with
+// (s, q) = the full sums (threads < 64); every other workgroup returns false
+__device__ __forceinline__ bool fin_publish(float* __restrict__ ws, int* __restrict__ tickets, int C, int c, bool ok,
+                                            float* red, int* flag, double& s, double& q) {
+    if (threadIdx.x < 64 && ok) {
+        ws[(long)blockIdx.y * 2 * C + c] = (float)s;
+        ws[(long)blockIdx.y * 2 * C + C + c] = (float)q;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the fence's own wait can be dropped
+        const int t = __hip_atomic_fetch_add(tickets + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == (int)gridDim.y - 1;
+        if (last) {
+            __hip_atomic_store(tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*flag) return false;
+    fin_slice(ws, 0, gridDim.y, 2L * C, C, c, ok, red, s, q);
+    return true;
+}
+
+template <typename TP>
+__global__ __launch_bounds__(1024) void bn_fwd_finalize_k(const float* __restrict__ part, int nblk, int rps, int C,
+                                   long M, float* __restrict__ ws, int* __restrict__ tickets, const TP* __restrict__ gamma,
+                                   const TP* __restrict__ beta, float* __restrict__ running_mean,
+                                   float* __restrict__ running_var, float momentum, float eps,
+                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                   float* __restrict__ scale, float* __restrict__ shift) {
+    __shared__ float red[2048];
+    __shared__ int flag;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool ok = c < C;
+    const int r0 = blockIdx.y * rps;
+    double s, q;
+    fin_slice(part, r0, min(nblk, r0 + rps), 2L * C, C, c, ok, red, s, q);
+    if (gridDim.y > 1 && !fin_publish(ws, tickets, C, c, ok, red, &flag, s, q)) return;
+    if (threadIdx.x < 64 && ok)
+        bn_fwd_finish_channel<TP>(c, s, q, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+                                  save_invstd, scale, shift);
+}
+
+template <typename TP>
+__global__ __launch_bounds__(1024) void bn_bwd_finalize2_k(const float* __restrict__ part, int nblk, int rps, int C,
+                                    long M, float* __restrict__ ws, int* __restrict__ tickets, const TP* __restrict__ gamma,
+                                    const float* __restrict__ invstd, TP* __restrict__ dgamma, TP* __restrict__ dbeta,
+                                    float* __restrict__ coef, int acc) {
+    __shared__ float red[2048];
+    __shared__ int flag;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool ok = c < C;
+    const int r0 = blockIdx.y * rps;
+    double s, q;
+    fin_slice(part, r0, min(nblk, r0 + rps), 2L * C, C, c, ok, red, s, q);
+    if (gridDim.y > 1 && !fin_publish(ws, tickets, C, c, ok, red, &flag, s, q)) return;
+    if (threadIdx.x < 64 && ok)
+        bn_bwd_finish_channel<TP>(c, s, q, C, M, gamma, invstd, dgamma, dbeta, coef, acc, nullptr);
+}
+
+// The same merged scheme for the LayerNorm backward's column sums: NV = 2 ([dgamma | dbeta]) or 3
+// (+ the sum of dx: the producing Linear's bias gradient) columns of width H per partial row, all
+// NV loads of a row issued together (the single-workgroup colsum_partials_k walked the three
+// columns one after another: 3 x 4 dependent round trips over 512 rows).
+template <int NV>
+__device__ __forceinline__ void fin_slice_nv(const float* __restrict__ part, int r0, int r1, long ld, int H, int c,
+                                             bool ok, float* red, float* out) {
+    const int rl = threadIdx.x >> 6;
+    float a[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) a[v] = 0.f;
+    if (ok) {
+        float x[NV][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = r0 + rl + 16 * i;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) x[v][i] = r < r1 ? part[(long)r * ld + v * H + c] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) a[v] += x[v][i];
+        for (int r = r0 + rl + 128; r < r1; r += 16)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) a[v] += part[(long)r * ld + v * H + c];
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) red[v * 1024 + threadIdx.x] = a[v];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            float t = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) t += red[v * 1024 + i * 64 + threadIdx.x];
+            out[v] = t;
+        }
+    }
+    __syncthreads();
+}
+
+template <typename TP, int NV>
+__global__ __launch_bounds__(1024) void ln_colsum_k(const float* __restrict__ part, int nblk, int rps, int H,
+                                                    float* __restrict__ ws, int* __restrict__ tickets,
+                                                    TP* __restrict__ dg, TP* __restrict__ db, int acc,
+                                                    float* __restrict__ dxsum, TP* __restrict__ dxsink) {
+    __shared__ float red[NV * 1024];
+    __shared__ int flag;
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool ok = c < H;
+    const int r0 = blockIdx.y * rps;
+    float sum[NV];
+    fin_slice_nv<NV>(part, r0, min(nblk, r0 + rps), (long)NV * H, H, c, ok, red, sum);
+    if (gridDim.y > 1) {
+        if (threadIdx.x < 64 && ok) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) ws[(long)blockIdx.y * NV * H + v * H + c] = sum[v];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int t = __hip_atomic_fetch_add(tickets + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = t == (int)gridDim.y - 1;
+            if (last) {
+                __hip_atomic_store(tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            flag = last ? 1 : 0;
+        }
+        __syncthreads();
+        if (!flag) return;
+        fin_slice_nv<NV>(ws, 0, gridDim.y, (long)NV * H, H, c, ok, red, sum);
+    }
+    if (threadIdx.x >= 64 || !ok) return;
+    dg[c] = from_f<TP>(sum[0] + (acc ? to_f(dg[c]) : 0.f));
+    db[c] = from_f<TP>(sum[1] + (acc ? to_f(db[c]) : 0.f));
+    if constexpr (NV == 3) {
+        if (dxsum) dxsum[c] = sum[2];
+        if (dxsink) dxsink[c] = from_f<TP>(sum[2] + (acc ? to_f(dxsink[c]) : 0.f));
+    }
+}
+
+// slices for nblk partial rows: S = ceil(nblk / FIN_RPS), capped so the last arriver's pass over
+// the slice rows stays one round trip of 16 row lanes x 8 (ws holds S x 2C floats)
+static int fin_slices(int nblk) { return std::max(1, std::min(128, (nblk + FIN_RPS - 1) / FIN_RPS)); }
+static int fin_rps(int nblk) { return (nblk + fin_slices(nblk) - 1) / fin_slices(nblk); }
+static bool merged_finalize() {
+    static const bool on = [] { const char* e = getenv("DDL_BN_MERGED_FIN"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 // Partial rows beyond this are first collapsed 32:1 (a single finalize block per
 // 64 columns is too little parallelism for ~1000 rows).  The caller allocates
 // `part` with room for the collapsed rows behind the nblk partial rows.
@@ -821,6 +1050,22 @@ DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, lon
                                      const void* beta, float* running_mean, float* running_var, float momentum,
                                      float eps, float* save_mean, float* save_invstd, float* scale, float* shift,
                                      float* ws, long ws_elems, hipStream_t st) {
+    if (merged_finalize()) {
+        const int S = fin_slices(nblk);
+        int* tk = S > 1 ? fin_tickets() : nullptr;
+        if (S == 1 || (tk && ws && ws_elems >= (long)S * 2 * C)) {
+            const dim3 grid((C + 63) / 64, S);
+            if (dtype == 1)
+                bn_fwd_finalize_k<bf16_t><<<grid, 1024, 0, st>>>(part, nblk, fin_rps(nblk), C, M, ws, tk,
+                    (const bf16_t*)gamma, (const bf16_t*)beta, running_mean, running_var, momentum, eps, save_mean,
+                    save_invstd, scale, shift);
+            else
+                bn_fwd_finalize_k<float><<<grid, 1024, 0, st>>>(part, nblk, fin_rps(nblk), C, M, ws, tk,
+                    (const float*)gamma, (const float*)beta, running_mean, running_var, momentum, eps, save_mean,
+                    save_invstd, scale, shift);
+            DDL_RETURN_LAUNCH();
+        }
+    }
     const long need = ddl_bn_partials_ws(nblk, C);
     if (need > 0) {
         if (!ws || ws_elems < need) return -2;
@@ -897,9 +1142,20 @@ DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float*
 }
 
 // backward coefficients (+ dgamma / dbeta) from nblk partial rows: collapse (if many) + finalize
+// ws: null = the room behind the nblk partial rows (ceil(nblk / 32) rows of 2C floats)
 template <typename T>
 static void bwd_finalize(const float* part, int nblk, float* ws, int C, long M, const T* gamma, const float* invstd,
                          T* dgamma, T* dbeta, float* coef, int acc, hipStream_t st) {
+    if (merged_finalize()) {
+        const int S = fin_slices(nblk);
+        int* tk = S > 1 ? fin_tickets() : nullptr;
+        if (S == 1 || tk) {
+            if (!ws) ws = const_cast<float*>(part) + (long)nblk * 2 * C;
+            bn_bwd_finalize2_k<T><<<dim3((C + 63) / 64, S), 1024, 0, st>>>(part, nblk, fin_rps(nblk), C, M, ws, tk,
+                                                                           gamma, invstd, dgamma, dbeta, coef, acc);
+            return;
+        }
+    }
     int nrows = nblk;
     const float* fin = collapse_partials(part, nrows, 2 * C, st, ws);
     bn_bwd_finalize_k<T><<<(C + 63) / 64, 1024, 0, st>>>(fin, nrows, C, M, gamma, invstd, dgamma, dbeta, coef, acc);
@@ -1189,6 +1445,21 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
         default: return -1;
     }
 #undef LNB_ADD
+    if (merged_finalize()) {
+        // one launch: 128-row slices + last-arriver combine (ws: the room behind the partial rows)
+        const int S = fin_slices(nblk);
+        int* tk = S > 1 ? fin_tickets() : nullptr;
+        if (S == 1 || tk) {
+            const int nv = dxsum ? 3 : 2;
+            float* ws = part + (long)nblk * nv * H;
+            const dim3 grid((H + 63) / 64, S);
+            if (dxsum) ln_colsum_k<T, 3><<<grid, 1024, 0, st>>>(part, nblk, fin_rps(nblk), H, ws, tk, dg, db, acc, dxsum,
+                                                               dxsink);
+            else ln_colsum_k<T, 2><<<grid, 1024, 0, st>>>(part, nblk, fin_rps(nblk), H, ws, tk, dg, db, acc, nullptr,
+                                                         nullptr);
+            return 0;
+        }
+    }
     int nrows = nblk;
     const float* fin = collapse_partials(part, nrows, (dxsum ? 3 : 2) * H, st);
     colsum_partials_k<T><<<(H + 63) / 64, 1024, 0, st>>>(fin, nrows, H, dg, db, acc, dxsum, dxsink);
@@ -1342,6 +1613,13 @@ DDL_API int ddl_bn_bwd_from_partials(int dtype, const float* part, int nrows, fl
                                      const void* gamma, long M, int C, void* dgamma, void* dbeta, float* coef, void* dx,
                                      void* dres, int acc_params, hipStream_t st) {
     if (!rows_ok(C) || dtype != 1) return -1;
+    if (merged_finalize() && (fin_slices(nrows) == 1 || (ws && ws_elems >= (long)fin_slices(nrows) * 2 * C))) {
+        bwd_finalize<bf16_t>(part, nrows, fin_slices(nrows) == 1 ? nullptr : ws, C, M, (const bf16_t*)gamma, invstd,
+                             (bf16_t*)dgamma, (bf16_t*)dbeta, coef, acc_params, st);
+        bn_bwd_apply_only((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, M, C, 0, coef, (bf16_t*)dx,
+                          (bf16_t*)dres, st);
+        DDL_RETURN_LAUNCH();
+    }
     const long need = ddl_bn_partials_ws(nrows, C);
     if (need > 0 && (!ws || ws_elems < need)) return -2;
     if (need > 0) {

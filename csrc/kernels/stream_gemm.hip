@@ -1,0 +1,396 @@
+// Streaming NT GEMM with the weight operand resident in REGISTERS, for the memory-bound 1x1
+// convolutions of ResNet stage 2 (and any (N, K) with N * K <= 64 Ki elements):
+//   C[M, N] = A[M, K] . B[N, K]^T,  (N, K) = (512, 128) or (128, 512), bf16, fp32 accumulate,
+// with the epilogues those convolutions need: BatchNorm statistics of the output (forward), the
+// BatchNorm-backward reduction of the next layer (dgrad, EPI_BNB), that plus the block-input
+// residual (EPI_RESBNB).
+//
+// Why a kernel of its own: these GEMMs move ~10x more bytes than their MFMA time (200704 x 512 x
+// 128: 4 MFLOP against ~100 KB of HBM traffic per 32-row tile), and the general 128-row kernels --
+// B restaged for every tile, epilogue operands loaded after the MFMAs, no overlap of one tile's
+// stores with the next tile's loads -- ran them at 2.5-3.1 TB/s (profiles/gemm_trace_r50.md).  The
+// stage-1 streaming kernel (skinny_gemm.hip) keeps B in LDS, which at stage 2 (128 KB of B) no
+// longer leaves room for the double-buffered tiles.  Here:
+//   * 8 wave64 (two per SIMD) each own N/8 output columns; a wave's B fragments for ALL of K
+//     (N/8 x K bf16 = 64 VGPRs) are loaded once per workgroup and stay in registers, so LDS holds
+//     only the streamed images;
+//   * a persistent workgroup walks a contiguous chunk of 32-row tiles; everything the NEXT tile
+//     reads -- its A rows, its epilogue operand (residual or BatchNorm input) and its ReLU-mask
+//     bytes -- is in flight by LDS-DMA into the other half of double-buffered images while the
+//     current tile computes (the RESBNB BatchNorm input rides in registers, a tile ahead);
+//   * the epilogue writes the bf16 result into the tile's C image (in place over its operand)
+//     and the tile leaves as whole rows, 1 KB of contiguous bytes per store instruction;
+//   * every wave issues a fixed number of DMA and store instructions per tile, so "the next tile
+//     landed" is a counted vmcnt that never waits out the stores;
+//   * BatchNorm sums accumulate in registers over all of a workgroup's tiles; a wave owns whole
+//     columns, so each workgroup writes one partial row with no cross-wave reduction.
+// Reference behaviour: torchvision Bottleneck 1x1 convolutions under cuDNN.
+#include "ddl_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int NW = 8, NTH = NW * 64;
+enum Epi { EPI_PLAIN = 0, EPI_BNB = 2, EPI_RESBNB = 3 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct StParams {
+    const bf16_t* A;
+    const bf16_t* B;
+    bf16_t* C;
+    long M;
+    int tiles, chunk;
+    float* colstats;       // [gridDim.x][2][N] or null
+    const bf16_t* res;     // EPI_RESBNB
+    const bf16_t* aux;     // EPI_BNB / EPI_RESBNB: BatchNorm input (same layout as C)
+    const uint8_t* mask;   // ReLU bit mask of the BatchNorm output (null: all kept)
+    const float* mean;
+    const float* istd;
+    uint32_t c_bytes;
+};
+
+__device__ __forceinline__ void glds(const void* g, char* dst, int bytes) {
+    if (bytes == 16) __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 4, 0, 0);
+}
+__device__ __forceinline__ bf16x8 ds_read16(uint32_t addr) {
+    bf16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+__device__ __forceinline__ uint2 ds_read8(uint32_t addr) {
+    uint2 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+__device__ __forceinline__ uint32_t ds_read32(uint32_t addr) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+__device__ __forceinline__ void ds_write8(uint32_t addr, uint2 v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// swizzled [rows][W] bf16 image: 16-byte chunk c of row r sits at chunk c ^ (r & swm): the 16
+// rows a ds_read_b128 lane group touches land on 16 distinct 16-byte slots of the bank row
+template <int W>
+constexpr int swm() { return W / 8 >= 16 ? 15 : W / 8 - 1; }
+
+// NROWS rows of a [rows][W] bf16 matrix into a swizzled LDS image by LDS-DMA: a fixed
+// (compile-time) number of 1 KB instructions per wave, so the waits can count them
+template <int W, int NROWS>
+__device__ __forceinline__ void dma_rows(const bf16_t* src, long row0, long rows_valid, char* dst, int wv, int lane) {
+    constexpr int CPR = W / 8;                    // 16-byte chunks per row
+    constexpr int RPI = CPR >= 64 ? 1 : 64 / CPR; // rows per 1 KB wave instruction
+    constexpr int IPR = CPR >= 64 ? CPR / 64 : 1; // instructions per row (W > 512)
+    constexpr int NINST = NROWS * IPR / RPI;
+    static_assert(NINST % NW == 0, "instructions split evenly over the waves");
+#pragma unroll
+    for (int qq = 0; qq < NINST / NW; ++qq) {
+        const int q = qq * NW + wv;
+        const int r = (q / IPR) * RPI + (CPR >= 64 ? 0 : lane / CPR);
+        const int cl = CPR >= 64 ? (q % IPR) * 64 + lane : lane % CPR;
+        const int c = cl ^ (r & swm<W>());
+        const long gr = min(row0 + r, rows_valid - 1);   // rows past the end: any valid row
+        glds(src + gr * W + c * 8, dst + q * 1024, 16);
+    }
+}
+
+template <int N, int K, int TM, int EPI>
+__global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
+    constexpr bool BNB = EPI == EPI_BNB || EPI == EPI_RESBNB;
+    constexpr int CW = N / NW;                    // columns per wave
+    constexpr int NCF = CW / 16;                  // 16-column fragments per wave
+    constexpr int KK = K / 32;                    // 32-deep k-steps
+    constexpr int TI = TM / 16;                   // 16-row fragments per tile
+    static_assert(NCF >= 1 && CW % 16 == 0 && TM % 16 == 0, "shape");
+    constexpr int ABYTES = TM * K * 2, CBYTES = TM * N * 2;
+    constexpr int NCIMG = EPI == EPI_PLAIN ? 1 : 2;
+    constexpr int MBYTES = TM * N / 8;            // mask bytes per tile
+    constexpr int MINST = BNB ? (MBYTES + 255) / 256 : 0;   // 4-byte-per-lane DMA instructions
+    constexpr int MS = MINST * 256 > 1024 ? MINST * 256 : 1024;
+    constexpr int OFF_A = 0, OFF_C = 2 * ABYTES, OFF_M = OFF_C + NCIMG * CBYTES;
+    constexpr int LDS = OFF_M + (BNB ? 2 * MS : 0);
+    static_assert(LDS <= 160 * 1024, "LDS");
+    constexpr int SPW = CBYTES / 1024 / NW;       // whole-row store instructions per wave per tile
+    static_assert(SPW >= 1 && CBYTES % (1024 * NW) == 0, "stores split evenly over the waves");
+    __shared__ __attribute__((aligned(16))) char smem[LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, r16 = lane & 15;
+    const int cb = wv * CW;                       // this wave's first column
+    const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+    const __amdgpu_buffer_rsrc_t crs = rsrc(p.C, p.c_bytes);
+    const bf16_t* eop = EPI == EPI_RESBNB ? p.res : p.aux;
+
+    const int t0 = blockIdx.x * p.chunk, t1 = min(p.tiles, t0 + p.chunk);
+    auto prefetch = [&](int t, int buf) {
+        dma_rows<K, TM>(p.A, (long)t * TM, p.M, smem + OFF_A + buf * ABYTES, wv, lane);
+        if constexpr (EPI != EPI_PLAIN) dma_rows<N, TM>(eop, (long)t * TM, p.M, smem + OFF_C + buf * CBYTES, wv, lane);
+        if constexpr (BNB) {
+            // TM x N/8 mask bytes as 4-byte-per-lane DMA instructions; every wave issues the
+            // same ones (identical data), so each wave's count is the same
+            const long byte0 = (long)t * MBYTES, last = p.M * (N / 8) - 4;
+#pragma unroll
+            for (int k = 0; k < MINST; ++k) {
+                const long b = min(byte0 + (long)(k * 64 + lane) * 4, last);
+                const uint8_t* src = p.mask ? p.mask + b : (const uint8_t*)p.A;
+                glds(src, smem + OFF_M + buf * MS + k * 256, 4);
+            }
+        }
+    };
+    // EPI_RESBNB: this lane's BN-input values (rows 16 i + r16, columns cb + 16 j + 4 g ..+3) of
+    // tile t, one tile ahead in registers (two sets alternating per tile; see skinny_gemm.hip)
+    uint2 xa[TI][NCF], xb[TI][NCF];
+    auto prefetch_x = [&](int t, uint2 (&dst)[TI][NCF]) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const long row = min((long)t * TM + 16 * i + r16, p.M - 1);
+#pragma unroll
+            for (int j = 0; j < NCF; ++j)
+                dst[i][j] = *reinterpret_cast<const uint2*>(p.aux + row * N + cb + 16 * j + 4 * g);
+        }
+    };
+    // the wave's B fragments for the whole reduction: lane holds B[cb + 16 j + r16][32 kk + 8 g .. +7]
+    bf16x8 breg[NCF][KK];
+#pragma unroll
+    for (int j = 0; j < NCF; ++j)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+            breg[j][kk] = *reinterpret_cast<const bf16x8*>(p.B + (long)(cb + 16 * j + r16) * K + 32 * kk + 8 * g);
+    if (t0 < t1) {
+        prefetch(t0, 0);
+        if constexpr (EPI == EPI_RESBNB) prefetch_x(t0, xa);
+    }
+
+    // A fragment offsets in the tile image (kernel constants)
+    uint32_t aoff[TI][KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const int r = 16 * i + r16;
+            aoff[i][kk] = r * (K * 2) + (((kk * 4 + g) ^ (r & swm<K>())) << 4);
+        }
+    // C-tile image offset of this lane's 4 columns in row 16 i + r16, column block j
+    auto coff = [&](int i, int j) -> uint32_t {
+        const int row = 16 * i + r16, c = (cb + 16 * j) / 8 + (g >> 1);
+        return row * (N * 2) + ((c ^ (row & swm<N>())) << 4) + (g & 1) * 8;
+    };
+
+    float st_s[NCF][4], st_q[NCF][4];
+#pragma unroll
+    for (int j = 0; j < NCF; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st_s[j][e] = st_q[j][e] = 0.f;
+
+    auto tile = [&](const int t, uint2 (&xc)[TI][NCF], uint2 (&xn)[TI][NCF]) __attribute__((always_inline)) {
+        const int buf = (t - t0) & 1;
+        // the previous tile's stores (SPW per wave) may stay in flight; everything older -- this
+        // tile's DMA (and register prefetch) issued at the previous tile's top -- has landed
+        if constexpr (EPI == EPI_RESBNB) __builtin_amdgcn_s_waitcnt(0xF70 | SPW);   // vmcnt(SPW), compiler-visible
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW) : "memory");
+        __builtin_amdgcn_s_barrier();
+        // the next tile's loads (none after the last tile: LDS-DMA still landing when the
+        // workgroup exits would write into the LDS of the next workgroup on this CU)
+        if (t + 1 < t1) prefetch(t + 1, buf ^ 1);
+        // unconditional (a clamped row past the last tile): the same number of loads on every
+        // path lets the compiler's wait before the first use of xc leave these in flight
+        if constexpr (EPI == EPI_RESBNB) prefetch_x(t + 1, xn);
+
+        const uint32_t abase = lds0 + OFF_A + buf * ABYTES;
+        f32x4 acc[TI][NCF];
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < NCF; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+            bf16x8 af[TI];
+#pragma unroll
+            for (int i = 0; i < TI; ++i) af[i] = ds_read16(abase + aoff[i][kk]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < NCF; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(breg[j][kk], af[i], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+
+        // ---- epilogue: lane holds C[m0 + 16 i + r16][cb + 16 j + 4 g .. + 3]
+        const long m0 = (long)t * TM;
+        const uint32_t cimg = lds0 + OFF_C + (EPI == EPI_PLAIN ? 0 : buf * CBYTES);
+        // mask bits of this lane's row: columns cb + 16 j + 4 g .. +3 are bits of byte
+        // (cb + 16 j) / 8 + (g >> 1), nibble g & 1
+        // (raw words: nothing may touch an asm ds_read's result before the lgkmcnt wait below)
+        uint32_t mraw[TI][NCF];
+        if constexpr (BNB) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i) {
+                const uint32_t rowm = lds0 + OFF_M + buf * MS + (16 * i + r16) * (N / 8) + cb / 8;
+#pragma unroll
+                for (int j = 0; j < NCF; ++j)   // fragment j's 16 columns = 2 mask bytes at rowm + 2 j
+                    mraw[i][j] = p.mask ? ds_read32((rowm + 2 * j) & ~3u) : ~0u;
+            }
+        }
+        uint2 ev[TI][NCF];
+        if constexpr (EPI != EPI_PLAIN) {
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < NCF; ++j) ev[i][j] = ds_read8(cimg + coff(i, j));
+        }
+        // the asm reads are invisible to the compiler's waits: nothing may use their
+        // results above this wait (sched_barrier: ALU would otherwise move up)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+            const bool ok = m0 + 16 * i + r16 < p.M;
+#pragma unroll
+            for (int j = 0; j < NCF; ++j) {
+                float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                float xv[4] = {0.f, 0.f, 0.f, 0.f};
+                if constexpr (EPI != EPI_PLAIN) {
+                    xv[0] = __uint_as_float(ev[i][j].x << 16);
+                    xv[1] = __uint_as_float(ev[i][j].x & 0xffff0000u);
+                    xv[2] = __uint_as_float(ev[i][j].y << 16);
+                    xv[3] = __uint_as_float(ev[i][j].y & 0xffff0000u);
+                }
+                if constexpr (EPI == EPI_RESBNB) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += xv[e];      // + residual
+                    xv[0] = __uint_as_float(xc[i][j].x << 16);      // the BN input for the statistics
+                    xv[1] = __uint_as_float(xc[i][j].x & 0xffff0000u);
+                    xv[2] = __uint_as_float(xc[i][j].y << 16);
+                    xv[3] = __uint_as_float(xc[i][j].y & 0xffff0000u);
+                }
+                if constexpr (BNB) {
+                    // bytes (rowm + 2 j), +1 sit at bits 0-15 or 16-31 of the word; columns 4 g .. +3
+                    const uint32_t bits = mraw[i][j] >> (((cb / 8 + 2 * j) & 2) * 8 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = ((bits >> e) & 1u) ? v[e] : 0.f;
+                }
+                const uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+                ds_write8(cimg + coff(i, j), make_uint2(lo, hi));
+                if (ok) {
+                    const float tq[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                         __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        st_s[j][e] += tq[e];
+                        st_q[j][e] += BNB ? tq[e] * xv[e] : tq[e] * tq[e];
+                    }
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // whole-row stores: each instruction writes 1 KB of contiguous bytes
+        constexpr int CPR = N * 2 / 16;                        // 16-byte chunks per row
+        constexpr int RPI = CPR >= 64 ? 1 : 64 / CPR;
+        constexpr int IPR = CPR >= 64 ? CPR / 64 : 1;
+#pragma unroll
+        for (int qq = 0; qq < SPW; ++qq) {
+            const int q = qq * NW + wv;
+            const int row = (q / IPR) * RPI + (CPR >= 64 ? 0 : lane / CPR);
+            const int c = CPR >= 64 ? (q % IPR) * 64 + lane : lane % CPR;
+            const u32x4 d = __builtin_bit_cast(u32x4, ds_read16(cimg + row * (N * 2) + ((c ^ (row & swm<N>())) << 4)));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            const long grow = m0 + row;
+            const uint32_t off = grow < p.M ? (uint32_t)((grow * N + c * 8) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(d, crs, (int)off, 0, 0);
+        }
+    };
+    // B, the first tile's operands (and BN input): vmcnt(0), visible to the compiler's own
+    // wait tracking (the register B fragments must not look outstanding inside the loop)
+    __builtin_amdgcn_s_waitcnt(0xF70);
+    if constexpr (EPI == EPI_RESBNB) {
+        for (int t = t0; t < t1; t += 2) {
+            tile(t, xa, xb);
+            if (t + 1 < t1) tile(t + 1, xb, xa);
+        }
+    } else {
+        for (int t = t0; t < t1; ++t) tile(t, xa, xb);
+    }
+
+    if (p.colstats) {
+        // a wave owns its columns: lanes r16 == 0 hold the column sums after the row reduction
+#pragma unroll
+        for (int j = 0; j < NCF; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float a = row16_sum(st_s[j][e]), b = row16_sum(st_q[j][e]);
+                const int col = cb + 16 * j + 4 * g + e;
+                if constexpr (BNB) b = (b - p.mean[col] * a) * p.istd[col];   // sum dz * xhat
+                if (r16 == 0) {
+                    p.colstats[(long)blockIdx.x * 2 * N + col] = a;
+                    p.colstats[(long)blockIdx.x * 2 * N + N + col] = b;
+                }
+            }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int N, int K, int TM, int EPI>
+int launch(const StParams& p0, int grid, hipStream_t st) {
+    StParams p = p0;
+    int g = grid > 0 ? grid : 256;                // one workgroup per CU (LDS + 8 waves)
+    p.tiles = (int)((p.M + TM - 1) / TM);
+    g = std::min(g, p.tiles);
+    p.chunk = (p.tiles + g - 1) / g;
+    g = (p.tiles + p.chunk - 1) / p.chunk;
+    hipLaunchKernelGGL((stream_gemm_k<N, K, TM, EPI>), dim3(g), dim3(NTH), 0, st, p);
+    return g;
+}
+
+}  // namespace
+
+// C[M, N] = A[M, K] B[N, K]^T for (N, K) = (512, 128) or (128, 512), bf16, row-major contiguous.
+// Epilogue: aux (the BatchNorm input, same layout as C) -> the BatchNorm backward: C = (acc [+ res])
+// * relu_mask, colstats rows [sum C | sum C * (aux - mean) * istd] (res only for N = 512);
+// otherwise colstats (nullable) rows [sum C | sum C^2].  Returns the number of statistics rows
+// written (0 without colstats), -1 when not covered (nothing launched), -2 - hipError.
+DDL_API int ddl_stream_gemm(const void* A, const void* B, void* C, long M, int N, int K, float* colstats,
+                            const void* res, const void* aux, const uint8_t* mask, const float* mean,
+                            const float* istd, int grid, hipStream_t stream) {
+    if (M < 1 || M * (long)N * 2 >= (1l << 31)) return -1;
+    const bool w512 = N == 512 && K == 128, w128 = N == 128 && K == 512;
+    if (!w512 && !w128) return -1;
+    if (res && !aux) return -1;
+    if (aux && (!mean || !istd)) return -1;
+    StParams p{};
+    p.A = (const bf16_t*)A;
+    p.B = (const bf16_t*)B;
+    p.C = (bf16_t*)C;
+    p.M = M;
+    p.colstats = colstats;
+    p.res = (const bf16_t*)res;
+    p.aux = (const bf16_t*)aux;
+    p.mask = mask;
+    p.mean = mean;
+    p.istd = istd;
+    p.c_bytes = (uint32_t)(M * N * 2);
+    int g;
+    if (w512) {
+        if (res) g = launch<512, 128, 32, EPI_RESBNB>(p, grid, stream);
+        else if (aux) g = launch<512, 128, 32, EPI_BNB>(p, grid, stream);
+        else g = launch<512, 128, 64, EPI_PLAIN>(p, grid, stream);
+    } else {
+        if (res) return -1;
+        if (aux) g = launch<128, 512, 32, EPI_BNB>(p, grid, stream);
+        else g = launch<128, 512, 64, EPI_PLAIN>(p, grid, stream);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return -2 - (int)e;
+    return colstats ? g : 0;
+}

@@ -76,15 +76,51 @@ _SKINNY = os.environ.get("DDL_SKINNY", "1") != "0"
 _SKINNY_RESBNB = os.environ.get("DDL_SKINNY_RESBNB", "1") != "0"
 
 
+_STREAM = os.environ.get("DDL_STREAM_GEMM", "1") != "0"
+
+
+def _stream(a, b, c, part=None, res=None, bnb=None):
+    """c[M, N] = a[M, K] b[N, K]^T by the register-B streaming kernel (csrc/kernels/stream_gemm.hip)
+    when it covers the shape -- ResNet stage 2: (N, K) = (512, 128) or (128, 512), bf16, contiguous;
+    a residual only together with the BN-backward epilogue (N = 512).  Returns the statistics rows
+    written, or None when not covered (nothing launched)."""
+    if not (_STREAM and a.is_cuda):
+        return None
+    M, K = a.shape
+    N = b.shape[0]
+    if (N, K) not in ((512, 128), (128, 512)) or tuple(c.shape) != (M, N) or b.shape[1] != K:
+        return None
+    ts = [a, b, c] + ([res] if res is not None else []) + ([bnb.x] if bnb is not None else [])
+    if any(t.dtype != torch.bfloat16 or not t.is_contiguous() for t in ts):
+        return None
+    if res is not None and (bnb is None or N != 512 or tuple(res.shape) != (M, N)):
+        return None
+    if bnb is not None and bnb.x.numel() != M * N:
+        return None
+    if part is not None and part.numel() < 256 * 2 * N:
+        return None
+    args = (_lib.p(bnb.x), _lib.p(bnb.mask), _lib.p(bnb.mean), _lib.p(bnb.istd)) if bnb is not None else (0, 0, 0, 0)
+    rc = _lib.fn("ddl_stream_gemm")(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, _lib.p(part), _lib.p(res),
+                                    *args, 0, _lib.stream())
+    if rc == -1:
+        return None
+    if rc < 0:
+        raise RuntimeError(f"ddl_stream_gemm failed: {rc}")
+    return rc
+
+
 def _skinny(a, b, c, part=None, res=None, bnb=None):
     """c[M, N] = a[M, K] b[N, K]^T by the streaming kernel (csrc/kernels/skinny_gemm.hip) when
     it covers the shape -- (N, K) = (256, 64) or (64, 256), bf16, contiguous, residual only
     for N = 256, BN-backward epilogue for N = 64, or for N = 256 together with the residual.
+    Stage-2 shapes go to the register-B kernel (``_stream``).
     Returns the statistics rows written, or None when not covered (nothing launched)."""
     if not (_SKINNY and a.is_cuda):
         return None
     M, K = a.shape
     N = b.shape[0]
+    if (N, K) in ((512, 128), (128, 512)):
+        return _stream(a, b, c, part, res, bnb)
     if (N, K) not in ((256, 64), (64, 256)) or tuple(c.shape) != (M, N) or b.shape[1] != K:
         return None
     ts = [a, b, c] + ([res] if res is not None else []) + ([bnb.x] if bnb is not None else [])

@@ -191,10 +191,12 @@ def test_stem_bn_relu_maxpool(shape, fused_bwd, monkeypatch):
     torch.testing.assert_close(res[0][5], res[1][5])
 
 
-@pytest.mark.parametrize("nblk,C", [(300, 64), (3000, 512), (1057, 2048)])
+@pytest.mark.parametrize("nblk,C", [(300, 64), (3000, 512), (1057, 2048), (128, 256), (129, 64), (20000, 64)])
 def test_bn_finalize_from_many_partial_rows(nblk, C):
-    """Many GEMM-epilogue partial rows (collapsed 32:1, then finalized) -> BatchNorm
-    forward statistics and backward coefficients, against fp64 sums of the same rows."""
+    """Many GEMM-epilogue partial rows -> BatchNorm forward statistics and backward coefficients
+    (the merged multi-workgroup finalize: 128-row slices + last-arriver combine; 129 rows = a
+    one-row last slice, 20000 = more rows than 128 slices of 128), against fp64 sums of the same
+    rows, and bit-identical over repeated launches (fixed summation order, tickets re-armed)."""
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd.ops._lib import call, p
     torch.manual_seed(5)
@@ -205,6 +207,7 @@ def test_bn_finalize_from_many_partial_rows(nblk, C):
     gamma = (torch.rand(C, device=dev) + 0.5).bfloat16()
     beta = torch.randn(C, device=dev).bfloat16()
     s, q = part.double().sum(0)[:C], part.double().sum(0)[C:]
+    first = None
     for rep in range(3):
         rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
         st = torch.empty(4, C, device=dev)
@@ -215,6 +218,9 @@ def test_bn_finalize_from_many_partial_rows(nblk, C):
         torch.testing.assert_close(st[0].double(), mean, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(st[1].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(rm.double(), 0.1 * mean, rtol=1e-5, atol=1e-6)
+        if first is None:
+            first = st.clone()
+        assert torch.equal(st, first), "finalize not deterministic across launches"
     # backward: coefficients (k1, mean dz, mean dz*xhat) and dgamma / dbeta from the same rows
     x = torch.randn(M, C, device=dev).bfloat16()
     dz = torch.randn(M, C, device=dev).bfloat16()
