@@ -1014,9 +1014,17 @@ __global__ __launch_bounds__(1024) void ln_colsum_k(const float* __restrict__ pa
 // the slice rows stays one round trip of 16 row lanes x 8 (ws holds S x 2C floats)
 static int fin_slices(int nblk) { return std::max(1, std::min(128, (nblk + FIN_RPS - 1) / FIN_RPS)); }
 static int fin_rps(int nblk) { return (nblk + fin_slices(nblk) - 1) / fin_slices(nblk); }
-static bool merged_finalize() {
-    static const bool on = [] { const char* e = getenv("DDL_BN_MERGED_FIN"); return !(e && e[0] == '0'); }();
-    return on;
+// Measured in-model (profiles/kernels_r50.md, round 5): the merged launch takes 7.6-8.3 us -- its
+// two agent-scope fences cost about what the saved round trips gain -- so it replaces only the
+// TWO launches of the collapse path (> COLLAPSE_OVER rows: 5 + 6.7 us); up to that the single
+// finalize workgroup reads every row itself.  DDL_BN_MERGED_FIN=0: never, =2: always (A/B).
+static int merged_mode() {
+    static const int m = [] { const char* e = getenv("DDL_BN_MERGED_FIN"); return e ? atoi(e) : 1; }();
+    return m;
+}
+static bool merged_finalize(int nblk) {
+    const int m = merged_mode();
+    return m == 2 || (m == 1 && nblk > 512);
 }
 
 // Partial rows beyond this are first collapsed 32:1 (a single finalize block per
@@ -1050,7 +1058,7 @@ DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, lon
                                      const void* beta, float* running_mean, float* running_var, float momentum,
                                      float eps, float* save_mean, float* save_invstd, float* scale, float* shift,
                                      float* ws, long ws_elems, hipStream_t st) {
-    if (merged_finalize()) {
+    if (merged_finalize(nblk)) {
         const int S = fin_slices(nblk);
         int* tk = S > 1 ? fin_tickets() : nullptr;
         if (S == 1 || (tk && ws && ws_elems >= (long)S * 2 * C)) {
@@ -1146,7 +1154,7 @@ DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float*
 template <typename T>
 static void bwd_finalize(const float* part, int nblk, float* ws, int C, long M, const T* gamma, const float* invstd,
                          T* dgamma, T* dbeta, float* coef, int acc, hipStream_t st) {
-    if (merged_finalize()) {
+    if (merged_finalize(nblk)) {
         const int S = fin_slices(nblk);
         int* tk = S > 1 ? fin_tickets() : nullptr;
         if (S == 1 || tk) {
@@ -1445,7 +1453,7 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
         default: return -1;
     }
 #undef LNB_ADD
-    if (merged_finalize()) {
+    if (merged_finalize(nblk)) {
         // one launch: 128-row slices + last-arriver combine (ws: the room behind the partial rows)
         const int S = fin_slices(nblk);
         int* tk = S > 1 ? fin_tickets() : nullptr;
@@ -1613,7 +1621,7 @@ DDL_API int ddl_bn_bwd_from_partials(int dtype, const float* part, int nrows, fl
                                      const void* gamma, long M, int C, void* dgamma, void* dbeta, float* coef, void* dx,
                                      void* dres, int acc_params, hipStream_t st) {
     if (!rows_ok(C) || dtype != 1) return -1;
-    if (merged_finalize() && (fin_slices(nrows) == 1 || (ws && ws_elems >= (long)fin_slices(nrows) * 2 * C))) {
+    if (merged_finalize(nrows) && (fin_slices(nrows) == 1 || (ws && ws_elems >= (long)fin_slices(nrows) * 2 * C))) {
         bwd_finalize<bf16_t>(part, nrows, fin_slices(nrows) == 1 ? nullptr : ws, C, M, (const bf16_t*)gamma, invstd,
                              (bf16_t*)dgamma, (bf16_t*)dbeta, coef, acc_params, st);
         bn_bwd_apply_only((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, M, C, 0, coef, (bf16_t*)dx,

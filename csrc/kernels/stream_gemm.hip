@@ -394,3 +394,245 @@ DDL_API int ddl_stream_gemm(const void* A, const void* B, void* C, long M, int N
     if (e != hipSuccess) return -2 - (int)e;
     return colstats ? g : 0;
 }
+
+// ====================================================================== streaming weight gradient
+// C[M, N] (+)= A^T B with A = [K][M], B = [K][N] (k-outer: the TN weight gradient dW = dY^T X of a
+// 1x1 convolution, K = pixels) for the memory-bound ResNet shapes M, N in {64 .. 512}, M * N <=
+// 64 Ki.  The general kernels tile the OUTPUT (128 x 64 / 256 x 128) and split K, so every operand
+// row is streamed once per output tile it feeds and the split-K slabs are wide: they ran these at
+// 1.8-2.6 TB/s (tuner timings in bench.py's log).  Here each workgroup (8 waves, one per CU) owns
+// the WHOLE M x N output over a contiguous range of K rows:
+//   * A and B rows stream through an LDS ring of 32-row slots by LDS-DMA, R - 1 slots in flight
+//     (~100 KB per CU), in the swizzled k-outer image of gemm_big.hip (128-column panels of
+//     256-byte rows, read by ds_read_b64_tr_b16);
+//   * every operand byte is read once; the only extra traffic is one bf16 partial of M x N per
+//     workgroup (32 MB at 512 x 128 against 256 MB of operands), summed by wgrad_reduce_k.
+namespace {
+
+constexpr int WS_ROWS = 32;                      // K rows per ring slot
+constexpr int PANEL = WS_ROWS * 256;             // one 128-column panel of a slot: 8 KB
+
+__device__ __forceinline__ int swz_ko2(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+typedef __attribute__((address_space(3))) s16x4 lds_s4;
+__device__ __forceinline__ s16x4 ds_read_tr4(lds_s4* __restrict__ p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+}
+
+// 16 columns (rbase .. +15 of a panel) x 32 k-rows as an MFMA operand fragment: lane holds column
+// rbase + (lane & 15), k = 8 (lane >> 4) .. +7 (two transposed reads of 4 rows each)
+__device__ __forceinline__ bf16x8 frag_ko(const char* panel, int rbase, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+    const int col = rbase + 4 * pq, chunk = col >> 3;
+    const int ra = 8 * g + q, rb = ra + 4;
+    const s16x4 lo = ds_read_tr4((lds_s4*)(panel + ra * 256 + ((chunk ^ swz_ko2(ra)) << 4) + (pq & 1) * 8));
+    const s16x4 hi = ds_read_tr4((lds_s4*)(panel + rb * 256 + ((chunk ^ swz_ko2(rb)) << 4) + (pq & 1) * 8));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+struct WgParams {
+    const bf16_t* A;     // [K][lda]
+    const bf16_t* B;     // [K][ldb]
+    long lda, ldb;
+    long K;
+    int rows_per_blk;    // multiple of WS_ROWS
+    bf16_t* part;        // [gridDim.x][M][N]
+    const bf16_t* zero;  // >= 16 zero bytes
+};
+
+// wave grid: WM waves along M x (8 / WM) along N, picked to minimise fragment reads per MFMA
+template <int M, int N>
+constexpr int wg_wm() {
+    int best = 1, cost = 1 << 30;
+    for (int wm = 1; wm <= 8; wm *= 2) {
+        const int wn = 8 / wm;
+        if (M % (16 * wm) || N % (16 * wn)) continue;
+        const int c = M / wm / 16 + N / wn / 16;
+        if (c < cost) { cost = c; best = wm; }
+    }
+    return best;
+}
+
+template <int M, int N>
+__global__ __launch_bounds__(512, 1) void stream_wgrad_k(WgParams p) {
+    constexpr int PA = M >= 128 ? M / 128 : 1, PB = N >= 128 ? N / 128 : 1;
+    constexpr int SLOT = (PA + PB) * PANEL;
+    constexpr int R = (150 * 1024) / SLOT < 8 ? (150 * 1024) / SLOT : 8;   // ring slots
+    static_assert(R >= 3, "ring");
+    constexpr int WM = wg_wm<M, N>(), WN = 8 / WM;
+    constexpr int TMW = M / WM, TNW = N / WN, FI = TMW / 16, FJ = TNW / 16;
+    constexpr int DPW = PA + PB;                 // DMA instructions per wave per slot
+    __shared__ __attribute__((aligned(16))) char smem[R * SLOT];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = w / WN, wn = w % WN;
+    const long k0 = (long)blockIdx.x * p.rows_per_blk;
+    const long k1 = min(p.K, k0 + p.rows_per_blk);
+    const int nsteps = (int)((k1 - k0 + WS_ROWS - 1) / WS_ROWS);
+
+    // DMA of slot s <- k rows [k0 + 32 t, +32): panel instruction q (0..7) covers rows 4q .. 4q+3;
+    // wave w issues panel (w) of A then B (round-robin over the PA + PB panels x 8 instructions)
+    auto stage = [&](int t, int s) {
+        char* base = smem + s * SLOT;
+#pragma unroll
+        for (int d = 0; d < DPW; ++d) {
+            const int inst = d * 8 + w;              // 0 .. 8 (PA + PB) - 1
+            const int pnl = inst >> 3, q = inst & 7;
+            const int row = 4 * q + (lane >> 4);
+            const int c = (lane & 15) ^ swz_ko2(row);  // data chunk this lane's slot holds
+            const long k = k0 + (long)t * WS_ROWS + row;
+            const bool isA = pnl < PA;
+            const int col = (isA ? pnl : pnl - PA) * 128 + 8 * c;
+            const bool ok = k < k1 && col < (isA ? M : N);
+            const bf16_t* src = ok ? (isA ? p.A + k * p.lda + col : p.B + k * p.ldb + col) : p.zero;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + pnl * PANEL + q * 1024), 16, 0, 0);
+        }
+    };
+    f32x4 acc[FI][FJ];
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // prologue: R - 1 slots in flight
+#pragma unroll
+    for (int t = 0; t < R - 1; ++t)
+        if (t < nsteps) stage(t, t);
+    for (int t = 0; t < nsteps; ++t) {
+        // slot t landed: the younger ones (t + 1 .. t + R - 2, issued if they exist) may stay in flight
+        const int younger = min(R - 2, nsteps - 1 - t);
+        switch (younger) {
+            case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+            case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory"); break;
+            case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory"); break;
+            case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * DPW) : "memory"); break;
+            case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * DPW) : "memory"); break;
+            case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * DPW) : "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * DPW) : "memory"); break;
+        }
+        // (every wave's reads of slot t - 1 completed before this barrier: lgkmcnt(0) below)
+        __builtin_amdgcn_s_barrier();
+        if (t + R - 1 < nsteps) stage(t + R - 1, (t + R - 1) % R);
+        const char* base = smem + (t % R) * SLOT;
+        bf16x8 fa[FI], fb[FJ];
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+            const int r = wm * TMW + 16 * i;
+            fa[i] = frag_ko(base + (r >> 7) * PANEL, r & 127, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+            const int r = wn * TNW + 16 * j;
+            fb[j] = frag_ko(base + (PA + (r >> 7)) * PANEL, r & 127, lane);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < FJ; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    // lane holds C[wm TMW + 16 i + (lane & 15)][wn TNW + 16 j + 4 g .. +3]: one 8-byte bf16 store each
+    bf16_t* out = p.part + (long)blockIdx.x * M * N;
+    const int g4 = (lane >> 4) * 4, r16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+            *reinterpret_cast<uint2*>(out + (long)(wm * TMW + 16 * i + r16) * N + wn * TNW + 16 * j + g4) =
+                make_uint2(pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3]));
+}
+
+// C[m][n] (+)= sum over the G bf16 partials: 64 output quads x 4 partial lanes per workgroup
+__global__ __launch_bounds__(256) void wgrad_reduce_k(const bf16_t* __restrict__ part, int G, int M, int N,
+                                                      bf16_t* __restrict__ C, long ldc, int accumulate) {
+    __shared__ f32x4 red[256];
+    const int quad = blockIdx.x * 64 + (threadIdx.x & 63), gl = threadIdx.x >> 6;
+    const int nq = M * N / 4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (quad < nq) {
+        const bf16_t* src = part + (long)quad * 4;
+        int gg = gl;
+        for (; gg + 28 < G; gg += 32) {
+            uint2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint2*>(src + (long)(gg + 4 * u) * M * N);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s[0] += __uint_as_float(v[u].x << 16);
+                s[1] += __uint_as_float(v[u].x & 0xffff0000u);
+                s[2] += __uint_as_float(v[u].y << 16);
+                s[3] += __uint_as_float(v[u].y & 0xffff0000u);
+            }
+        }
+        for (; gg < G; gg += 4) {
+            const uint2 v = *reinterpret_cast<const uint2*>(src + (long)gg * M * N);
+            s[0] += __uint_as_float(v.x << 16);
+            s[1] += __uint_as_float(v.x & 0xffff0000u);
+            s[2] += __uint_as_float(v.y << 16);
+            s[3] += __uint_as_float(v.y & 0xffff0000u);
+        }
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (gl != 0 || quad >= nq) return;
+    const f32x4 t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    const int m = quad * 4 / N, n = quad * 4 - m * N;
+    bf16_t* dst = C + (long)m * ldc + n;
+    float o[4] = {t[0], t[1], t[2], t[3]};
+    if (accumulate) {
+        float a[4];
+        load4(dst, a);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += a[e];
+    }
+    store4(dst, o);
+}
+
+template <int M, int N>
+int launch_wgrad(const WgParams& p0, int G, bf16_t* C, long ldc, int accumulate, hipStream_t st) {
+    WgParams p = p0;
+    hipLaunchKernelGGL((stream_wgrad_k<M, N>), dim3(G), dim3(512), 0, st, p);
+    hipLaunchKernelGGL(wgrad_reduce_k, dim3((M * N / 4 + 63) / 64), dim3(256), 0, st, (const bf16_t*)p.part, G, M, N, C,
+                       ldc, accumulate);
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// TN weight gradient C[M, N] (+)= A^T B, A = [K][lda], B = [K][ldb] bf16 (lda, ldb % 8 == 0, 16-byte
+// aligned), C bf16 (ldc % 4 == 0), M, N in {64, 128, 256, 512} with M * N <= 65536.  workspace:
+// >= ddl_stream_wgrad_ws(M, N) bf16 elements (the workgroups' partials); zero: >= 16 zero bytes.
+// Returns -1 when the shape is not covered (nothing launched).
+DDL_API long ddl_stream_wgrad_ws(int M, int N) { return 256L * M * N; }
+
+DDL_API int ddl_stream_wgrad(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, long K,
+                             int accumulate, void* workspace, long ws_elems, const void* zero, int grid,
+                             hipStream_t st) {
+    auto pow2 = [](int v) { return v == 64 || v == 128 || v == 256 || v == 512; };
+    if (!pow2(M) || !pow2(N) || (long)M * N > 65536 || K < WS_ROWS || lda % 8 || ldb % 8 || ldc % 4 || lda < M ||
+        ldb < N || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || !zero)
+        return -1;
+    const int G = grid > 0 ? std::min(grid, 256) : 256;
+    if (!workspace || ws_elems < (long)G * M * N) return -2;
+    WgParams p{};
+    p.A = (const bf16_t*)A;
+    p.B = (const bf16_t*)B;
+    p.lda = lda;
+    p.ldb = ldb;
+    p.K = K;
+    const long steps = (K + WS_ROWS - 1) / WS_ROWS;
+    p.rows_per_blk = (int)((steps + G - 1) / G) * WS_ROWS;
+    p.part = (bf16_t*)workspace;
+    p.zero = (const bf16_t*)zero;
+    // blocks past the end of K (K small against the grid) write zero partials: every partial is summed
+    bf16_t* c = (bf16_t*)C;
+#define WGR(m, n) if (M == m && N == n) return launch_wgrad<m, n>(p, G, c, ldc, accumulate, st)
+    WGR(64, 64); WGR(64, 128); WGR(64, 256); WGR(64, 512);
+    WGR(128, 64); WGR(128, 128); WGR(128, 256); WGR(128, 512);
+    WGR(256, 64); WGR(256, 128); WGR(256, 256);
+    WGR(512, 64); WGR(512, 128);
+#undef WGR
+    return -1;
+}

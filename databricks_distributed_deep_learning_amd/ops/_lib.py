@@ -135,6 +135,7 @@ _SIGS = {
     "ddl_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, L, I, I, I, P],
     "ddl_skinny_gemm": [P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_stream_gemm": [P, P, P, L, I, I, P, P, P, P, P, P, I, P],
+    "ddl_stream_wgrad_ws": [I, I],
     "ddl_bn_bwd": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_ln_supported": [I],
     "ddl_ln_fwd": [I, P, P, L, P, P, P, P, P, L, I, F, U64, F, P],

@@ -16,6 +16,7 @@ _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L
                "ddl_gemm_n64": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P],
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
                "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, I, P],
+               "ddl_stream_wgrad": [P, L, P, L, P, L, I, I, L, I, P, L, P, I, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -37,7 +38,7 @@ def set_big_gemm(enabled: bool) -> None:
 
 
 _forced: Optional[str] = None
-_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg", "wg2")
+_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg", "wg2", "swg")
 # per-call device timing for diagnostics (scripts/debug/gemm_trace.py): list of
 # (signature, (kernel, splits), start event, end event) while enabled
 _trace: Optional[list] = None
@@ -160,6 +161,18 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
         A, lda, B, ldb, M, N = B, ldb, A, lda, N, M
     bias_bf16 = 1 if (bias is not None and bias.dtype == torch.bfloat16) else 0
     out_f32 = 1 if C.dtype == torch.float32 else 0
+    if kind == "swg":
+        if (mode == MODE_TN and bias is None and act is None and residual is None and colstats is None
+                and not row_remap and not out_f32 and swg_ok(M, N, K, lda, ldb) and ldc % 4 == 0
+                and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0):
+            ws = torch.empty(int(_lib.fn("ddl_stream_wgrad_ws")(M, N)), dtype=torch.bfloat16, device=C.device)
+            rc = _lib.fn("ddl_stream_wgrad")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
+                                             int(accumulate), ws.data_ptr(), ws.numel(),
+                                             _zero_page(C.device).data_ptr(), 0, _lib.stream())
+            if rc != 0:
+                raise RuntimeError(f"ddl_stream_wgrad(M={M}, N={N}, K={K}) failed: {rc}")
+            return
+        kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
     if kind in ("wg", "wg2"):
         cw = mode == MODE_CONVW and conv_arr is not None and conv_arr[3] % 8 == 0
         wide = kind == "wg2"
@@ -223,6 +236,10 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
         if _WG2 and N % 256 == 0:
             w2 = big_splits(M, N, K)
             out += [("wg2", s) for s in sorted({max(1, w2 // 2), w2, 2 * w2})]
+    if _SWG and mode == MODE_TN and plain and not row_remap and swg_ok(M, N, K, lda, ldb):
+        # streaming weight gradient (stream_gemm.hip stream_wgrad_k): every workgroup owns the whole
+        # M x N output over a range of K rows (no operand re-reads), bf16 partials + one reduce
+        out.append(("swg", 1))
     if mode in (MODE_TN, MODE_CONVW) and plain and (M <= 192 or M % 128 == 64):
         ts = pick_splits(N, 2 * M, K)     # transposed: N' = M (output channels) on 64-wide tiles
         out += [("tnarrow", s) for s in sorted({1, max(1, ts // 2), ts})]
@@ -243,6 +260,16 @@ _WG = os.environ.get("DDL_GEMM_WG", "1") != "0"   # tuner candidate "wg" (A/B: 0
 # exceed the 256-register budget and spill in the loop -- slower than both "wg" and the 256x256 kernel
 # on every BERT-base weight gradient (profiles/tn_kinds_r04_wg2.log)
 _WG2 = os.environ.get("DDL_GEMM_WG2", "0") == "1"
+
+
+_SWG = os.environ.get("DDL_GEMM_SWG", "1") != "0"   # tuner candidate "swg" (A/B: 0 = never)
+
+
+def swg_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
+    """Shapes the streaming weight-gradient kernel takes (ddl_stream_wgrad's contract): M, N in
+    {64, 128, 256, 512} with M * N <= 64 Ki (the output in registers), a long reduction."""
+    return M in (64, 128, 256, 512) and N in (64, 128, 256, 512) and M * N <= 65536 and K >= 8192 \
+        and lda % 8 == 0 and ldb % 8 == 0 and lda >= M and ldb >= N
 
 
 def wg_ok(M: int, N: int, K: int, lda: int, ldb: int, wide: bool = False) -> bool:

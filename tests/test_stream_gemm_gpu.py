@@ -82,3 +82,22 @@ def test_stream_not_covered():
     rc = _lib.fn("ddl_stream_gemm")(a.data_ptr(), w.data_ptr(), c.data_ptr(), 64, 64, 256, 0, 0, 0, 0, 0, 0, 0,
                                     _lib.stream())
     assert rc == -1
+
+
+@pytest.mark.parametrize("M,N", [(256, 64), (64, 256), (64, 64), (512, 128), (128, 512), (128, 256), (256, 256)])
+@pytest.mark.parametrize("K,accumulate", [(200704, False), (50000 + 17, True)])
+def test_stream_wgrad(M, N, K, accumulate):
+    """Streaming weight gradient C (+)= A^T B (A = [K][M] output gradient, B = [K][N] input) on the
+    register-accumulator kernel ("swg": whole M x N output per workgroup, bf16 partials + reduce),
+    against fp32; K not a multiple of the 32-row slot (the zero-page tail)."""
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    torch.manual_seed(7)
+    a = torch.randn(K, M, device="cuda").bfloat16()
+    b = torch.randn(K, N, device="cuda").bfloat16()
+    c0 = (torch.randn(M, N, device="cuda") * 100).bfloat16()
+    c = c0.clone()
+    NG.gemm(NG.MODE_TN, a, M, b, N, c, N, M, N, K, accumulate=accumulate, kernel="swg")
+    torch.cuda.synchronize()
+    ref = a.float().t() @ b.float() + (c0.float() if accumulate else 0)
+    err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
