@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Stage-2 1x1 conv GEMMs (M = 200704 = 256 x 28 x 28): the register-B streaming kernel
+"""Stage-2 / 3 1x1 conv GEMMs (M = 200704 = 256 x 28 x 28 / 50176 = 256 x 14 x 14): the register-B streaming kernel
 (csrc/kernels/stream_gemm.hip) vs the tuned general kernels, with the epilogues the ResNet-50
 step runs (statistics, BN-backward, residual + BN-backward).  Effective TB/s = the bytes the
 GEMM must move (operands, epilogue inputs, output) over its time.
@@ -29,9 +29,8 @@ def timeit(fn, iters=20):
 
 def main():
     dev = "cuda"
-    M = 200704
     f = _lib.fn("ddl_stream_gemm")
-    for N, K in ((512, 128), (128, 512)):
+    for N, K, M in ((512, 128, 200704), (128, 512, 200704), (1024, 256, 50176), (256, 1024, 50176)):
         a = torch.randn(M, K, device=dev).bfloat16()
         w = (torch.randn(N, K, device=dev) * 0.1).bfloat16()
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -41,7 +40,7 @@ def main():
         mean, istd = torch.zeros(N, device=dev), torch.ones(N, device=dev)
         part = torch.empty(max(stats_rows_max(M), 1024) * 2 * N + 64 * 2 * N, device=dev)
         cases = {"stats": dict(stats=True), "bnb": dict(bnb=True, stats=True)}
-        if N == 512:
+        if N in (512, 1024):
             cases["res,bnb"] = dict(res=True, bnb=True, stats=True)
         for name, o in cases.items():
             def st():

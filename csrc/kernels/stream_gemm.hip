@@ -83,10 +83,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 template <int W>
 constexpr int swm() { return W / 8 >= 16 ? 15 : W / 8 - 1; }
 
-// NROWS rows of a [rows][W] bf16 matrix into a swizzled LDS image by LDS-DMA: a fixed
-// (compile-time) number of 1 KB instructions per wave, so the waits can count them
-template <int W, int NROWS>
-__device__ __forceinline__ void dma_rows(const bf16_t* src, long row0, long rows_valid, char* dst, int wv, int lane) {
+// NROWS rows of W bf16 columns (row stride LD elements) into a swizzled [NROWS][W] LDS image by
+// LDS-DMA: a fixed (compile-time) number of 1 KB instructions per wave, so the waits can count them
+template <int W, int NROWS, long LD = W>
+__device__ __forceinline__ void dma_rows(const bf16_t* src, long row0, long rows_valid, char* dst, int wv, int lane,
+                                         long ld = LD) {
     constexpr int CPR = W / 8;                    // 16-byte chunks per row
     constexpr int RPI = CPR >= 64 ? 1 : 64 / CPR; // rows per 1 KB wave instruction
     constexpr int IPR = CPR >= 64 ? CPR / 64 : 1; // instructions per row (W > 512)
@@ -99,48 +100,58 @@ __device__ __forceinline__ void dma_rows(const bf16_t* src, long row0, long rows
         const int cl = CPR >= 64 ? (q % IPR) * 64 + lane : lane % CPR;
         const int c = cl ^ (r & swm<W>());
         const long gr = min(row0 + r, rows_valid - 1);   // rows past the end: any valid row
-        glds(src + gr * W + c * 8, dst + q * 1024, 16);
+        glds(src + gr * ld + c * 8, dst + q * 1024, 16);
     }
 }
 
-template <int N, int K, int TM, int EPI>
+// NT = the whole output width, NB = the column slab one workgroup owns (NT / NB slabs; the slabs of
+// one row chunk are workgroups b, b + 8, ... -- one XCD under round-robin placement, so they share
+// the chunk's A rows in its L2: speed only, never correctness)
+template <int NT, int NB, int K, int TM, int EPI>
 __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
     constexpr bool BNB = EPI == EPI_BNB || EPI == EPI_RESBNB;
-    constexpr int CW = N / NW;                    // columns per wave
+    constexpr int NSLAB = NT / NB;
+    constexpr int CW = NB / NW;                   // columns per wave
     constexpr int NCF = CW / 16;                  // 16-column fragments per wave
     constexpr int KK = K / 32;                    // 32-deep k-steps
     constexpr int TI = TM / 16;                   // 16-row fragments per tile
-    static_assert(NCF >= 1 && CW % 16 == 0 && TM % 16 == 0, "shape");
-    constexpr int ABYTES = TM * K * 2, CBYTES = TM * N * 2;
+    static_assert(NCF >= 1 && CW % 16 == 0 && TM % 16 == 0 && NT % NB == 0, "shape");
+    constexpr int ABYTES = TM * K * 2, CBYTES = TM * NB * 2;
     constexpr int NCIMG = EPI == EPI_PLAIN ? 1 : 2;
-    constexpr int MBYTES = TM * N / 8;            // mask bytes per tile
-    constexpr int MINST = BNB ? (MBYTES + 255) / 256 : 0;   // 4-byte-per-lane DMA instructions
+    constexpr int MWPR = NB / 32;                 // mask words per row of the slab
+    constexpr int MINST = BNB ? (TM * MWPR + 63) / 64 : 0;   // 4-byte-per-lane DMA instructions
     constexpr int MS = MINST * 256 > 1024 ? MINST * 256 : 1024;
     constexpr int OFF_A = 0, OFF_C = 2 * ABYTES, OFF_M = OFF_C + NCIMG * CBYTES;
     constexpr int LDS = OFF_M + (BNB ? 2 * MS : 0);
     static_assert(LDS <= 160 * 1024, "LDS");
-    constexpr int SPW = CBYTES / 1024 / NW;       // whole-row store instructions per wave per tile
+    constexpr int SPW = CBYTES / 1024 / NW;       // store instructions per wave per tile (1 KB each)
     static_assert(SPW >= 1 && CBYTES % (1024 * NW) == 0, "stores split evenly over the waves");
     __shared__ __attribute__((aligned(16))) char smem[LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
-    const int cb = wv * CW;                       // this wave's first column
+    // workgroup -> (column slab, row chunk)
+    const int slab = NSLAB > 1 ? (int)((blockIdx.x >> 3) % NSLAB) : 0;
+    const int chunk = NSLAB > 1 ? (int)((blockIdx.x & 7) + 8 * (blockIdx.x / (8 * NSLAB))) : (int)blockIdx.x;
+    const int n0 = slab * NB;                     // the slab's first output column
+    const int cl0 = wv * CW;                      // this wave's first column inside the slab
+    const int cb = n0 + cl0;                      // ... in the output
     const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
     const __amdgpu_buffer_rsrc_t crs = rsrc(p.C, p.c_bytes);
     const bf16_t* eop = EPI == EPI_RESBNB ? p.res : p.aux;
 
-    const int t0 = blockIdx.x * p.chunk, t1 = min(p.tiles, t0 + p.chunk);
+    const int t0 = chunk * p.chunk, t1 = min(p.tiles, t0 + p.chunk);
     auto prefetch = [&](int t, int buf) {
         dma_rows<K, TM>(p.A, (long)t * TM, p.M, smem + OFF_A + buf * ABYTES, wv, lane);
-        if constexpr (EPI != EPI_PLAIN) dma_rows<N, TM>(eop, (long)t * TM, p.M, smem + OFF_C + buf * CBYTES, wv, lane);
+        if constexpr (EPI != EPI_PLAIN)
+            dma_rows<NB, TM, NT>(eop + n0, (long)t * TM, p.M, smem + OFF_C + buf * CBYTES, wv, lane);
         if constexpr (BNB) {
-            // TM x N/8 mask bytes as 4-byte-per-lane DMA instructions; every wave issues the
-            // same ones (identical data), so each wave's count is the same
-            const long byte0 = (long)t * MBYTES, last = p.M * (N / 8) - 4;
+            // the slab's TM x NB/8 mask bytes as 4-byte-per-lane DMA instructions (a row's NB/8 bytes
+            // are contiguous, rows NT/8 apart); every wave issues the same ones (identical data)
 #pragma unroll
             for (int k = 0; k < MINST; ++k) {
-                const long b = min(byte0 + (long)(k * 64 + lane) * 4, last);
-                const uint8_t* src = p.mask ? p.mask + b : (const uint8_t*)p.A;
+                const int wi = k * 64 + lane, row = min(wi / MWPR, TM - 1), wc = wi % MWPR;
+                const long r = min((long)t * TM + row, p.M - 1);
+                const uint8_t* src = p.mask ? p.mask + r * (NT / 8) + n0 / 8 + 4 * wc : (const uint8_t*)p.A;
                 glds(src, smem + OFF_M + buf * MS + k * 256, 4);
             }
         }
@@ -154,7 +165,7 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
             const long row = min((long)t * TM + 16 * i + r16, p.M - 1);
 #pragma unroll
             for (int j = 0; j < NCF; ++j)
-                dst[i][j] = *reinterpret_cast<const uint2*>(p.aux + row * N + cb + 16 * j + 4 * g);
+                dst[i][j] = *reinterpret_cast<const uint2*>(p.aux + row * NT + cb + 16 * j + 4 * g);
         }
     };
     // the wave's B fragments for the whole reduction: lane holds B[cb + 16 j + r16][32 kk + 8 g .. +7]
@@ -178,10 +189,10 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
             const int r = 16 * i + r16;
             aoff[i][kk] = r * (K * 2) + (((kk * 4 + g) ^ (r & swm<K>())) << 4);
         }
-    // C-tile image offset of this lane's 4 columns in row 16 i + r16, column block j
+    // C-tile image (the slab: [TM][NB]) offset of this lane's 4 columns in row 16 i + r16, block j
     auto coff = [&](int i, int j) -> uint32_t {
-        const int row = 16 * i + r16, c = (cb + 16 * j) / 8 + (g >> 1);
-        return row * (N * 2) + ((c ^ (row & swm<N>())) << 4) + (g & 1) * 8;
+        const int row = 16 * i + r16, c = (cl0 + 16 * j) / 8 + (g >> 1);
+        return row * (NB * 2) + ((c ^ (row & swm<NB>())) << 4) + (g & 1) * 8;
     };
 
     float st_s[NCF][4], st_q[NCF][4];
@@ -228,14 +239,12 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
         // ---- epilogue: lane holds C[m0 + 16 i + r16][cb + 16 j + 4 g .. + 3]
         const long m0 = (long)t * TM;
         const uint32_t cimg = lds0 + OFF_C + (EPI == EPI_PLAIN ? 0 : buf * CBYTES);
-        // mask bits of this lane's row: columns cb + 16 j + 4 g .. +3 are bits of byte
-        // (cb + 16 j) / 8 + (g >> 1), nibble g & 1
         // (raw words: nothing may touch an asm ds_read's result before the lgkmcnt wait below)
         uint32_t mraw[TI][NCF];
         if constexpr (BNB) {
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
-                const uint32_t rowm = lds0 + OFF_M + buf * MS + (16 * i + r16) * (N / 8) + cb / 8;
+                const uint32_t rowm = lds0 + OFF_M + buf * MS + (16 * i + r16) * (NB / 8) + cl0 / 8;
 #pragma unroll
                 for (int j = 0; j < NCF; ++j)   // fragment j's 16 columns = 2 mask bytes at rowm + 2 j
                     mraw[i][j] = p.mask ? ds_read32((rowm + 2 * j) & ~3u) : ~0u;
@@ -275,7 +284,7 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
                 }
                 if constexpr (BNB) {
                     // bytes (rowm + 2 j), +1 sit at bits 0-15 or 16-31 of the word; columns 4 g .. +3
-                    const uint32_t bits = mraw[i][j] >> (((cb / 8 + 2 * j) & 2) * 8 + 4 * g);
+                    const uint32_t bits = mraw[i][j] >> (((cl0 / 8 + 2 * j) & 2) * 8 + 4 * g);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = ((bits >> e) & 1u) ? v[e] : 0.f;
                 }
@@ -294,8 +303,8 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        // whole-row stores: each instruction writes 1 KB of contiguous bytes
-        constexpr int CPR = N * 2 / 16;                        // 16-byte chunks per row
+        // stores of the slab's rows: each instruction writes 1 KB (whole slab rows, NB * 2 bytes each)
+        constexpr int CPR = NB * 2 / 16;                       // 16-byte chunks per slab row
         constexpr int RPI = CPR >= 64 ? 1 : 64 / CPR;
         constexpr int IPR = CPR >= 64 ? CPR / 64 : 1;
 #pragma unroll
@@ -303,11 +312,11 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
             const int q = qq * NW + wv;
             const int row = (q / IPR) * RPI + (CPR >= 64 ? 0 : lane / CPR);
             const int c = CPR >= 64 ? (q % IPR) * 64 + lane : lane % CPR;
-            const u32x4 d = __builtin_bit_cast(u32x4, ds_read16(cimg + row * (N * 2) + ((c ^ (row & swm<N>())) << 4)));
+            const u32x4 d = __builtin_bit_cast(u32x4, ds_read16(cimg + row * (NB * 2) + ((c ^ (row & swm<NB>())) << 4)));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             const long grow = m0 + row;
-            const uint32_t off = grow < p.M ? (uint32_t)((grow * N + c * 8) * 2) : 0x80000000u;
+            const uint32_t off = grow < p.M ? (uint32_t)((grow * NT + n0 + c * 8) * 2) : 0x80000000u;
             __builtin_amdgcn_raw_buffer_store_b128(d, crs, (int)off, 0, 0);
         }
     };
@@ -324,7 +333,8 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
     }
 
     if (p.colstats) {
-        // a wave owns its columns: lanes r16 == 0 hold the column sums after the row reduction
+        // a wave owns its columns: lanes r16 == 0 hold the column sums after the row reduction;
+        // statistics row = this workgroup's row chunk (the NSLAB slab workgroups fill its columns)
 #pragma unroll
         for (int j = 0; j < NCF; ++j)
 #pragma unroll
@@ -333,40 +343,48 @@ __global__ __launch_bounds__(NTH, 1) void stream_gemm_k(StParams p) {
                 const int col = cb + 16 * j + 4 * g + e;
                 if constexpr (BNB) b = (b - p.mean[col] * a) * p.istd[col];   // sum dz * xhat
                 if (r16 == 0) {
-                    p.colstats[(long)blockIdx.x * 2 * N + col] = a;
-                    p.colstats[(long)blockIdx.x * 2 * N + N + col] = b;
+                    p.colstats[(long)chunk * 2 * NT + col] = a;
+                    p.colstats[(long)chunk * 2 * NT + NT + col] = b;
                 }
             }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int N, int K, int TM, int EPI>
+// returns the number of statistics rows (row chunks)
+template <int NT, int NB, int K, int TM, int EPI>
 int launch(const StParams& p0, int grid, hipStream_t st) {
     StParams p = p0;
-    int g = grid > 0 ? grid : 256;                // one workgroup per CU (LDS + 8 waves)
+    constexpr int NSLAB = NT / NB;
+    // one workgroup per CU (LDS + 8 waves): 256 / NSLAB row chunks, a multiple of 8 per slab set
+    int chunks = grid > 0 ? grid : 256 / NSLAB;
     p.tiles = (int)((p.M + TM - 1) / TM);
-    g = std::min(g, p.tiles);
-    p.chunk = (p.tiles + g - 1) / g;
-    g = (p.tiles + p.chunk - 1) / p.chunk;
-    hipLaunchKernelGGL((stream_gemm_k<N, K, TM, EPI>), dim3(g), dim3(NTH), 0, st, p);
-    return g;
+    chunks = std::min(chunks, p.tiles);
+    if (NSLAB > 1) chunks = std::max(8, chunks / 8 * 8);
+    p.chunk = (p.tiles + chunks - 1) / chunks;
+    if (NSLAB == 1) chunks = (p.tiles + p.chunk - 1) / p.chunk;
+    hipLaunchKernelGGL((stream_gemm_k<NT, NB, K, TM, EPI>), dim3(chunks * NSLAB), dim3(NTH), 0, st, p);
+    return chunks;
 }
 
 }  // namespace
 
-// C[M, N] = A[M, K] B[N, K]^T for (N, K) = (512, 128) or (128, 512), bf16, row-major contiguous.
-// Epilogue: aux (the BatchNorm input, same layout as C) -> the BatchNorm backward: C = (acc [+ res])
-// * relu_mask, colstats rows [sum C | sum C * (aux - mean) * istd] (res only for N = 512);
-// otherwise colstats (nullable) rows [sum C | sum C^2].  Returns the number of statistics rows
-// written (0 without colstats), -1 when not covered (nothing launched), -2 - hipError.
+// C[M, N] = A[M, K] B[N, K]^T for (N, K) = (512, 128), (128, 512) (ResNet stage 2, B whole in
+// registers) or (1024, 256), (256, 1024) (stage 3, B in column slabs of 256 / 128 over workgroups),
+// bf16, row-major contiguous.  Epilogue: aux (the BatchNorm input, same layout as C) -> the
+// BatchNorm backward: C = (acc [+ res]) * relu_mask, colstats rows [sum C | sum C * (aux - mean) *
+// istd] (res only for the wide outputs N = 512 / 1024); otherwise colstats (nullable) rows
+// [sum C | sum C^2].  Returns the number of statistics rows written (0 without colstats; at most
+// 256), -1 when not covered (nothing launched), -2 - hipError.
 DDL_API int ddl_stream_gemm(const void* A, const void* B, void* C, long M, int N, int K, float* colstats,
                             const void* res, const void* aux, const uint8_t* mask, const float* mean,
                             const float* istd, int grid, hipStream_t stream) {
     if (M < 1 || M * (long)N * 2 >= (1l << 31)) return -1;
     const bool w512 = N == 512 && K == 128, w128 = N == 128 && K == 512;
-    if (!w512 && !w128) return -1;
+    const bool w1024 = N == 1024 && K == 256, w256 = N == 256 && K == 1024;
+    if (!w512 && !w128 && !w1024 && !w256) return -1;
     if (res && !aux) return -1;
+    if (res && (w128 || w256)) return -1;
     if (aux && (!mean || !istd)) return -1;
     StParams p{};
     p.A = (const bf16_t*)A;
@@ -382,13 +400,19 @@ DDL_API int ddl_stream_gemm(const void* A, const void* B, void* C, long M, int N
     p.c_bytes = (uint32_t)(M * N * 2);
     int g;
     if (w512) {
-        if (res) g = launch<512, 128, 32, EPI_RESBNB>(p, grid, stream);
-        else if (aux) g = launch<512, 128, 32, EPI_BNB>(p, grid, stream);
-        else g = launch<512, 128, 64, EPI_PLAIN>(p, grid, stream);
+        if (res) g = launch<512, 512, 128, 32, EPI_RESBNB>(p, grid, stream);
+        else if (aux) g = launch<512, 512, 128, 32, EPI_BNB>(p, grid, stream);
+        else g = launch<512, 512, 128, 64, EPI_PLAIN>(p, grid, stream);
+    } else if (w128) {
+        if (aux) g = launch<128, 128, 512, 32, EPI_BNB>(p, grid, stream);
+        else g = launch<128, 128, 512, 64, EPI_PLAIN>(p, grid, stream);
+    } else if (w1024) {
+        if (res) g = launch<1024, 256, 256, 32, EPI_RESBNB>(p, grid, stream);
+        else if (aux) g = launch<1024, 256, 256, 32, EPI_BNB>(p, grid, stream);
+        else g = launch<1024, 256, 256, 64, EPI_PLAIN>(p, grid, stream);
     } else {
-        if (res) return -1;
-        if (aux) g = launch<128, 512, 32, EPI_BNB>(p, grid, stream);
-        else g = launch<128, 512, 64, EPI_PLAIN>(p, grid, stream);
+        if (aux) g = launch<256, 128, 1024, 32, EPI_BNB>(p, grid, stream);
+        else g = launch<256, 128, 1024, 32, EPI_PLAIN>(p, grid, stream);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return -2 - (int)e;

@@ -77,23 +77,31 @@ _SKINNY_RESBNB = os.environ.get("DDL_SKINNY_RESBNB", "1") != "0"
 
 
 _STREAM = os.environ.get("DDL_STREAM_GEMM", "1") != "0"
+# (N, K) the streaming kernel takes: ResNet stage 2 (B whole in registers) and stage 3's wide output
+# (B in 256-column slabs over workgroups that share their A rows in one XCD's L2); DDL_STREAM_GEMM=2:
+# stage 2 only.  (256, 1024) is covered by the kernel (128-column slabs) but measured no faster than
+# the 256x256 kernel (benchmarks/stream_bench.py: 45 vs 36 us with statistics, 51 vs 52 with the
+# BN-backward epilogue: its A operand is the 103 MB side and two slabs read it twice)
+_STREAM_SHAPES = ((512, 128), (128, 512)) + (((1024, 256),) if os.environ.get("DDL_STREAM_GEMM", "1") != "2"
+                                             else ())
 
 
 def _stream(a, b, c, part=None, res=None, bnb=None):
     """c[M, N] = a[M, K] b[N, K]^T by the register-B streaming kernel (csrc/kernels/stream_gemm.hip)
-    when it covers the shape -- ResNet stage 2: (N, K) = (512, 128) or (128, 512), bf16, contiguous;
-    a residual only together with the BN-backward epilogue (N = 512).  Returns the statistics rows
+    when it covers the shape -- ResNet stage 2 / 3: (N, K) = (512, 128), (128, 512), (1024, 256),
+    (256, 1024), bf16, contiguous; a residual only together with the BN-backward epilogue (N = 512
+    / 1024).  Returns the statistics rows
     written, or None when not covered (nothing launched)."""
     if not (_STREAM and a.is_cuda):
         return None
     M, K = a.shape
     N = b.shape[0]
-    if (N, K) not in ((512, 128), (128, 512)) or tuple(c.shape) != (M, N) or b.shape[1] != K:
+    if (N, K) not in _STREAM_SHAPES or tuple(c.shape) != (M, N) or b.shape[1] != K:
         return None
     ts = [a, b, c] + ([res] if res is not None else []) + ([bnb.x] if bnb is not None else [])
     if any(t.dtype != torch.bfloat16 or not t.is_contiguous() for t in ts):
         return None
-    if res is not None and (bnb is None or N != 512 or tuple(res.shape) != (M, N)):
+    if res is not None and (bnb is None or N not in (512, 1024) or tuple(res.shape) != (M, N)):
         return None
     if bnb is not None and bnb.x.numel() != M * N:
         return None
@@ -119,7 +127,7 @@ def _skinny(a, b, c, part=None, res=None, bnb=None):
         return None
     M, K = a.shape
     N = b.shape[0]
-    if (N, K) in ((512, 128), (128, 512)):
+    if (N, K) in _STREAM_SHAPES:
         return _stream(a, b, c, part, res, bnb)
     if (N, K) not in ((256, 64), (64, 256)) or tuple(c.shape) != (M, N) or b.shape[1] != K:
         return None

@@ -25,8 +25,8 @@ def _mask(bits):
     return (bits.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
 
 
-@pytest.mark.parametrize("N,K", [(512, 128), (128, 512)])
-@pytest.mark.parametrize("M,grid", [(8192, 0), (1000, 3), (64 * 37 + 5, 8), (200704, 0)])
+@pytest.mark.parametrize("N,K", [(512, 128), (128, 512), (1024, 256), (256, 1024)])
+@pytest.mark.parametrize("M,grid", [(8192, 0), (1000, 3), (64 * 37 + 5, 8), (200704, 0), (50176, 0)])
 def test_stream_plain_and_stats(N, K, M, grid):
     torch.manual_seed(0)
     a = torch.randn(M, K, device="cuda").bfloat16()
@@ -42,14 +42,14 @@ def test_stream_plain_and_stats(N, K, M, grid):
     torch.testing.assert_close(st[1], (cf * cf).sum(0), atol=0.5, rtol=1e-3)
 
 
-@pytest.mark.parametrize("N,K", [(512, 128), (128, 512)])
+@pytest.mark.parametrize("N,K", [(512, 128), (128, 512), (1024, 256), (256, 1024)])
 @pytest.mark.parametrize("M,grid,with_mask,with_res", [(8192, 0, True, True), (32 * 37 + 5, 8, True, True),
                                                        (32 * 9, 3, True, False), (1000, 5, False, True),
                                                        (50000, 0, True, False)])
 def test_stream_bn_backward_epilogue(N, K, M, grid, with_mask, with_res):
     """dz = (a w^T [+ res]) * relu_mask, rows [sum dz | sum dz * xhat] (residual: N = 512 only)."""
-    if with_res and N != 512:
-        pytest.skip("residual epilogue: N = 512 (the residual-adding stage-2 dgrad)")
+    if with_res and N not in (512, 1024):
+        pytest.skip("residual epilogue: N = 512 / 1024 (the residual-adding stage-2 / 3 dgrads)")
     torch.manual_seed(3)
     a = torch.randn(M, K, device="cuda").bfloat16()
     w = (torch.randn(N, K, device="cuda") * 0.1).bfloat16()
