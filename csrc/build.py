@@ -58,7 +58,7 @@ def needs(src, obj, hdr_mtime):
 # 260), the skinny GEMMs.  gemm_big.hip's 8-wave kernels compile identically either way.
 _VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 EXTRA = {"gemm_big.hip": _VGPR_FORM, "conv3x3.hip": _VGPR_FORM, "skinny_gemm.hip": _VGPR_FORM,
-         "stream_gemm.hip": _VGPR_FORM}
+         "stream_gemm.hip": _VGPR_FORM, "gemm_duo.hip": _VGPR_FORM}
 
 
 def compile_one(src, debug=False):

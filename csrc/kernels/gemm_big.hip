@@ -113,6 +113,7 @@ struct BigParams {
     int* sched;               // persistent grid: per-XCD tile tickets (null: static tile striding)
     int xsplit;               // split-K on a 1-D grid whose XCDs run contiguous (split, tile) runs
     int part_bf16;            // split-K partial slabs stored as bf16 (DDL_GEMM_PART_BF16, default on)
+    int zero_b1;              // 256 x 192 NT tiles: unused B rows from the zero page (DDL_GEMM_ZB1, default on)
 };
 // tile-ticket slot layout: 8 per-XCD counters + one exit counter, 128 B apart
 constexpr int SCHED_STRIDE = 32;
@@ -171,14 +172,20 @@ struct Stager {
     bool lok[2];
     Pix px[2];       // CONV: this lane's row in half 0 / half 1
     int kcol;        // KC/CONV: lane's k offset inside a subtile (8 c); KO/CONVW: unused
+    bool zero_h1;    // KC B of a 256 x 192 tile: this wave's rows of half 1 lie past the tile (zero page)
 
-    __device__ __forceinline__ void init(const BigParams& p, int origin) {
+    // n192: a 192-wide B tile (N192).  Its second 128-row half holds 64 useful rows, those of waves
+    // 0-3; waves 4-7 stage theirs from the zero page (every lane one 16-byte address: one cache
+    // line per instruction instead of 1 KB of operand rows) -- the same DMA count per wave, so the
+    // counted vmcnt waits are unchanged, and 1/8 fewer operand bytes per k-tile through L2.
+    __device__ __forceinline__ void init(const BigParams& p, int origin, bool n192 = false) {
         base = IS_A ? p.A : p.B;
         ld = IS_A ? p.lda : p.ldb;
         rows = IS_A ? p.M : p.N;
         K = p.K;
         r0 = origin;
         const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        zero_h1 = L == KC && !IS_A && n192 && w >= 4;
         if (L == KC || L == CONV) {
             const int lb = swz_kc(l * 16);
             const int r = lb >> 6;
@@ -222,6 +229,7 @@ struct Stager {
                 const int off = kt * BK + j * 32;
                 const bf16_t* g = lp[h] + off;
                 if (ktail) g = (off + kcol < K) ? g : p.zero;
+                if (!IS_A && h == 1 && zero_h1) g = p.zero;
                 glds(g, hbase + (w * 2 + j) * 1024);
             }
         } else if (L == KO) {
@@ -921,7 +929,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
     Stager<LA, true, KTAIL> sa;
     Stager<LB, false, KTAIL> sb;
     sa.init(p, m0);
-    sb.init(p, n0);
+    sb.init(p, n0, N192 && p.zero_b1);
 
     f32x4 acc[2][2][4][2];
     auto zero_acc = [&]() {
@@ -1255,7 +1263,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_big_k(BigParams p) {
                 coords(vn);
                 ask();
                 sa.init(p, m0);
-                sb.init(p, n0);
+                sb.init(p, n0, N192 && p.zero_b1);
                 if (nK > 0) prologueE();
                 if (behind && nK > 1) {
                     sa.stage(p, smem, 1, 0, kt0 + 1);
@@ -1711,6 +1719,15 @@ bool dynamic_enabled() {
     return on;
 }
 
+// DDL_GEMM_PERSIST=0: one block per tile (grid = tiles) instead of one persistent block per CU (A/B)
+bool persist_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_PERSIST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Tile-ticket slots of the persistent kernel, per device: SLOTS launches in flight at
 // most (the launching stream orders the rest), each slot zero at launch and re-armed by
 // the launch's last block.  Null while a stream is being captured before the first
@@ -1756,6 +1773,15 @@ bool part_bf16_enabled() {
     return on;
 }
 
+// DDL_GEMM_ZB1=0: 256 x 192 NT tiles stage all 256 B rows (the 64 past the tile read, never used) (A/B)
+bool zero_b1_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DDL_GEMM_ZB1");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // DDL_GEMM_EPI_LDS=1: plain bf16 interior tiles store whole rows through LDS (epi_lds_bf16)
 bool epi_lds_enabled() {
     static const bool on = [] {
@@ -1769,6 +1795,7 @@ template <int LA, int LB>
 int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t st, bool n192 = false) {
     p.behind_mask = behind_mask();
     p.epi_lds = epi_lds_enabled() ? 1 : 0;
+    p.zero_b1 = zero_b1_enabled() ? 1 : 0;
     const int tbn = n192 ? 192 : TB;
     p.tiles_m = (p.M + TB - 1) / TB;
     p.tiles_n = (p.N + tbn - 1) / tbn;
@@ -1815,7 +1842,7 @@ int launch_big(BigParams& p, float* ws, long ws_elems, int splits, hipStream_t s
     if (p.act == ACT_BNB && (!direct || splits > 1)) return -8;   // register epilogue only
     const int nwg = p.tiles_m * p.tiles_n;
     int gx = nwg;
-    if (direct && splits == 1) {
+    if (direct && splits == 1 && persist_enabled()) {
         // persistent: one block per CU walks tiles blockIdx.x, +gridDim.x, ...
         // (a multiple of 8, so a block's tiles stay on its XCD); split-K grids keep
         // one block per (tile, split) -- a capped grid would leave tiles for a second round

@@ -1,0 +1,398 @@
+// Dual-workgroup 256x128 bf16 GEMM for gfx950: the forward (NT: y = x W^T) and input-gradient
+// (NN: dx = dy W) GEMMs of the transformer Linears at short reduction depth (K = 768 .. 3072) --
+// kernel family K13 (reference workload: notebooks/cv/onnx_experiments.py:32,174,
+// the BERT / ViT encoders).
+//
+// Why a second GEMM kernel next to the persistent 256x256 one (gemm_big.hip): there ONE workgroup
+// owns a CU, so a tile's epilogue -- bias / GELU VALU work and the output stores -- runs with no MFMA
+// work beside it, and the stores of every CU leave in one chip-wide burst at the HBM write rate
+// (stamps: 3.5-4.2 us per 256x192 tile at ~6.6 TB/s chip-wide; the bias+GELU tile stores twice the
+// bytes and ran 111 us against 83 us plain at 16384x3072x768).  A persistent block cannot hide them
+// behind its next tile either: vmcnt retires loads and stores in issue order, so the next tile's
+// operand waits wait out the stores.
+//
+// Here TWO workgroups share each CU (72 KB of LDS and <= 256 VGPRs per wave each): every SIMD runs
+// one wave of each, and whatever one workgroup is doing that is not MFMA work -- its epilogue, its
+// prologue loads, a barrier, an LDS read it waits for -- the other workgroup's wave fills with its
+// MFMAs.  The two drift apart by themselves, so the output stores spread over the whole kernel.
+//   * tile 256 x 128, 4 waves as 2 (M) x 2 (N), each 128 x 64 (8 x 4 accumulators of 16 x 16,
+//     128 registers);
+//   * operands by LDS-DMA (global_load_lds, 16 B per lane) in 32-deep k-stages through a 3-slot
+//     ring (two stages in flight); A and a k-contiguous B (NT) as 16 x 32 subtiles of 1 KB with the
+//     st_16x32 swizzle (gemm_big.hip swz_kc), a k-outer B (NN) as [32 k][128] rows of 256 B with the
+//     XOR chunk swizzle (read by ds_read_b64_tr_b16);
+//   * one barrier per stage: it publishes the stage every wave waited for and frees the slot the
+//     stage after next is staged into;
+//   * epilogue math from the MFMA layout (bias, residual, GELU with the pre-activation kept, dGELU,
+//     column statistics), the bf16 tile through LDS and out as whole-row stores;
+//   * one block per tile (no persistence: the next workgroup on a CU starts as soon as one ends,
+//     with counters of its own), XCD-aware tile order (gemm_big.hip coords).
+// Needs N % 128 == 0, K % 32 == 0, lda / ldb / ldc % 8 == 0, 16-byte aligned operands, operands and
+// output under 2 GB; M is free (rows past M load zeros and are not stored: buffer range checks).
+#include "ddl_common.h"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int TM = 256, TN = 128, DBK = 32, NST = 3, NTH = 256;
+constexpr int A_BYTES = TM * DBK * 2;          // 16 KB: 16 subtiles of 16 rows x 32 k
+constexpr int B_BYTES = TN * DBK * 2;          // 8 KB
+constexpr int ST_BYTES = A_BYTES + B_BYTES;    // 24 KB per stage
+constexpr int GROUP_M = 8;
+
+enum { LKC = 0, LKO = 1 };
+enum { E_BF16 = 0, E_GELU = 1, E_DGELU = 2 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_v4;
+
+struct DuoParams {
+    const bf16_t* A;
+    const bf16_t* B;
+    long lda, ldb;
+    bf16_t* C;
+    long ldc;
+    int M, N, K;
+    const bf16_t* bias;     // [N] or null
+    const bf16_t* res;      // E_BF16: residual [M][ldc] or null
+    bf16_t* aux;            // E_GELU: pre-activation out; E_DGELU: pre-activation in
+    float* colstats;        // [2 * tiles_m][2][N] partial column sums of the bf16 output, or null
+    int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
+__device__ __forceinline__ int swz_ko(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+__device__ __forceinline__ void glds(const bf16_t* g, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 0);
+}
+__device__ __forceinline__ s16x4 ds_read_tr(lds_v4* __restrict__ p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+}
+
+// 16 x 32 fragment of a subtile image (rows on lane & 15, k chunk lane >> 4)
+__device__ __forceinline__ bf16x8 frag_kc(const char* sub) {
+    const int l = threadIdx.x & 63;
+    return *reinterpret_cast<const bf16x8*>(sub + swz_kc((l & 15) * 64 + (l >> 4) * 16));
+}
+// 16 columns (cbase ..) x 32 k of a [32 k][128] k-outer image, transposed on read
+__device__ __forceinline__ bf16x8 frag_ko(const char* img, int cbase) {
+    const int l = threadIdx.x & 63;
+    const int g = l >> 4, q = (l >> 2) & 3, pq = l & 3;
+    const int chunk = (cbase + 4 * pq) >> 3;
+    const int ra = 8 * g + q, rb = ra + 4;
+    const char* pa = img + ra * 256 + ((chunk ^ swz_ko(ra)) << 4) + (pq & 1) * 8;
+    const char* pb = img + rb * 256 + ((chunk ^ swz_ko(rb)) << 4) + (pq & 1) * 8;
+    const s16x4 lo = ds_read_tr((lds_v4*)pa);
+    const s16x4 hi = ds_read_tr((lds_v4*)pb);
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+#define BARRIER() __builtin_amdgcn_s_barrier()
+#define VMN(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+__device__ __forceinline__ float lo_f(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_f(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+template <int LB, int EK>
+__global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
+    // one LDS object (a second __shared__ variable makes the compiler's LDS-DMA alias tracking
+    // wait vmcnt(0) before the fragment reads)
+    __shared__ __attribute__((aligned(16))) char smem[NST * ST_BYTES];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int wm = w >> 1, wn = w & 1;
+
+    // XCD-aware tile order: XCD x (blocks x, x + 8, ...) owns a contiguous range of tile ids,
+    // walked GROUP_M row tiles at a time (the A / B panels its resident blocks read stay in its L2)
+    int tm, tn;
+    {
+        const int nwg = p.tiles_m * p.tiles_n, bid = blockIdx.x;
+        const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
+        const int wg = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+        const int per_group = GROUP_M * p.tiles_n;
+        const int grp = wg / per_group, first_m = grp * GROUP_M;
+        const int gsz = min(p.tiles_m - first_m, GROUP_M);
+        const int wl = wg - grp * per_group;
+        tm = first_m + wl % gsz;
+        tn = wl / gsz;
+    }
+    const int m0 = tm * TM, n0 = tn * TN;
+    const int nt = p.K / DBK;
+
+    // DMA sources: buffer loads to LDS (per-lane 32-bit byte offsets, the k-stage as the scalar
+    // offset; rows past M read zeros from the buffer range check).  A: this wave's 4 subtiles (rows
+    // (4w + s) * 16 ..); B (KC): 2 subtiles (rows (2w + s) * 16 ..); B (KO): 2 groups of 4 k-rows
+    // ((2w + s) * 4 + (l >> 4)), 16-byte chunk (l & 15) ^ the swizzle of its row
+    const int lb = swz_kc(l * 16);
+    const int r_in = lb >> 6, kcol = ((lb >> 4) & 3) * 8;
+    const __amdgpu_buffer_rsrc_t ars_op =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, (int)((long)p.M * p.lda * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t brs_op = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(p.B), 0, (int)((long)(LB == LKC ? p.N : p.K) * p.ldb * 2), 0x00020000);
+    int ao[4], bo[2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ao[s] = ((m0 + (4 * w + s) * 16 + r_in) * (int)p.lda + kcol) * 2;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        if (LB == LKC) {
+            bo[s] = ((n0 + (2 * w + s) * 16 + r_in) * (int)p.ldb + kcol) * 2;
+        } else {
+            const int krow = (2 * w + s) * 4 + (l >> 4);
+            bo[s] = (krow * (int)p.ldb + n0 + 8 * ((l & 15) ^ swz_ko(krow))) * 2;
+        }
+    }
+    const int b_kstep = LB == LKC ? DBK * 2 : DBK * (int)p.ldb * 2;   // bytes per k-stage
+    auto stage = [&](int kt, int slot) {
+        char* sb = smem + slot * ST_BYTES;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ars_op, (lds_void*)(sb + (4 * w + s) * 1024), 16, ao[s],
+                                                     kt * (DBK * 2), 0, 0);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(brs_op, (lds_void*)(sb + A_BYTES + (2 * w + s) * 1024), 16, bo[s],
+                                                     kt * b_kstep, 0, 0);
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    // Main loop, software-pipelined across the stage barrier: stage t's fragments are in registers
+    // (F) when its MFMAs start; after the first 16 of them the wave waits for stage t + 1 (stage
+    // t + 2 stays in flight: 6 DMAs per wave per stage), passes the barrier -- which also tells it
+    // every wave has read slot t -- stages t + 3 into slot t, reads stage t + 1's fragments (G) and
+    // issues the last 16 MFMAs of stage t under those reads.  Unrolled by two (F / G alternate), the
+    // ring slot is a run-time value.
+    bf16x8 fa0[8], fb0[4], fa1[8], fb1[4];
+    auto read_frags = [&](int slot, bf16x8 (&fa)[8], bf16x8 (&fb)[4]) {
+        const char* sb = smem + slot * ST_BYTES;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            fb[j] = LB == LKC ? frag_kc(sb + A_BYTES + (wn * 4 + j) * 1024) : frag_ko(sb + A_BYTES, wn * 64 + j * 16);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[i] = frag_kc(sb + (wm * 8 + i) * 1024);
+    };
+    auto mma_half = [&](int i0, bf16x8 (&fa)[8], bf16x8 (&fb)[4]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // prologue: stages 0, 1, 2 in flight, stage 0 landed and its fragments read
+    stage(0, 0);
+    if (nt > 1) stage(1, 1);
+    if (nt > 2) stage(2, 2);
+    if (nt > 2) VMN(12);
+    else if (nt > 1) VMN(6);
+    else VMN(0);
+    BARRIER();
+    read_frags(0, fa0, fb0);
+    // one stage with fragments F; G receives stage t + 1's
+    auto step = [&](int t, int slot, bf16x8 (&fa)[8], bf16x8 (&fb)[4], bf16x8 (&ga)[8], bf16x8 (&gb)[4]) {
+        mma_half(0, fa, fb);
+        if (t + 1 < nt) {
+            if (t + 2 < nt) VMN(6);
+            else VMN(0);
+            // this wave's reads of slot t retired before the barrier that lets slot t be restaged
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            BARRIER();
+            if (t + 3 < nt) stage(t + 3, slot);
+            read_frags(slot == 2 ? 0 : slot + 1, ga, gb);
+        }
+        mma_half(4, fa, fb);
+    };
+    int slot = 0, t = 0;
+#pragma unroll 1
+    for (; t + 2 <= nt; t += 2) {
+        const int s1 = slot == 2 ? 0 : slot + 1;
+        step(t, slot, fa0, fb0, fa1, fb1);
+        step(t + 1, s1, fa1, fb1, fa0, fb0);
+        slot = s1 == 2 ? 0 : s1 + 1;
+    }
+    if (t < nt) step(t, slot, fa0, fb0, fa1, fb1);
+
+    // ---------------- epilogue: acc[i][j] = rows m0 + wm*128 + i*16 + (l & 15), columns
+    // n0 + wn*64 + j*16 + 4*(l >> 4) .. +3.  The finished bf16 tile goes through LDS (the operand ring
+    // is free now: 64 KB image, rows of 256 B with the 16-byte chunks XOR-swizzled by row) and leaves
+    // as whole-row stores -- every store instruction writes 4 rows x 256 B, i.e. whole 128-B lines,
+    // where stores from the MFMA layout touch 32 rows x 32 B each (4x the lines per instruction for
+    // the vector memory path).  Stores and the residual / pre-activation loads go through buffer
+    // resources of M rows: rows past M are dropped (stores) or read as zeros.
+    const int r16 = l & 15, g4 = (l >> 4) * 4;
+    const int mw = m0 + wm * 128;
+    const int nw = n0 + wn * 64;
+    const uint32_t cbytes = (uint32_t)((long)p.M * p.ldc * 2);
+    float bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (EK != E_DGELU && p.bias) {
+            const uint2 b2 = *reinterpret_cast<const uint2*>(p.bias + nw + j * 16 + g4);
+            bv[j][0] = lo_f(b2.x); bv[j][1] = hi_f(b2.x); bv[j][2] = lo_f(b2.y); bv[j][3] = hi_f(b2.y);
+        } else {
+            bv[j][0] = bv[j][1] = bv[j][2] = bv[j][3] = 0.f;
+        }
+    }
+    // residual (E_BF16) / saved pre-activation (E_DGELU): every site's load goes out before the
+    // first store (a load's wait would also wait out the stores issued before it)
+    const bf16_t* pre = EK == E_BF16 ? p.res : (EK == E_DGELU ? (const bf16_t*)p.aux : nullptr);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x2 rb[8][4];
+    if (pre) {
+        const __amdgpu_buffer_rsrc_t prs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(pre), 0, (int)cbytes, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                rb[i][j] = __builtin_amdgcn_raw_buffer_load_b64(
+                    prs, (int)(((long)(mw + i * 16 + r16) * p.ldc + nw + j * 16 + g4) * 2), 0, 0);
+    }
+    // tile image: row r (0..255), 16-byte chunk c (0..15) at r * 256 + ((c ^ (r & 15)) << 4)
+    const int wr0 = wm * 128 + r16;                    // this lane's image row for i = 0
+    auto img_off = [&](int i, int j) {
+        const int c = wn * 8 + j * 2 + (l >> 5);
+        return (wr0 + i * 16) * 256 + ((c ^ r16) << 4) + ((l >> 4) & 1) * 8;
+    };
+    // every wave's last fragment reads of the ring are done (each waited lgkmcnt before its MFMAs)
+    BARRIER();
+    const bool stats = EK != E_GELU && p.colstats;
+    u32x2 yk[8][4];                                    // GELU: the output, held while aux leaves
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = mw + i * 16 + r16;
+            const f32x4 a = acc[i][j];
+            uint32_t lo, hi;
+            if (EK == E_BF16) {
+                float rv[4] = {0.f, 0.f, 0.f, 0.f};
+                if (pre) { rv[0] = lo_f(rb[i][j][0]); rv[1] = hi_f(rb[i][j][0]); rv[2] = lo_f(rb[i][j][1]); rv[3] = hi_f(rb[i][j][1]); }
+                lo = pack2bf(a[0] + bv[j][0] + rv[0], a[1] + bv[j][1] + rv[1]);
+                hi = pack2bf(a[2] + bv[j][2] + rv[2], a[3] + bv[j][3] + rv[3]);
+                *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(lo, hi);
+            } else if (EK == E_GELU) {
+                const float z[4] = {a[0] + bv[j][0], a[1] + bv[j][1], a[2] + bv[j][2], a[3] + bv[j][3]};
+                const f32x2_t y0 = gelu_erf2(f32x2_t{z[0], z[1]}), y1 = gelu_erf2(f32x2_t{z[2], z[3]});
+                lo = pack2bf(y0.x, y0.y);
+                hi = pack2bf(y1.x, y1.y);
+                yk[i][j] = u32x2{lo, hi};
+                // the pre-activation leaves first (aux); without aux the output goes straight in
+                *reinterpret_cast<uint2*>(smem + img_off(i, j)) =
+                    p.aux ? make_uint2(pack2bf(z[0], z[1]), pack2bf(z[2], z[3])) : make_uint2(lo, hi);
+            } else {
+                const u32x2 z2 = rb[i][j];
+                const f32x2_t d0 = f32x2_t{a[0], a[1]} * gelu_erf_grad2(f32x2_t{lo_f(z2[0]), hi_f(z2[0])});
+                const f32x2_t d1 = f32x2_t{a[2], a[3]} * gelu_erf_grad2(f32x2_t{lo_f(z2[1]), hi_f(z2[1])});
+                lo = pack2bf(d0.x, d0.y);
+                hi = pack2bf(d1.x, d1.y);
+                *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(lo, hi);
+            }
+            if (stats) {
+                const float keep = m < p.M ? 1.f : 0.f;    // rows past M: zero operand rows, not stored
+                const float tv[4] = {lo_f(lo) * keep, hi_f(lo) * keep, lo_f(hi) * keep, hi_f(hi) * keep};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    cs[e] += tv[e];
+                    cq[e] += tv[e] * tv[e];
+                }
+            }
+        }
+        if (stats) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                cs[e] = row16_sum(cs[e]);
+                cq[e] = row16_sum(cq[e]);
+            }
+            if (r16 == 0) {
+                // one partial row per 128 output rows (as the 256x256 kernel: row 2 tm + wm)
+                float* row = p.colstats + (long)(tm * 2 + wm) * 2 * p.N;
+                const int n = nw + j * 16 + g4;
+                *reinterpret_cast<f32x4*>(row + n) = (f32x4){cs[0], cs[1], cs[2], cs[3]};
+                *reinterpret_cast<f32x4*>(row + p.N + n) = (f32x4){cq[0], cq[1], cq[2], cq[3]};
+            }
+        }
+    }
+    // whole-row stores of the image: wave w takes rows 4 it + (l >> 4) of its 64-row quarter, lane
+    // chunk l & 15 (16 B); 16 instructions per wave, each 4 rows x 256 B
+    auto store_image = [&](bf16_t* dst) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        BARRIER();
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)cbytes, 0x00020000);
+        const int c = l & 15;
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int r = w * 64 + it * 4 + (l >> 4);
+            const u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(((long)(m0 + r) * p.ldc + n0 + c * 8) * 2), 0, 0);
+        }
+    };
+    if (EK == E_GELU && p.aux) {
+        store_image(p.aux);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        BARRIER();                                     // every image read done before it is rewritten
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(yk[i][j][0], yk[i][j][1]);
+    }
+    store_image(p.C);
+}
+
+template <int LB>
+int launch(const DuoParams& p, int ek, hipStream_t st) {
+    const dim3 grid(p.tiles_m * p.tiles_n), block(NTH);
+    switch (ek) {
+        case E_BF16: hipLaunchKernelGGL((gemm_duo_k<LB, E_BF16>), grid, block, 0, st, p); break;
+        case E_GELU: hipLaunchKernelGGL((gemm_duo_k<LB, E_GELU>), grid, block, 0, st, p); break;
+        default: hipLaunchKernelGGL((gemm_duo_k<LB, E_DGELU>), grid, block, 0, st, p); break;
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// C[M, N] = A[M, K] op(B) (+ epilogue), bf16 in / out, fp32 accumulation, on 256 x 128 tiles with two
+// workgroups per CU.  mode 0: NT (B = [N][K]), mode 1: NN (B = [K][N]).
+// act: 0 none (bias / residual optional), 1 GELU (bias optional; aux <- the pre-activation), 4 dGELU
+// (aux = the pre-activation: C = acc * GELU'(aux); no bias / residual).  colstats (nullable, not with
+// GELU): [2 * ceil(M / 256)][2][N] fp32 column sums / sums of squares of the stored output, one row
+// pair per 128 output rows.  Returns -1 for shapes outside the contract (N % 128, K % 32, ld % 8,
+// 16-byte alignment), -2 for an unsupported epilogue.
+DDL_API int ddl_gemm_duo(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
+                         int K, const void* bias, int act, void* aux, const void* res, float* colstats,
+                         hipStream_t st) {
+    if (M <= 0 || N <= 0) return 0;
+    if (N % TN || K % DBK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldc < N ||
+        (mode == 0 ? ldb < K : ldb < N) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 15))
+        return -1;
+    if (mode != 0 && mode != 1) return -1;
+    int ek;
+    if (act == 0) ek = E_BF16;
+    else if (act == 1 && !res) ek = E_GELU;
+    else if (act == 4 && aux && !bias && !res) ek = E_DGELU;
+    else return -2;
+    if (ek == E_GELU && colstats) return -2;
+    if ((res && ((uintptr_t)res & 7)) || (aux && ((uintptr_t)aux & 15)) || (bias && ((uintptr_t)bias & 7))) return -1;
+    // 32-bit offsets: operand element offsets and output byte extents
+    const long a_bytes = (long)M * lda * 2, b_bytes = (long)(mode == 0 ? N : K) * ldb * 2, c_bytes = (long)M * ldc * 2;
+    if (a_bytes >= (1L << 31) || b_bytes >= (1L << 31) || c_bytes >= (1L << 31)) return -1;
+    DuoParams p{};
+    p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
+    p.C = (bf16_t*)C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+    p.bias = (const bf16_t*)bias; p.res = (const bf16_t*)res; p.aux = (bf16_t*)aux; p.colstats = colstats;
+    p.tiles_m = (M + TM - 1) / TM;
+    p.tiles_n = N / TN;
+    return mode == 0 ? launch<LKC>(p, ek, st) : launch<LKO>(p, ek, st);
+}

@@ -17,6 +17,7 @@ _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
                "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, I, P],
                "ddl_stream_wgrad": [P, L, P, L, P, L, I, I, L, I, P, L, P, I, P],
+               "ddl_gemm_duo": [I, P, L, P, L, P, L, I, I, I, P, I, P, P, P, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -38,7 +39,7 @@ def set_big_gemm(enabled: bool) -> None:
 
 
 _forced: Optional[str] = None
-_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg", "wg2", "swg")
+_KINDS = ("big", "big192", "hybrid", "small", "narrow", "tnarrow", "wg", "wg2", "swg", "duo")
 # per-call device timing for diagnostics (scripts/debug/gemm_trace.py): list of
 # (signature, (kernel, splits), start event, end event) while enabled
 _trace: Optional[list] = None
@@ -173,6 +174,16 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
                 raise RuntimeError(f"ddl_stream_wgrad(M={M}, N={N}, K={K}) failed: {rc}")
             return
         kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
+    if kind == "duo":
+        if duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap, conv_arr,
+                  accumulate, C) and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0 and C.data_ptr() % 16 == 0:
+            rc = _lib.fn("ddl_gemm_duo")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
+                                         _lib.p(bias), ACT[act], _lib.p(aux), _lib.p(residual), _lib.p(colstats),
+                                         _lib.stream())
+            if rc != 0:
+                raise RuntimeError(f"ddl_gemm_duo(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
+            return
+        kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
     if kind in ("wg", "wg2"):
         cw = mode == MODE_CONVW and conv_arr is not None and conv_arr[3] % 8 == 0
         wide = kind == "wg2"
@@ -263,6 +274,39 @@ _WG2 = os.environ.get("DDL_GEMM_WG2", "0") == "1"
 
 
 _SWG = os.environ.get("DDL_GEMM_SWG", "1") != "0"   # tuner candidate "swg" (A/B: 0 = never)
+
+
+_DUO = os.environ.get("DDL_GEMM_DUO", "1") != "0"   # tuner candidate "duo" (A/B: 0 = never)
+
+
+def duo_ok(mode: int, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, bias, act, aux, residual, colstats,
+           row_remap=False, conv=None, accumulate=False, C=None) -> bool:
+    """Calls the dual-workgroup 256x128 kernel takes (gemm_duo.hip ddl_gemm_duo's contract): NT / NN
+    bf16 GEMMs with N % 128 == 0, K % 32 == 0, 8-element leading dimensions, operands under 2 GB,
+    and a bias / residual / GELU (+ pre-activation) / dGELU / column-statistics epilogue."""
+    if mode not in (MODE_NT, MODE_NN) or row_remap or conv is not None or accumulate:
+        return False
+    if N % 128 or K % 32 or K <= 0 or lda % 8 or ldb % 8 or ldc % 8 or lda < K or ldc < N:
+        return False
+    if (ldb < K if mode == MODE_NT else ldb < N):
+        return False
+    if C is not None and C.dtype != torch.bfloat16:
+        return False
+    if bias is not None and bias.dtype != torch.bfloat16:
+        return False
+    if act is None:
+        pass
+    elif act == "gelu":
+        if residual is not None or colstats is not None:
+            return False
+    elif act == "dgelu":
+        if aux is None or bias is not None or residual is not None:
+            return False
+    else:
+        return False
+    if M * lda * 2 >= 2 ** 31 or (N if mode == MODE_NT else K) * ldb * 2 >= 2 ** 31 or M * ldc * 2 >= 2 ** 31:
+        return False
+    return True
 
 
 def swg_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
@@ -430,6 +474,8 @@ def _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residua
     cands = _candidates(mode, M, N, K, row_remap, lda, ldb, plain, conv_c)
     if act not in (None, "relu", "gelu", "dgelu") or (act == "dgelu" and aux is None):
         cands = [c for c in cands if c[0] != "big192"]     # LDS-staged epilogue: 256-wide tiles only
+    if _DUO and duo_ok(mode, M, N, K, lda, ldb, N, bias, act, aux, residual, colstats, row_remap, conv_c):
+        cands.append(("duo", 1))
     if colstats is not None:   # statistics epilogue: whole-K tiles only
         cands = [c for c in cands if c[1] == 1 and not c[0].startswith("t")]
         # 128x64 tiles (three blocks per CU) for the epilogue-heavy statistics / BN-backward
@@ -567,6 +613,9 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
                 and bias is None and act is None and residual is None and not row_remap and colstats is None \
                 and wg_ok(M, N, K, lda, ldb, kernel == "wg2"):
             choice = (kernel, splits or big_splits(M, N, K))
+        elif kernel == "duo" and duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap,
+                                        conv, False, C):
+            choice = ("duo", 1)
         elif kernel == "tnarrow" and mode in (MODE_TN, MODE_CONVW) and bias is None and act is None \
                 and residual is None and not row_remap and colstats is None:
             choice = ("tnarrow", pick_splits(N, 2 * M, K, splits))
@@ -601,7 +650,7 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
     else:
         choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
     if colstats is not None and (choice[1] != 1 or choice[0].startswith("t")):
-        choice = (choice[0] if choice[0] in ("big", "big192") else "small", 1)
+        choice = (choice[0] if choice[0] in ("big", "big192", "duo") else "small", 1)
     return choice
 
 
@@ -660,7 +709,7 @@ def gemm(mode: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int, C: tor
                         residual is not None, colstats is not None, accumulate), choice, e0, e1))
     if colstats is not None:
         # one partial row per 128 output rows (256x256 tiles: one per wave row)
-        return 2 * -(-M // 256) if choice[0] in ("big", "big192") else -(-M // 128)
+        return 2 * -(-M // 256) if choice[0] in ("big", "big192", "duo") else -(-M // 128)
     return C
 
 

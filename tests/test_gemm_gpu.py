@@ -621,3 +621,56 @@ def test_big192_tiles(M, N, K, epi):
             sums = kw["colstats"].view(-1, 2, N)[:rows, 0].sum(0)
             assert _rel_err(sums, c.float().sum(0)) < 1e-3
         assert _rel_err(c, exp) < 1e-2, (mode, epi)
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 768, 768), (1000, 384, 224), (4096, 3072, 768), (2048, 768, 3072)])
+@pytest.mark.parametrize("epi", ["plain", "bias", "bias_res", "gelu", "dgelu_stats", "stats"])
+def test_duo_kernel(M, N, K, epi):
+    """Dual-workgroup 256 x 128 kernel (kernel "duo", gemm_duo.hip): NT and NN against the fp32
+    reference for every epilogue it takes, a partial last row tile (M % 256) and odd stage counts
+    (K / 32 not a multiple of 3) included; column sums of the stored output (dGELU bias gradient,
+    BatchNorm statistics) against the output's own sums."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    torch.manual_seed(13)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev).to(torch.bfloat16)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    pre = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    for mode in (NG.MODE_NT, NG.MODE_NN):
+        wop = w if mode == NG.MODE_NT else w.t().contiguous()
+        ldb = K if mode == NG.MODE_NT else N
+        ref = a.float() @ w.float().t()
+        c = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        kw = {}
+        if epi == "bias":
+            kw = dict(bias=b)
+        elif epi == "bias_res":
+            kw = dict(bias=b, residual=res)
+        elif epi == "gelu":
+            kw = dict(bias=b, act="gelu", aux=torch.empty_like(c))
+        elif epi == "dgelu_stats":
+            kw = dict(act="dgelu", aux=pre, colstats=torch.zeros(NG.stats_rows_max(M) * 2 * N, device=dev))
+        elif epi == "stats":
+            kw = dict(colstats=torch.zeros(NG.stats_rows_max(M) * 2 * N, device=dev))
+        assert NG._choose(mode, a, K, wop, ldb, c, N, M, N, K, kw.get("bias"), kw.get("act"), kw.get("aux"), None,
+                          None, None, False, kw.get("residual"), "duo", kw.get("colstats"))[0] == "duo"
+        rows = NG.gemm(mode, a, K, wop, ldb, c, N, M, N, K, kernel="duo", **kw)
+        exp = ref
+        if epi in ("bias", "bias_res", "gelu"):
+            exp = exp + b.float()
+        if epi == "bias_res":
+            exp = exp + res.float()
+        if epi == "gelu":
+            assert _rel_err(kw["aux"], exp) < 1e-2
+            exp = torch.nn.functional.gelu(exp)
+        if epi == "dgelu_stats":
+            z = pre.float()
+            exp = exp * (0.5 * (1 + torch.erf(z / 2 ** 0.5)) + z * torch.exp(-0.5 * z * z) / (2 * torch.pi) ** 0.5)
+        if "stats" in epi:
+            st = kw["colstats"].view(-1, 2, N)[:rows]
+            assert _rel_err(st[:, 0].sum(0), c.float().sum(0)) < 1e-3
+            assert _rel_err(st[:, 1].sum(0), (c.float() ** 2).sum(0)) < 1e-3
+        assert not torch.isnan(c.float()).any(), (mode, epi)
+        assert _rel_err(c, exp) < 1e-2, (mode, epi)

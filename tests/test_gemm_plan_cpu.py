@@ -122,3 +122,26 @@ def test_wg_candidate_conv_wgrad(monkeypatch):
     assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_CONVW, 256, 2304, 50176, False, 256, 0, plain=True))
     assert not any(k == "wg" for k, _ in NG._candidates(NG.MODE_CONVW, 256, 1152, 50176, False, 256, 0, plain=True,
                                                          conv_c=4))
+
+
+def test_duo_candidate_contract():
+    """The dual-workgroup kernel ("duo", gemm_duo.hip) is a tuner candidate for NT / NN GEMMs with
+    N % 128 == 0, K % 32 == 0 and the epilogues it implements -- never for TN, convolutions, fp32
+    outputs, accumulation or a GELU with a residual."""
+    import torch
+    b = torch.zeros(768, dtype=torch.bfloat16)
+    ok = NG.duo_ok
+    assert ok(NG.MODE_NT, 16384, 3072, 768, 768, 768, 3072, b, "gelu", object(), None, None)
+    assert ok(NG.MODE_NN, 16384, 3072, 768, 768, 3072, 3072, None, "dgelu", object(), None, object())
+    assert ok(NG.MODE_NN, 25216, 768, 3072, 3072, 768, 768, None, None, None, object(), None)
+    assert not ok(NG.MODE_TN, 768, 768, 16384, 768, 768, 768, None, None, None, None, None)
+    assert not ok(NG.MODE_NT, 16384, 1000, 768, 768, 768, 1000, None, None, None, None, None)
+    assert not ok(NG.MODE_NT, 16384, 768, 200, 200, 200, 768, None, None, None, None, None)
+    assert not ok(NG.MODE_NT, 16384, 3072, 768, 768, 768, 3072, b, "gelu", object(), object(), None)
+    assert not ok(NG.MODE_NT, 16384, 3072, 768, 768, 768, 3072, b.float(), None, None, None, None)
+    assert not ok(NG.MODE_NN, 16384, 768, 768, 768, 768, 768, None, None, None, None, None, accumulate=True)
+    assert not ok(NG.MODE_NT, 16384, 768, 768, 768, 768, 768, None, "relu", None, None, None)
+    cands = NG._tune_candidates(NG.MODE_NT, 16384, 3072, 768, 768, 768, b, "gelu", object(), False, None, None)
+    assert ("duo", 1) in cands
+    cands = NG._tune_candidates(NG.MODE_TN, 768, 3072, 16384, 768, 3072, None, None, None, False, None, None)
+    assert ("duo", 1) not in cands
