@@ -28,7 +28,7 @@
 //   * one block per tile (no persistence: the next workgroup on a CU starts as soon as one ends,
 //     with counters of its own), XCD-aware tile order (gemm_big.hip coords).
 // Needs N % 128 == 0, K % 32 == 0, lda / ldb / ldc % 8 == 0, 16-byte aligned operands, operands and
-// output under 2 GB; M is free (rows past M load zeros and are not stored: buffer range checks).
+// output under 2 GB; M is free (rows past M re-read row M - 1 and are not stored: buffer range checks).
 #include "ddl_common.h"
 
 #include <cstdlib>
@@ -41,8 +41,8 @@ constexpr int B_BYTES = TN * DBK * 2;          // 8 KB
 constexpr int ST_BYTES = A_BYTES + B_BYTES;    // 24 KB per stage
 constexpr int GROUP_M = 8;
 
-enum { LKC = 0, LKO = 1 };
-enum { E_BF16 = 0, E_GELU = 1, E_DGELU = 2 };
+enum { LKC = 0, LKO = 1, LCONV = 2 };
+enum { E_BF16 = 0, E_GELU = 1, E_DGELU = 2, E_BNB = 3 };
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_v4;
@@ -59,6 +59,16 @@ struct DuoParams {
     bf16_t* aux;            // E_GELU: pre-activation out; E_DGELU: pre-activation in
     float* colstats;        // [2 * tiles_m][2][N] partial column sums of the bf16 output, or null
     int tiles_m, tiles_n;
+    // A = implicit im2col of an NHWC tensor (LCONV): rows are output pixels (n, p, q), columns
+    // (r, s, c) with C % 32 == 0 (a 32-deep stage lies in one tap); input pixel (p * stride + h_off +
+    // r * h_step, q * stride + w_off + s * w_step)
+    int cN, cH, cW, cC, cP, cQ, cstride, h_off, w_off, h_step, w_step, cR, cS;
+    FastDiv fd_PQ, fd_Q, fd_C, fd_S;
+    // E_BNB: BatchNorm backward fused into the input gradient -- C = dz = (acc + res) * relu_mask,
+    // colstats rows [sum dz | sum dz * xhat], xhat = (aux - mean) * istd
+    const uint8_t* bn_mask;
+    const float* bn_mean;
+    const float* bn_istd;
 };
 
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -94,10 +104,15 @@ __device__ __forceinline__ bf16x8 frag_ko(const char* img, int cbase) {
 #define BARRIER() __builtin_amdgcn_s_barrier()
 #define VMN(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
+// 16 zero bytes (static device storage is zero-initialised): the source of padding pixels.  An
+// out-of-range LDS-DMA buffer load does not write its lane's LDS bytes (they keep stale data), so
+// zeros must be loaded, not produced by the range check.
+__device__ __attribute__((aligned(16))) uint4 g_duo_zero[1];
+
 __device__ __forceinline__ float lo_f(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_f(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
-template <int LB, int EK>
+template <int LA, int LB, int EK>
 __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     // one LDS object (a second __shared__ variable makes the compiler's LDS-DMA alias tracking
     // wait vmcnt(0) before the fragment reads)
@@ -123,18 +138,36 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     const int nt = p.K / DBK;
 
     // DMA sources: buffer loads to LDS (per-lane 32-bit byte offsets, the k-stage as the scalar
-    // offset; rows past M read zeros from the buffer range check).  A: this wave's 4 subtiles (rows
-    // (4w + s) * 16 ..); B (KC): 2 subtiles (rows (2w + s) * 16 ..); B (KO): 2 groups of 4 k-rows
-    // ((2w + s) * 4 + (l >> 4)), 16-byte chunk (l & 15) ^ the swizzle of its row
+    // offset); the convolution's A operand by global_load_lds (padding pixels from a zero page).
+    // A: this wave's 4 subtiles (rows (4w + s) * 16 ..); B (KC): 2 subtiles (rows (2w + s) * 16 ..);
+    // B (KO): 2 groups of 4 k-rows ((2w + s) * 4 + (l >> 4)), 16-byte chunk (l & 15) ^ its swizzle
     const int lb = swz_kc(l * 16);
     const int r_in = lb >> 6, kcol = ((lb >> 4) & 3) * 8;
+    const long a_bytes = LA == LCONV ? (long)p.cN * p.cH * p.cW * p.cC * 2 : (long)p.M * p.lda * 2;
     const __amdgpu_buffer_rsrc_t ars_op =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, (int)((long)p.M * p.lda * 2), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, (int)a_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t brs_op = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(p.B), 0, (int)((long)(LB == LKC ? p.N : p.K) * p.ldb * 2), 0x00020000);
-    int ao[4], bo[2];
+    // A row offsets; LCONV: the lane's pixel of each subtile -- element offset of its (hb, wb) corner
+    // + kcol, and the corner itself (rows past M: a corner that fails every bounds check)
+    int ao[4], hb[4], wb[4], bo[2];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) ao[s] = ((m0 + (4 * w + s) * 16 + r_in) * (int)p.lda + kcol) * 2;
+    for (int s = 0; s < 4; ++s) {
+        const int m = m0 + (4 * w + s) * 16 + r_in;
+        if (LA == LCONV) {
+            const int mm = m < p.M ? m : 0;
+            const int n = (int)fdiv((uint32_t)mm, p.fd_PQ);
+            const int rem = mm - n * p.cP * p.cQ;
+            const int pp = (int)fdiv((uint32_t)rem, p.fd_Q);
+            const int qq = rem - pp * p.cQ;
+            hb[s] = m < p.M ? pp * p.cstride + p.h_off : -(1 << 20);
+            wb[s] = qq * p.cstride + p.w_off;
+            ao[s] = ((n * p.cH + hb[s]) * p.cW + wb[s]) * p.cC + kcol;
+        } else {
+            // rows past M re-read row M - 1 (never stored; excluded from the statistics)
+            ao[s] = (min(m, p.M - 1) * (int)p.lda + kcol) * 2;
+        }
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         if (LB == LKC) {
@@ -147,10 +180,24 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     const int b_kstep = LB == LKC ? DBK * 2 : DBK * (int)p.ldb * 2;   // bytes per k-stage
     auto stage = [&](int kt, int slot) {
         char* sb = smem + slot * ST_BYTES;
+        if constexpr (LA == LCONV) {
+            // the stage's tap (uniform): padding pixels and rows past M read the zero page
+            const int k0 = kt * DBK;
+            const int tap = (int)fdiv((uint32_t)k0, p.fd_C), ci = k0 - tap * p.cC;
+            const int rr = (int)fdiv((uint32_t)tap, p.fd_S), ss = tap - rr * p.cS;
+            const int dh = rr * p.h_step, dw = ss * p.w_step;
+            const int toff = (dh * p.cW + dw) * p.cC + ci;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ars_op, (lds_void*)(sb + (4 * w + s) * 1024), 16, ao[s],
-                                                     kt * (DBK * 2), 0, 0);
+            for (int s = 0; s < 4; ++s) {
+                const bool ok = (unsigned)(hb[s] + dh) < (unsigned)p.cH && (unsigned)(wb[s] + dw) < (unsigned)p.cW;
+                glds(ok ? p.A + (ao[s] + toff) : (const bf16_t*)g_duo_zero, sb + (4 * w + s) * 1024);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ars_op, (lds_void*)(sb + (4 * w + s) * 1024), 16, ao[s],
+                                                         kt * (DBK * 2), 0, 0);
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(brs_op, (lds_void*)(sb + A_BYTES + (2 * w + s) * 1024), 16, bo[s],
@@ -244,6 +291,17 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     // residual (E_BF16) / saved pre-activation (E_DGELU): every site's load goes out before the
     // first store (a load's wait would also wait out the stores issued before it)
     const bf16_t* pre = EK == E_BF16 ? p.res : (EK == E_DGELU ? (const bf16_t*)p.aux : nullptr);
+    // E_BNB: BN mean / inverse std of the lane's 4 columns of each column block
+    float bnm[4][4], bns[4][4];
+    if (EK == E_BNB) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x4 mv = *reinterpret_cast<const f32x4*>(p.bn_mean + nw + j * 16 + g4);
+            const f32x4 sv = *reinterpret_cast<const f32x4*>(p.bn_istd + nw + j * 16 + g4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { bnm[j][e] = mv[e]; bns[j][e] = sv[e]; }
+        }
+    }
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x2 rb[8][4];
@@ -267,9 +325,28 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     BARRIER();
     const bool stats = EK != E_GELU && p.colstats;
     u32x2 yk[8][4];                                    // GELU: the output, held while aux leaves
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(EK == E_BNB ? (void*)p.aux : (void*)p.C, 0, (int)cbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rrs =
+        __builtin_amdgcn_make_buffer_rsrc(EK == E_BNB && p.res ? (void*)p.res : (void*)p.C, 0, (int)cbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+        EK == E_BNB && p.bn_mask ? (void*)p.bn_mask : (void*)p.C, 0, (int)(cbytes / 16), 0x00020000);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         float cs[4] = {0.f, 0.f, 0.f, 0.f}, cq[4] = {0.f, 0.f, 0.f, 0.f};
+        // E_BNB: this column block's BN input, residual and mask bits of the 8 row blocks, loaded
+        // together (rows past M read zeros)
+        u32x2 bx[8], br[8];
+        uint32_t bmk[8];
+        if (EK == E_BNB) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int o = (mw + i * 16 + r16) * (int)p.ldc + nw + j * 16 + g4;
+                bx[i] = __builtin_amdgcn_raw_buffer_load_b64(xrs, o * 2, 0, 0);
+                br[i] = p.res ? __builtin_amdgcn_raw_buffer_load_b64(rrs, o * 2, 0, 0) : u32x2{0u, 0u};
+                bmk[i] = p.bn_mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mrs, o >> 3, 0, 0) >> (o & 4) : 0xfu;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int m = mw + i * 16 + r16;
@@ -290,6 +367,17 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
                 // the pre-activation leaves first (aux); without aux the output goes straight in
                 *reinterpret_cast<uint2*>(smem + img_off(i, j)) =
                     p.aux ? make_uint2(pack2bf(z[0], z[1]), pack2bf(z[2], z[3])) : make_uint2(lo, hi);
+            } else if (EK == E_BNB) {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t rw = br[i][e >> 1];
+                    const float rv = (e & 1) ? hi_f(rw) : lo_f(rw);
+                    v[e] = ((bmk[i] >> e) & 1u) ? a[e] + rv : 0.f;
+                }
+                lo = pack2bf(v[0], v[1]);
+                hi = pack2bf(v[2], v[3]);
+                *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(lo, hi);
             } else {
                 const u32x2 z2 = rb[i][j];
                 const f32x2_t d0 = f32x2_t{a[0], a[1]} * gelu_erf_grad2(f32x2_t{lo_f(z2[0]), hi_f(z2[0])});
@@ -299,12 +387,22 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
                 *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(lo, hi);
             }
             if (stats) {
-                const float keep = m < p.M ? 1.f : 0.f;    // rows past M: zero operand rows, not stored
-                const float tv[4] = {lo_f(lo) * keep, hi_f(lo) * keep, lo_f(hi) * keep, hi_f(hi) * keep};
+                const bool keep = m < p.M;                 // rows past M: not stored, not counted
+                const float tv[4] = {keep ? lo_f(lo) : 0.f, keep ? hi_f(lo) : 0.f, keep ? lo_f(hi) : 0.f,
+                                     keep ? hi_f(hi) : 0.f};
+                if (EK == E_BNB) {
+                    const float xv[4] = {lo_f(bx[i][0]), hi_f(bx[i][0]), lo_f(bx[i][1]), hi_f(bx[i][1])};
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    cs[e] += tv[e];
-                    cq[e] += tv[e] * tv[e];
+                    for (int e = 0; e < 4; ++e) {
+                        cs[e] += tv[e];
+                        cq[e] += tv[e] * (xv[e] - bnm[j][e]) * bns[j][e];
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        cs[e] += tv[e];
+                        cq[e] += tv[e] * tv[e];
+                    }
                 }
             }
         }
@@ -350,13 +448,14 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     store_image(p.C);
 }
 
-template <int LB>
+template <int LA, int LB>
 int launch(const DuoParams& p, int ek, hipStream_t st) {
     const dim3 grid(p.tiles_m * p.tiles_n), block(NTH);
     switch (ek) {
-        case E_BF16: hipLaunchKernelGGL((gemm_duo_k<LB, E_BF16>), grid, block, 0, st, p); break;
-        case E_GELU: hipLaunchKernelGGL((gemm_duo_k<LB, E_GELU>), grid, block, 0, st, p); break;
-        default: hipLaunchKernelGGL((gemm_duo_k<LB, E_DGELU>), grid, block, 0, st, p); break;
+        case E_BF16: hipLaunchKernelGGL((gemm_duo_k<LA, LB, E_BF16>), grid, block, 0, st, p); break;
+        case E_GELU: hipLaunchKernelGGL((gemm_duo_k<LA, LB, E_GELU>), grid, block, 0, st, p); break;
+        case E_DGELU: hipLaunchKernelGGL((gemm_duo_k<LA, LB, E_DGELU>), grid, block, 0, st, p); break;
+        default: hipLaunchKernelGGL((gemm_duo_k<LA, LB, E_BNB>), grid, block, 0, st, p); break;
     }
     return (int)hipGetLastError();
 }
@@ -364,35 +463,56 @@ int launch(const DuoParams& p, int ek, hipStream_t st) {
 }  // namespace
 
 // C[M, N] = A[M, K] op(B) (+ epilogue), bf16 in / out, fp32 accumulation, on 256 x 128 tiles with two
-// workgroups per CU.  mode 0: NT (B = [N][K]), mode 1: NN (B = [K][N]).
+// workgroups per CU.  mode 0: NT (B = [N][K]), mode 1: NN (B = [K][N]), mode 3: A = the implicit im2col
+// of an NHWC tensor (`conv`: the 18-int descriptor of ddl_gemm_big2, channel count % 32 == 0, no
+// output row remap), B = [N][K] (a convolution forward / input gradient).
 // act: 0 none (bias / residual optional), 1 GELU (bias optional; aux <- the pre-activation), 4 dGELU
-// (aux = the pre-activation: C = acc * GELU'(aux); no bias / residual).  colstats (nullable, not with
-// GELU): [2 * ceil(M / 256)][2][N] fp32 column sums / sums of squares of the stored output, one row
-// pair per 128 output rows.  Returns -1 for shapes outside the contract (N % 128, K % 32, ld % 8,
-// 16-byte alignment), -2 for an unsupported epilogue.
+// (aux = the pre-activation: C = acc * GELU'(aux); no bias / residual), 5 BatchNorm backward (side
+// arguments from ddl_gemm_bnb; aux = the BN input, res optional, colstats required).  colstats
+// (nullable, not with GELU): [2 * ceil(M / 256)][2][N] fp32, one row pair per 128 output rows.  Returns
+// -1 for shapes outside the contract (N % 128, K % 32, ld % 8, 16-byte alignment, 2 GB extents), -2
+// for an unsupported epilogue.
 DDL_API int ddl_gemm_duo(int mode, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
-                         int K, const void* bias, int act, void* aux, const void* res, float* colstats,
+                         int K, const void* bias, int act, void* aux, const void* res, float* colstats, const int* conv,
                          hipStream_t st) {
+    BnbArgs bn{};
+    if (act == 5) bn = ddl_take_bnb();          // consumed by this call whatever happens next
     if (M <= 0 || N <= 0) return 0;
-    if (N % TN || K % DBK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8 || lda < K || ldc < N ||
-        (mode == 0 ? ldb < K : ldb < N) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 15))
+    if (mode != 0 && mode != 1 && mode != 3) return -1;
+    if (mode == 3 && (!conv || conv[3] % 32 || conv[13] != conv[4] || conv[14] != conv[5] || conv[15] != 1 ||
+                      conv[16] != 0 || conv[17] != 0 || K != conv[11] * conv[12] * conv[3]))
         return -1;
-    if (mode != 0 && mode != 1) return -1;
+    if (N % TN || K % DBK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8 || (mode != 3 && lda < K) || ldc < N ||
+        (mode == 1 ? ldb < N : ldb < K) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 15))
+        return -1;
     int ek;
     if (act == 0) ek = E_BF16;
     else if (act == 1 && !res) ek = E_GELU;
     else if (act == 4 && aux && !bias && !res) ek = E_DGELU;
+    else if (act == 5 && aux && !bias && colstats && bn.mean && bn.istd && ldc == N) ek = E_BNB;
     else return -2;
     if (ek == E_GELU && colstats) return -2;
     if ((res && ((uintptr_t)res & 7)) || (aux && ((uintptr_t)aux & 15)) || (bias && ((uintptr_t)bias & 7))) return -1;
     // 32-bit offsets: operand element offsets and output byte extents
-    const long a_bytes = (long)M * lda * 2, b_bytes = (long)(mode == 0 ? N : K) * ldb * 2, c_bytes = (long)M * ldc * 2;
+    const long a_bytes = mode == 3 ? (long)conv[0] * conv[1] * conv[2] * conv[3] * 2 : (long)M * lda * 2;
+    const long b_bytes = (long)(mode == 1 ? K : N) * ldb * 2, c_bytes = (long)M * ldc * 2;
     if (a_bytes >= (1L << 31) || b_bytes >= (1L << 31) || c_bytes >= (1L << 31)) return -1;
     DuoParams p{};
     p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
     p.C = (bf16_t*)C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = (const bf16_t*)bias; p.res = (const bf16_t*)res; p.aux = (bf16_t*)aux; p.colstats = colstats;
+    p.bn_mask = bn.mask; p.bn_mean = bn.mean; p.bn_istd = bn.istd;
     p.tiles_m = (M + TM - 1) / TM;
     p.tiles_n = N / TN;
-    return mode == 0 ? launch<LKC>(p, ek, st) : launch<LKO>(p, ek, st);
+    if (mode == 3) {
+        p.cN = conv[0]; p.cH = conv[1]; p.cW = conv[2]; p.cC = conv[3]; p.cP = conv[4]; p.cQ = conv[5];
+        p.cstride = conv[6]; p.h_off = conv[7]; p.w_off = conv[8]; p.h_step = conv[9]; p.w_step = conv[10];
+        p.cR = conv[11]; p.cS = conv[12];
+        p.fd_PQ = make_fastdiv((uint32_t)(p.cP * p.cQ));
+        p.fd_Q = make_fastdiv((uint32_t)p.cQ);
+        p.fd_C = make_fastdiv((uint32_t)p.cC);
+        p.fd_S = make_fastdiv((uint32_t)std::max(1, p.cS));
+        return launch<LCONV, LKC>(p, ek, st);
+    }
+    return mode == 0 ? launch<LKC, LKC>(p, ek, st) : launch<LKC, LKO>(p, ek, st);
 }

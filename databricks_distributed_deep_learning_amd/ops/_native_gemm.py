@@ -17,7 +17,7 @@ _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L
                "ddl_gemm_big2": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L, P, I, P, I, P, P, P],
                "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, I, P],
                "ddl_stream_wgrad": [P, L, P, L, P, L, I, I, L, I, P, L, P, I, P],
-               "ddl_gemm_duo": [I, P, L, P, L, P, L, I, I, I, P, I, P, P, P, P],
+               "ddl_gemm_duo": [I, P, L, P, L, P, L, I, I, I, P, I, P, P, P, P, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -175,11 +175,14 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
             return
         kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
     if kind == "duo":
-        if duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap, conv_arr,
+        conv_c = None if conv_arr is None else int(conv_arr[3])
+        if duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap, conv_c,
                   accumulate, C) and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0 and C.data_ptr() % 16 == 0:
+            if bnb is not None:   # ACT_BNB side arguments (mask, mean, invstd), consumed by this launch
+                _lib.fn("ddl_gemm_bnb")(_lib.p(bnb[0]), _lib.p(bnb[1]), _lib.p(bnb[2]))
             rc = _lib.fn("ddl_gemm_duo")(mode, A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K,
                                          _lib.p(bias), ACT[act], _lib.p(aux), _lib.p(residual), _lib.p(colstats),
-                                         _lib.stream())
+                                         conv_arr, _lib.stream())
             if rc != 0:
                 raise RuntimeError(f"ddl_gemm_duo(mode={mode}, M={M}, N={N}, K={K}) failed: {rc}")
             return
@@ -280,15 +283,22 @@ _DUO = os.environ.get("DDL_GEMM_DUO", "1") != "0"   # tuner candidate "duo" (A/B
 
 
 def duo_ok(mode: int, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, bias, act, aux, residual, colstats,
-           row_remap=False, conv=None, accumulate=False, C=None) -> bool:
+           row_remap=False, conv_c=None, accumulate=False, C=None) -> bool:
     """Calls the dual-workgroup 256x128 kernel takes (gemm_duo.hip ddl_gemm_duo's contract): NT / NN
-    bf16 GEMMs with N % 128 == 0, K % 32 == 0, 8-element leading dimensions, operands under 2 GB,
-    and a bias / residual / GELU (+ pre-activation) / dGELU / column-statistics epilogue."""
-    if mode not in (MODE_NT, MODE_NN) or row_remap or conv is not None or accumulate:
+    bf16 GEMMs and implicit-GEMM convolutions (``conv_c``: the input channel count, % 32 == 0; no
+    output row remap) with N % 128 == 0, K % 32 == 0, 8-element leading dimensions, operands under
+    2 GB, and a bias / residual / GELU (+ pre-activation) / dGELU / BatchNorm-backward / column-
+    statistics epilogue."""
+    if mode not in (MODE_NT, MODE_NN, MODE_CONV) or row_remap or accumulate:
         return False
-    if N % 128 or K % 32 or K <= 0 or lda % 8 or ldb % 8 or ldc % 8 or lda < K or ldc < N:
+    if mode == MODE_CONV:
+        if conv_c is None or conv_c % 32:
+            return False
+    elif conv_c is not None or lda % 8 or lda < K or M * lda * 2 >= 2 ** 31:
         return False
-    if (ldb < K if mode == MODE_NT else ldb < N):
+    if N % 128 or K % 32 or K <= 0 or ldb % 8 or ldc % 8 or ldc < N:
+        return False
+    if (ldb < N if mode == MODE_NN else ldb < K):
         return False
     if C is not None and C.dtype != torch.bfloat16:
         return False
@@ -302,9 +312,12 @@ def duo_ok(mode: int, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, bias
     elif act == "dgelu":
         if aux is None or bias is not None or residual is not None:
             return False
+    elif act == "bnb":
+        if aux is None or bias is not None or colstats is None or ldc != N:
+            return False
     else:
         return False
-    if M * lda * 2 >= 2 ** 31 or (N if mode == MODE_NT else K) * ldb * 2 >= 2 ** 31 or M * ldc * 2 >= 2 ** 31:
+    if (K if mode == MODE_NN else N) * ldb * 2 >= 2 ** 31 or M * ldc * 2 >= 2 ** 31:
         return False
     return True
 
@@ -614,7 +627,7 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
                 and wg_ok(M, N, K, lda, ldb, kernel == "wg2"):
             choice = (kernel, splits or big_splits(M, N, K))
         elif kernel == "duo" and duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap,
-                                        conv, False, C):
+                                        None if conv is None else int(conv[3]), False, C):
             choice = ("duo", 1)
         elif kernel == "tnarrow" and mode in (MODE_TN, MODE_CONVW) and bias is None and act is None \
                 and residual is None and not row_remap and colstats is None:

@@ -51,7 +51,7 @@ def _run(x, w, g, b, K, R, stride, kernel, force_kernel, BNStats, ops, dev):
     return outs
 
 
-@pytest.mark.parametrize("kernel", ["big", "small", "narrow"])
+@pytest.mark.parametrize("kernel", ["big", "small", "narrow", "duo"])
 @pytest.mark.parametrize("M,C,K,res,relu", [(1000, 64, 256, False, True), (4096, 128, 512, True, True),
                                             (777, 256, 64, True, False), (2304, 64, 64, False, True)])
 def test_bn_backward_reduction_in_dgrad_epilogue(kernel, M, C, K, res, relu):

@@ -152,7 +152,7 @@ CONVS = [  # N, H, W, C, K, R, stride, pad
 ]
 
 
-@pytest.mark.parametrize("kernel", [None, "big", "small", "narrow"])
+@pytest.mark.parametrize("kernel", [None, "big", "small", "narrow", "duo"])
 @pytest.mark.parametrize("N,H,W,C,K,R,stride,pad", CONVS)
 def test_conv_fwd_bwd(N, H, W, C, K, R, stride, pad, kernel):
     dev = gpu_device()
@@ -674,3 +674,54 @@ def test_duo_kernel(M, N, K, epi):
             assert _rel_err(st[:, 1].sum(0), (c.float() ** 2).sum(0)) < 1e-3
         assert not torch.isnan(c.float()).any(), (mode, epi)
         assert _rel_err(c, exp) < 1e-2, (mode, epi)
+
+
+@pytest.mark.parametrize("N,H,W,C,K,stride", [(2, 28, 28, 128, 128, 1), (2, 56, 56, 128, 128, 2), (3, 14, 14, 256, 256, 1),
+                                              (1, 9, 7, 64, 384, 1)])
+@pytest.mark.parametrize("epi", ["plain", "stats", "bnb"])
+def test_duo_conv(N, H, W, C, K, stride, epi):
+    """Implicit-GEMM 3x3 convolution (pad 1) on the dual-workgroup kernel (gemm_duo.hip LCONV): the
+    forward against the fp32 reference, its BatchNorm statistics rows, and the BatchNorm-backward
+    epilogue (dz = (conv + res) * mask, rows [sum dz | sum dz * xhat])."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    from databricks_distributed_deep_learning_amd.ops._native_conv import _desc
+    from databricks_distributed_deep_learning_amd.ops.conv import conv2d_reference
+    torch.manual_seed(21)
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(K, 3, 3, C, device=dev) / (3 * C ** 0.5)).to(torch.bfloat16)
+    P, Q = (H + 2 - 3) // stride + 1, (W + 2 - 3) // stride + 1
+    M = N * P * Q
+    desc = _desc(N, H, W, C, P, Q, stride, -1, -1, 1, 1, 3, 3, P, Q)
+    ref = conv2d_reference(x.float(), w.float(), stride, 1).reshape(M, K)
+    y = torch.full((M, K), float("nan"), device=dev, dtype=torch.bfloat16)
+    part = torch.zeros(NG.stats_rows_max(M) * 2 * K, device=dev)
+    kw = {}
+    if epi == "stats":
+        kw = dict(colstats=part)
+    elif epi == "bnb":
+        xb = (torch.randn(M, K, device=dev) * 2 + 0.5).bfloat16()
+        mean = torch.randn(K, device=dev) * 0.3 + 0.5
+        istd = torch.rand(K, device=dev) + 0.5
+        r = torch.randn(M, K, device=dev).bfloat16()
+        mask = torch.randint(0, 256, (M * K // 8,), device=dev, dtype=torch.uint8)
+        kw = dict(act="bnb", aux=xb, residual=r, colstats=part, bnb=(mask, mean, istd))
+    assert NG._choose(NG.MODE_CONV, x, 0, w, 9 * C, y, K, M, K, 9 * C, None, kw.get("act"), kw.get("aux"), None,
+                      desc, None, False, kw.get("residual"), "duo", kw.get("colstats"))[0] == "duo"
+    rows = NG.gemm(NG.MODE_CONV, x, 0, w, 9 * C, y, K, M, K, 9 * C, conv=desc, kernel="duo", **kw)
+    assert not torch.isnan(y.float()).any()
+    if epi == "bnb":
+        keep = ((mask[:, None].int() >> torch.arange(8, device=dev)) & 1).view(M, K).bool()
+        g = torch.where(keep, ref + r.float(), torch.zeros_like(ref))
+        assert _rel_err(y, g) < 1e-2
+        dz = y.double()
+        sums = part[:rows * 2 * K].view(rows, 2 * K).double().sum(0)
+        torch.testing.assert_close(sums[:K], dz.sum(0), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(sums[K:], (dz * (xb.double() - mean.double()) * istd.double()).sum(0),
+                                   rtol=1e-4, atol=1e-3)
+        return
+    assert _rel_err(y, ref) < 1e-2
+    if epi == "stats":
+        st = part.view(-1, 2, K)[:rows]
+        assert _rel_err(st[:, 0].sum(0), y.float().sum(0)) < 1e-3
+        assert _rel_err(st[:, 1].sum(0), (y.float() ** 2).sum(0)) < 1e-3
