@@ -562,7 +562,9 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
                                                 const T* __restrict__ dadd = nullptr) {
     // part row per block: [dgamma(H) | dbeta(H) | (dxsum) sum of dx (H)] -- the last is the
     // bias gradient of the Linear that produced this LayerNorm's input
-    __shared__ __attribute__((aligned(16))) float s_acc[3][4][VPL * 256];
+    // (+4 floats per wave row: the column reads below pair a wave row with the next as ds_read2_b32,
+    // whose two dwords fell on one bank at a stride of VPL * 256 floats -- 2-way conflicts on every read)
+    __shared__ __attribute__((aligned(16))) float s_acc[3][4][VPL * 256 + 4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float dg[VPL][4], db[VPL][4], ds[VPL][4], g[VPL][4];
 #pragma unroll

@@ -489,6 +489,9 @@ def _tune_candidates(mode, M, N, K, lda, ldb, bias, act, aux, row_remap, residua
         cands = [c for c in cands if c[0] != "big192"]     # LDS-staged epilogue: 256-wide tiles only
     if _DUO and duo_ok(mode, M, N, K, lda, ldb, N, bias, act, aux, residual, colstats, row_remap, conv_c):
         cands.append(("duo", 1))
+    if act == "dgelu" and colstats is not None:
+        # dGELU column sums: register epilogues only (256x256 / 256x192 / dual-workgroup kernels)
+        cands = [c for c in cands if c[0] in ("big", "big192", "duo")]
     if colstats is not None:   # statistics epilogue: whole-K tiles only
         cands = [c for c in cands if c[1] == 1 and not c[0].startswith("t")]
         # 128x64 tiles (three blocks per CU) for the epilogue-heavy statistics / BN-backward
@@ -664,6 +667,8 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
         choice = _heuristic(mode, M, N, K, row_remap, lda, ldb)
     if colstats is not None and (choice[1] != 1 or choice[0].startswith("t")):
         choice = (choice[0] if choice[0] in ("big", "big192", "duo") else "small", 1)
+        if act == "dgelu" and choice[0] == "small" and _big_allowed(mode, K, lda, ldb):
+            choice = ("big", 1)        # dGELU column sums: register epilogues only
     return choice
 
 

@@ -228,12 +228,12 @@ class _Linear(torch.autograd.Function):
             if pre is not None and res is None and pre[0].shape == (M, K) and _dgelu_fusable(K):
                 # dx := dZ of the producing GELU Linear (dGELU + its bias column sums in the epilogue)
                 part = torch.empty(stats_rows_max(M) * 2 * K, dtype=torch.float32, device=dx.device)
+                # (tuned among the kernels with a register dGELU epilogue: big, big192, duo)
                 if _DGRAD_NT and M >= 4 * K:
                     nrows = gemm(MODE_NT, dz, N, _transposed(ctx.w_param, w), N, dx, K, M, K, N, act="dgelu",
-                                 aux=pre[0], colstats=part, kernel="big")
+                                 aux=pre[0], colstats=part)
                 else:
-                    nrows = gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N, act="dgelu", aux=pre[0], colstats=part,
-                                 kernel="big")
+                    nrows = gemm(MODE_NN, dz, N, w, K, dx, K, M, K, N, act="dgelu", aux=pre[0], colstats=part)
                 fused = _DgeluHandoff(pre[1], part, nrows, K)
             elif _DGRAD_NT and M >= 4 * K:
                 # dx = dz W as an NT GEMM against W^T (both operands k-contiguous: ds_read_b128
