@@ -351,6 +351,11 @@ _tuned: dict = {}
 _timings: dict = {}
 _NARROW_STATS = os.environ.get("DDL_TUNE_NARROW_STATS", "0") != "0"   # same-box A/B neutral: off
 _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
+# DDL_GEMM_PREFER=kind[:factor]: take `kind` when it is within `factor` of the fastest candidate.  Default
+# "swg:1.3": the cold-cache timing over-prices the streaming weight-gradient kernel (it streams its
+# operands once, in-model often from the Infinity Cache the producing pass just filled): ResNet-50
+# same-box alternating, backward 14.61-14.63 vs 14.73-14.78 ms, 11,676-11,739 vs 11,637-11,693 img/s
+_PREFER = os.environ.get("DDL_GEMM_PREFER", "swg:1.3")
 _TUNE_ROUNDS = max(1, int(os.environ.get("DDL_GEMM_TUNE_ROUNDS", "5")))   # interleaved timing rounds per candidate
 _TUNE_COLD = os.environ.get("DDL_GEMM_TUNE_COLD", "1") != "0"             # time candidates from evicted caches
 _ONLINE = os.environ.get("DDL_GEMM_TUNE_ONLINE", "0") == "1"              # in-model tuning during warm-up (opt-in)
@@ -531,6 +536,13 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     med = [sorted(v)[len(v) // 2] for v in rounds]
     _timings[key] = {c: t for c, t in zip(cands, med)}
     best = min(range(len(cands)), key=lambda i: med[i])
+    if _PREFER:
+        # DDL_GEMM_PREFER=kind[:factor] (A/B tooling): take `kind` whenever it is within `factor` of the best
+        kind, _, f = _PREFER.partition(":")
+        for i, c in enumerate(cands):
+            if c[0] == kind and med[i] <= med[best] * float(f or "1.5"):
+                best = i
+                break
     return cands[best]
 
 
