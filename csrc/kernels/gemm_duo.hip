@@ -69,6 +69,11 @@ struct DuoParams {
     const uint8_t* bn_mask;
     const float* bn_mean;
     const float* bn_istd;
+    // split-K (weight gradients, LA = LB = LKO): block = (split, tile); splits > 1 write bf16 partial
+    // tiles to ws[split][M][N] (duo_reduce_k sums them into C); accumulate: C += result
+    int splits, kt_per_split;
+    bf16_t* ws;
+    int accumulate;
 };
 
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -122,11 +127,15 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
 
     // XCD-aware tile order: XCD x (blocks x, x + 8, ...) owns a contiguous range of tile ids,
     // walked GROUP_M row tiles at a time (the A / B panels its resident blocks read stay in its L2)
-    int tm, tn;
+    int tm, tn, split = 0;
     {
-        const int nwg = p.tiles_m * p.tiles_n, bid = blockIdx.x;
-        const int xcd = bid & 7, qn = nwg >> 3, rn = nwg & 7;
-        const int wg = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+        // with split-K the (split, tile) order is split-major, so an XCD's contiguous range is mostly
+        // one split's k-range over neighbouring tiles (their A / B k-slices shared in its L2)
+        const int nwg = p.tiles_m * p.tiles_n, n = nwg * p.splits, bid = blockIdx.x;
+        const int xcd = bid & 7, qn = n >> 3, rn = n & 7;
+        const int q = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+        split = q / nwg;
+        const int wg = q - split * nwg;
         const int per_group = GROUP_M * p.tiles_n;
         const int grp = wg / per_group, first_m = grp * GROUP_M;
         const int gsz = min(p.tiles_m - first_m, GROUP_M);
@@ -135,7 +144,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
         tn = wl / gsz;
     }
     const int m0 = tm * TM, n0 = tn * TN;
-    const int nt = p.K / DBK;
+    const int kbase = split * p.kt_per_split;                   // this block's first k-stage
+    const int nt = min(p.K / DBK - kbase, p.kt_per_split);      // >= 1 (host)
 
     // DMA sources: buffer loads to LDS (per-lane 32-bit byte offsets, the k-stage as the scalar
     // offset); the convolution's A operand by global_load_lds (padding pixels from a zero page).
@@ -143,7 +153,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     // B (KO): 2 groups of 4 k-rows ((2w + s) * 4 + (l >> 4)), 16-byte chunk (l & 15) ^ its swizzle
     const int lb = swz_kc(l * 16);
     const int r_in = lb >> 6, kcol = ((lb >> 4) & 3) * 8;
-    const long a_bytes = LA == LCONV ? (long)p.cN * p.cH * p.cW * p.cC * 2 : (long)p.M * p.lda * 2;
+    const long a_bytes = LA == LCONV ? (long)p.cN * p.cH * p.cW * p.cC * 2
+                       : (LA == LKO ? (long)p.K * p.lda * 2 : (long)p.M * p.lda * 2);
     const __amdgpu_buffer_rsrc_t ars_op =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.A), 0, (int)a_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t brs_op = __builtin_amdgcn_make_buffer_rsrc(
@@ -163,6 +174,11 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
             hb[s] = m < p.M ? pp * p.cstride + p.h_off : -(1 << 20);
             wb[s] = qq * p.cstride + p.w_off;
             ao[s] = ((n * p.cH + hb[s]) * p.cW + wb[s]) * p.cC + kcol;
+        } else if (LA == LKO) {
+            // k-outer A (weight gradients): two [32 k][128] halves; instruction u = 4w + s stages
+            // k-rows 4 (u & 7) .. +3 of half u >> 3
+            const int u = 4 * w + s, krow = (u & 7) * 4 + (l >> 4);
+            ao[s] = (krow * (int)p.lda + m0 + (u >> 3) * 128 + 8 * ((l & 15) ^ swz_ko(krow))) * 2;
         } else {
             // rows past M re-read row M - 1 (never stored; excluded from the statistics)
             ao[s] = (min(m, p.M - 1) * (int)p.lda + kcol) * 2;
@@ -179,8 +195,16 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     }
     const int b_kstep = LB == LKC ? DBK * 2 : DBK * (int)p.ldb * 2;   // bytes per k-stage
     auto stage = [&](int kt, int slot) {
+        kt += kbase;
         char* sb = smem + slot * ST_BYTES;
-        if constexpr (LA == LCONV) {
+        if constexpr (LA == LKO) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int u = 4 * w + s;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ars_op, (lds_void*)(sb + (u >> 3) * 8192 + (u & 7) * 1024), 16,
+                                                         ao[s], kt * DBK * (int)p.lda * 2, 0, 0);
+            }
+        } else if constexpr (LA == LCONV) {
             // the stage's tap (uniform): padding pixels and rows past M read the zero page
             const int k0 = kt * DBK;
             const int tap = (int)fdiv((uint32_t)k0, p.fd_C), ci = k0 - tap * p.cC;
@@ -223,7 +247,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
         for (int j = 0; j < 4; ++j)
             fb[j] = LB == LKC ? frag_kc(sb + A_BYTES + (wn * 4 + j) * 1024) : frag_ko(sb + A_BYTES, wn * 64 + j * 16);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) fa[i] = frag_kc(sb + (wm * 8 + i) * 1024);
+        for (int i = 0; i < 8; ++i) fa[i] = LA == LKO ? frag_ko(sb + wm * 8192, i * 16) : frag_kc(sb + (wm * 8 + i) * 1024);
     };
     auto mma_half = [&](int i0, bf16x8 (&fa)[8], bf16x8 (&fb)[4]) {
         __builtin_amdgcn_s_setprio(1);
@@ -423,20 +447,31 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     }
     // whole-row stores of the image: wave w takes rows 4 it + (l >> 4) of its 64-row quarter, lane
     // chunk l & 15 (16 B); 16 instructions per wave, each 4 rows x 256 B
-    auto store_image = [&](bf16_t* dst) {
+    auto store_image = [&](bf16_t* dst, long ld, uint32_t bytes, bool acc_c) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         BARRIER();
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)cbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)bytes, 0x00020000);
         const int c = l & 15;
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
             const int r = w * 64 + it * 4 + (l >> 4);
-            const u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(((long)(m0 + r) * p.ldc + n0 + c * 8) * 2), 0, 0);
+            u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+            const int off = (int)(((long)(m0 + r) * ld + n0 + c * 8) * 2);
+            if (acc_c) {   // C += result (weight gradients into their arena slot), summed in fp32
+                const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = pack2bf(lo_f(v[e]) + lo_f(o[e]), hi_f(v[e]) + hi_f(o[e]));
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
         }
     };
+    if (p.splits > 1) {            // bf16 partial tile of this split
+        store_image(p.ws + (long)split * p.M * p.N, p.N, (uint32_t)((long)p.M * p.N * 2), false);
+        return;
+    }
     if (EK == E_GELU && p.aux) {
-        store_image(p.aux);
+        store_image(p.aux, p.ldc, cbytes, false);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         BARRIER();                                     // every image read done before it is rewritten
 #pragma unroll
@@ -445,7 +480,41 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
             for (int j = 0; j < 4; ++j)
                 *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(yk[i][j][0], yk[i][j][1]);
     }
-    store_image(p.C);
+    store_image(p.C, p.ldc, cbytes, p.accumulate != 0);
+}
+
+// split-K reduce of the weight-gradient path: C (+)= sum of the bf16 partial tiles, 8 columns per
+// thread, slabs summed in split order in fp32 (groups of 4 loads in flight)
+__global__ __launch_bounds__(256) void duo_reduce_k(const bf16_t* __restrict__ ws, bf16_t* __restrict__ C, long ldc,
+                                                    int M, int N, int splits, int accumulate) {
+    const long n8 = N / 8, total = (long)M * n8, slab = (long)M * N;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int m = (int)(i / n8), n = (int)(i - (long)m * n8) * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const bf16_t* pb = ws + (long)m * N + n;
+        auto add = [&](const uint4& r) {
+            const uint32_t wd[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[2 * e] += lo_f(wd[e]); v[2 * e + 1] += hi_f(wd[e]); }
+        };
+        int s = 0;
+        for (; s + 4 <= splits; s += 4) {
+            uint4 r[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const uint4*>(pb + (s + j) * slab);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) add(r[j]);
+        }
+        for (; s < splits; ++s) add(*reinterpret_cast<const uint4*>(pb + s * slab));
+        bf16_t* cp = C + (long)m * ldc + n;
+        if (accumulate) {
+            float o[8];
+            load8(cp, o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += o[e];
+        }
+        store8(cp, v);
+    }
 }
 
 template <int LA, int LB>
@@ -502,6 +571,8 @@ DDL_API int ddl_gemm_duo(int mode, const void* A, long lda, const void* B, long 
     p.C = (bf16_t*)C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
     p.bias = (const bf16_t*)bias; p.res = (const bf16_t*)res; p.aux = (bf16_t*)aux; p.colstats = colstats;
     p.bn_mask = bn.mask; p.bn_mean = bn.mean; p.bn_istd = bn.istd;
+    p.splits = 1;
+    p.kt_per_split = K / DBK;
     p.tiles_m = (M + TM - 1) / TM;
     p.tiles_n = N / TN;
     if (mode == 3) {
@@ -515,4 +586,43 @@ DDL_API int ddl_gemm_duo(int mode, const void* A, long lda, const void* B, long 
         return launch<LCONV, LKC>(p, ek, st);
     }
     return mode == 0 ? launch<LKC, LKC>(p, ek, st) : launch<LKC, LKO>(p, ek, st);
+}
+
+// TN weight gradient on the dual-workgroup kernel: C[M, N] (+)= A^T B, A = [K][M] (lda), B = [K][N] (ldb),
+// bf16 C, split-K over `splits` (bf16 partial tiles in `ws`, ws_elems >= splits * M * N when splits > 1;
+// then duo_reduce_k).  Needs M % 256 == 0, N % 128 == 0, K % 32 == 0, 8-element leading dimensions,
+// 16-byte aligned operands, operands under 2 GB.  Returns the split count used, or -1.
+DDL_API int ddl_gemm_duo_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                            int splits, int accumulate, void* ws, long ws_elems, hipStream_t st) {
+    if (M <= 0 || N <= 0) return 0;
+    if (M % TM || N % TN || K % DBK || K <= 0 || lda % 8 || ldb % 8 || ldc % 8 || lda < M || ldb < N || ldc < N ||
+        ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)C & 15))
+        return -1;
+    if ((long)K * lda * 2 >= (1L << 31) || (long)K * ldb * 2 >= (1L << 31) || (long)M * ldc * 2 >= (1L << 31)) return -1;
+    const int nkt = K / DBK;
+    if (splits < 1) splits = 1;
+    if (splits > nkt) splits = nkt;
+    DuoParams p{};
+    p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.lda = lda; p.ldb = ldb;
+    p.C = (bf16_t*)C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+    p.tiles_m = M / TM;
+    p.tiles_n = N / TN;
+    p.kt_per_split = (nkt + splits - 1) / splits;
+    splits = (nkt + p.kt_per_split - 1) / p.kt_per_split;
+    p.splits = splits;
+    p.accumulate = accumulate;
+    if (splits > 1) {
+        if (!ws || ws_elems < (long)splits * M * N || ((uintptr_t)ws & 15) || (long)splits * M * N * 2 >= (1L << 31))
+            return -1;
+        p.ws = (bf16_t*)ws;
+    }
+    const dim3 grid(p.tiles_m * p.tiles_n * splits);
+    hipLaunchKernelGGL((gemm_duo_k<LKO, LKO, E_BF16>), grid, dim3(NTH), 0, st, p);
+    if (splits > 1) {
+        const long total = (long)M * (N / 8);
+        const int g = (int)std::min<long>(16384, (total + 255) / 256);
+        duo_reduce_k<<<g, 256, 0, st>>>(p.ws, p.C, ldc, M, N, splits, accumulate);
+    }
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc - 1 : splits;
 }

@@ -18,6 +18,7 @@ _lib.register({"ddl_gemm": [I, P, L, P, L, P, L, I, I, I, P, I, I, P, I, I, P, L
                "ddl_gemm_wgrad": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P, P, I, P],
                "ddl_stream_wgrad": [P, L, P, L, P, L, I, I, L, I, P, L, P, I, P],
                "ddl_gemm_duo": [I, P, L, P, L, P, L, I, I, I, P, I, P, P, P, P, P],
+               "ddl_gemm_duo_tn": [P, L, P, L, P, L, I, I, I, I, I, P, L, P],
                "ddl_gemm_bnb": [P, P, P]})
 
 MODE_NT, MODE_NN, MODE_TN, MODE_CONV, MODE_CONVW = 0, 1, 2, 3, 4
@@ -174,6 +175,18 @@ def _launch(kind: str, s: int, mode: int, A, lda, B, ldb, C, ldc, M, N, K, bias,
                 raise RuntimeError(f"ddl_stream_wgrad(M={M}, N={N}, K={K}) failed: {rc}")
             return
         kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
+    if kind == "duo" and mode == MODE_TN:
+        if (bias is None and act is None and residual is None and colstats is None and not row_remap
+                and C.dtype == torch.bfloat16 and duo_tn_ok(M, N, K, lda, ldb, ldc)
+                and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0 and C.data_ptr() % 16 == 0):
+            ws = torch.empty(s * M * N, dtype=torch.bfloat16, device=C.device) if s > 1 else None
+            rc = _lib.fn("ddl_gemm_duo_tn")(A.data_ptr(), lda, B.data_ptr(), ldb, C.data_ptr(), ldc, M, N, K, s,
+                                            int(accumulate), _lib.p(ws), 0 if ws is None else ws.numel(),
+                                            _lib.stream())
+            if rc < 0:
+                raise RuntimeError(f"ddl_gemm_duo_tn(M={M}, N={N}, K={K}, splits={s}) failed: {rc}")
+            return
+        kind, s = _heuristic(mode, M, N, K, row_remap, lda, ldb)   # a cached choice outside its contract
     if kind == "duo":
         conv_c = None if conv_arr is None else int(conv_arr[3])
         if duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap, conv_c,
@@ -250,6 +263,10 @@ def _candidates(mode: int, M: int, N: int, K: int, row_remap: bool, lda: int, ld
         if _WG2 and N % 256 == 0:
             w2 = big_splits(M, N, K)
             out += [("wg2", s) for s in sorted({max(1, w2 // 2), w2, 2 * w2})]
+    if _DUO and mode == MODE_TN and plain and not row_remap and duo_tn_ok(M, N, K, lda, ldb):
+        # dual-workgroup kernel, k-outer A: bf16 partial tiles + one reduce (split 1: straight into C)
+        ds = duo_tn_splits(M, N, K)
+        out += [("duo", s) for s in sorted({max(1, ds // 2), ds, min(2 * ds, K // 32)})]
     if _SWG and mode == MODE_TN and plain and not row_remap and swg_ok(M, N, K, lda, ldb):
         # streaming weight gradient (stream_gemm.hip stream_wgrad_k): every workgroup owns the whole
         # M x N output over a range of K rows (no operand re-reads), bf16 partials + one reduce
@@ -320,6 +337,20 @@ def duo_ok(mode: int, M: int, N: int, K: int, lda: int, ldb: int, ldc: int, bias
     if (K if mode == MODE_NN else N) * ldb * 2 >= 2 ** 31 or M * ldc * 2 >= 2 ** 31:
         return False
     return True
+
+
+def duo_tn_ok(M: int, N: int, K: int, lda: int, ldb: int, ldc: int = None) -> bool:
+    """TN weight gradients the dual-workgroup kernel takes (ddl_gemm_duo_tn's contract)."""
+    ldc = N if ldc is None else ldc
+    return M % 256 == 0 and N % 128 == 0 and K % 32 == 0 and K > 0 and lda % 8 == 0 and ldb % 8 == 0 \
+        and ldc % 8 == 0 and lda >= M and ldb >= N and ldc >= N and K * lda * 2 < 2 ** 31 \
+        and K * ldb * 2 < 2 ** 31 and M * ldc * 2 < 2 ** 31
+
+
+def duo_tn_splits(M: int, N: int, K: int) -> int:
+    """Split-K count that fills two workgroups per CU with 256 x 128 (tile, split) blocks."""
+    tiles = (M // 256) * (N // 128)
+    return max(1, min((K // 32) // 4, (2 * NUM_CU) // max(tiles, 1)))
 
 
 def swg_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
@@ -536,13 +567,14 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
     med = [sorted(v)[len(v) // 2] for v in rounds]
     _timings[key] = {c: t for c, t in zip(cands, med)}
     best = min(range(len(cands)), key=lambda i: med[i])
-    if _PREFER:
-        # DDL_GEMM_PREFER=kind[:factor] (A/B tooling): take `kind` whenever it is within `factor` of the best
-        kind, _, f = _PREFER.partition(":")
-        for i, c in enumerate(cands):
-            if c[0] == kind and med[i] <= med[best] * float(f or "1.5"):
-                best = i
-                break
+    fastest = best
+    for pref in filter(None, _PREFER.split(",")):
+        # DDL_GEMM_PREFER=kind[:factor],...: the first listed kind within `factor` of the fastest candidate
+        kind, _, f = pref.partition(":")
+        near = [i for i, c in enumerate(cands) if c[0] == kind and med[i] <= med[fastest] * float(f or "1.5")]
+        if near:
+            best = min(near, key=lambda i: med[i])
+            break
     return cands[best]
 
 
@@ -641,6 +673,9 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
                 and bias is None and act is None and residual is None and not row_remap and colstats is None \
                 and wg_ok(M, N, K, lda, ldb, kernel == "wg2"):
             choice = (kernel, splits or big_splits(M, N, K))
+        elif kernel == "duo" and mode == MODE_TN and bias is None and act is None and residual is None \
+                and colstats is None and not row_remap and duo_tn_ok(M, N, K, lda, ldb, ldc):
+            choice = ("duo", splits or duo_tn_splits(M, N, K))
         elif kernel == "duo" and duo_ok(mode, M, N, K, lda, ldb, ldc, bias, act, aux, residual, colstats, row_remap,
                                         None if conv is None else int(conv[3]), False, C):
             choice = ("duo", 1)

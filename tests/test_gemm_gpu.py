@@ -725,3 +725,24 @@ def test_duo_conv(N, H, W, C, K, stride, epi):
         st = part.view(-1, 2, K)[:rows]
         assert _rel_err(st[:, 0].sum(0), y.float().sum(0)) < 1e-3
         assert _rel_err(st[:, 1].sum(0), (y.float() ** 2).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(768, 768, 16384, None), (768, 3072, 4096, 3), (2304, 768, 2048, 1),
+                                          (256, 128, 96, 2), (512, 256, 4096, 7)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_duo_weight_gradient(M, N, K, splits, accumulate):
+    """TN weight gradient on the dual-workgroup kernel (k-outer A staged as two [32 k][128] halves, split-K
+    bf16 partial tiles + duo_reduce_k): against the fp32 reference, accumulating into a bf16 gradient."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_gemm as NG
+    torch.manual_seed(17)
+    dy = torch.randn(K, M, device=dev).to(torch.bfloat16)     # [tokens, out]
+    x = torch.randn(K, N, device=dev).to(torch.bfloat16)      # [tokens, in]
+    base = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    dw = base.clone() if accumulate else torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    ch = NG._choose(NG.MODE_TN, dy, M, x, N, dw, N, M, N, K, None, None, None, splits, None, None, False, None,
+                    "duo", None)
+    assert ch[0] == "duo"
+    NG.gemm(NG.MODE_TN, dy, M, x, N, dw, N, M, N, K, accumulate=accumulate, kernel="duo", splits=splits)
+    ref = dy.float().t() @ x.float() + (base.float() if accumulate else 0.)
+    assert _rel_err(dw, ref) < 1e-2
