@@ -548,6 +548,81 @@ __global__ __launch_bounds__(256) void ln_fwd_k(const T* __restrict__ x, const T
     if (lane == 0) { save_mean[row] = mean; save_rstd[row] = rstd; }
 }
 
+// bf16 LayerNorm forward with 16-byte accesses: half a wave per row (32 lanes x 8 contiguous columns
+// per chunk, chunk k covers columns 256 k + 8 lane32 .. +7), two rows per wave.  The wave-per-row
+// kernel above moves 8 bytes per lane (H = 768: three 512-B instructions per operand and row); here an
+// instruction moves 1 KB (two rows x 512 B).  Half-wave sums: DPP row sums + one permlane16 swap.
+__device__ __forceinline__ float half_sum(float v) {
+    v = row16_sum(v);
+    const uint32_t u = __float_as_uint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_fwd8_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                 long res_rows, const bf16_t* __restrict__ gamma,
+                                                 const bf16_t* __restrict__ beta, bf16_t* __restrict__ y,
+                                                 float* __restrict__ save_mean, float* __restrict__ save_rstd, long rows,
+                                                 int H, float eps, Drop drop) {
+    const int lane = threadIdx.x & 63, l32 = lane & 31;
+    const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+    const bool ok = row < rows;             // both halves take part in the DPP sums
+    const long rw = ok ? row : rows - 1;
+    uint4 xr[VPL], rr[VPL];
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        const int col = 256 * k + 8 * l32;
+        xr[k] = *reinterpret_cast<const uint4*>(x + rw * H + col);
+        if (res) rr[k] = *reinterpret_cast<const uint4*>(res + (rw % res_rows) * H + col);
+    }
+    float v[VPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        const int col = 256 * k + 8 * l32;
+        const uint32_t wx[4] = {xr[k].x, xr[k].y, xr[k].z, xr[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[k][2 * e] = __uint_as_float(wx[e] << 16);
+            v[k][2 * e + 1] = __uint_as_float(wx[e] & 0xffff0000u);
+        }
+        if (drop.thresh) {
+            drop4(drop, rw * H + col, v[k]);
+            drop4(drop, rw * H + col + 4, v[k] + 4);
+        }
+        if (res) {
+            const uint32_t wr[4] = {rr[k].x, rr[k].y, rr[k].z, rr[k].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[k][2 * e] += __uint_as_float(wr[e] << 16);
+                v[k][2 * e + 1] += __uint_as_float(wr[e] & 0xffff0000u);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[k][j];
+    }
+    const float mean = half_sum(s) / H;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[k][j] - mean; q += d * d; }
+    const float rstd = rsqrtf(half_sum(q) / H + eps);
+    if (!ok) return;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+        const int col = 256 * k + 8 * l32;
+        float g[8], b[8], o[8];
+        load8(gamma + col, g);
+        load8(beta + col, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + b[j];
+        store8(y + row * H + col, o);
+    }
+    if (l32 == 0) { save_mean[row] = mean; save_rstd[row] = rstd; }
+}
+
 // dx per row + dgamma/dbeta partials per block (ROWS_PER_BLK rows, 4 waves).
 // ADD: dadd (the gradient of this LayerNorm's input from its other consumer -- a pre-LN
 // block's residual branch) is added to dx in the same pass, before the column sums, so dx is
@@ -1363,9 +1438,23 @@ DDL_API int ddl_bn_bwd_pool(int dtype, const void* dy, const uint8_t* idx, const
 }
 
 // ---------------------------------------------------------------- LayerNorm
+// DDL_LN_FWD8=0: the wave-per-row bf16 forward (A/B timing)
+static bool ln_fwd8_enabled() {
+    static const bool on = [] { const char* e = getenv("DDL_LN_FWD8"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 template <typename T>
 static int ln_fwd_dispatch(const T* x, const T* res, long res_rows, const T* g, const T* b, T* y, float* mean,
                            float* rstd, long rows, int H, float eps, Drop drop, hipStream_t st) {
+    if constexpr (sizeof(T) == 2) {
+        if (ln_fwd8_enabled() && (H / 256 == 3 || H / 256 == 4)) {
+            const int grid8 = (int)((rows + 7) / 8);
+            if (H / 256 == 3) ln_fwd8_k<3><<<grid8, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop);
+            else ln_fwd8_k<4><<<grid8, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop);
+            return 0;
+        }
+    }
     const int grid = (int)((rows + 3) / 4);
     switch (H / 256) {
         case 1: ln_fwd_k<T, 1><<<grid, 256, 0, st>>>(x, res, res_rows, g, b, y, mean, rstd, rows, H, eps, drop); break;
