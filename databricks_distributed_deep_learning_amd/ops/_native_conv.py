@@ -82,8 +82,11 @@ _STREAM = os.environ.get("DDL_STREAM_GEMM", "1") != "0"
 # stage 2 only.  (256, 1024) is covered by the kernel (128-column slabs) but measured no faster than
 # the 256x256 kernel (benchmarks/stream_bench.py: 45 vs 36 us with statistics, 51 vs 52 with the
 # BN-backward epilogue: its A operand is the 103 MB side and two slabs read it twice)
-_STREAM_SHAPES = ((512, 128), (128, 512)) + (((1024, 256),) if os.environ.get("DDL_STREAM_GEMM", "1") != "2"
-                                             else ())
+# (256, 1024) -- stage 3's conv1 input gradient with the BN-backward epilogue only (forward with
+# statistics stays on the general GEMMs): ResNet-50 same-box backward 14.58 vs 14.63-14.64 ms (11,723-
+# 11,739 img/s; DDL_STREAM_GEMM=2, stage 2 only: 11,488-11,506)
+_STREAM_SHAPES = ((512, 128), (128, 512)) + (((1024, 256), (256, 1024)) if os.environ.get("DDL_STREAM_GEMM", "1")
+                                             != "2" else ())
 
 
 def _stream(a, b, c, part=None, res=None, bnb=None):
@@ -104,6 +107,8 @@ def _stream(a, b, c, part=None, res=None, bnb=None):
     if res is not None and (bnb is None or N not in (512, 1024) or tuple(res.shape) != (M, N)):
         return None
     if bnb is not None and bnb.x.numel() != M * N:
+        return None
+    if (N, K) == (256, 1024) and bnb is None:      # its forward (statistics): the general GEMMs are faster
         return None
     if part is not None and part.numel() < 256 * 2 * N:
         return None
