@@ -304,6 +304,87 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_k(const T* __restrict__ x
     }
 }
 
+// Row forms of the two kernels above and below for the ResNet stem: one block per output (input) row,
+// 32-bit index math.  The flat forms decompose a 64-bit element index per thread with 64-bit div /
+// mod (software sequences) and ran at ~2.3-2.5 TB/s on the 411 MB stem activation.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_relu_maxpool_rows_k(const T* __restrict__ x, const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, T* __restrict__ y,
+                                                              uint8_t* __restrict__ idx, uint8_t* __restrict__ mask,
+                                                              int H, int W, int C, int P, int Q) {
+    const int c8 = C / 8, n = blockIdx.x / P, p = blockIdx.x - n * P;
+    const long img = (long)n * H * W * C;
+    for (int t = threadIdx.x; t < Q * c8; t += 256) {
+        const int q = t / c8, cg = t - q * c8;
+        float sc[8], sh[8], best[8];
+        uint8_t arg[8];
+        load8(scale + cg * 8, sc);
+        load8(shift + cg * 8, sh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int h = 2 * p - 1 + r;
+            if (h < 0) continue;
+#pragma unroll
+            for (int s_ = 0; s_ < 3; ++s_) {
+                const int w = 2 * q - 1 + s_;
+                if (w < 0) continue;
+                const long e = img + ((long)h * W + w) * C + cg * 8;
+                float v[8];
+                load8(x + e, v);
+                uint32_t bits = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float a = to_f(from_f<T>(fmaxf(v[j] * sc[j] + sh[j], 0.f)));
+                    bits |= (a > 0.f ? 1u : 0u) << j;
+                    if (a > best[j] || (a != a)) { best[j] = a; arg[j] = (uint8_t)(r * 3 + s_); }
+                }
+                if (r >= 1 && s_ >= 1) mask[e >> 3] = (uint8_t)bits;   // an owned pixel
+            }
+        }
+        const long o = (((long)n * P + p) * Q + q) * C + cg * 8;
+        store8(y + o, best);
+        uint2 packed;
+        packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+        packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
+        *reinterpret_cast<uint2*>(idx + o) = packed;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_rows_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                          T* __restrict__ dx, int H, int W, int C, int P, int Q, int K,
+                                                          int S, int pad) {
+    const int c8 = C / 8, n = blockIdx.x / H, h = blockIdx.x - n * H;
+    const int p_lo = max(0, (h + pad - K + S) / S), p_hi = min(P - 1, (h + pad) / S);
+    for (int t = threadIdx.x; t < W * c8; t += 256) {
+        const int w = t / c8, cg = t - w * c8;
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int q_lo = max(0, (w + pad - K + S) / S), q_hi = min(Q - 1, (w + pad) / S);
+        for (int p = p_lo; p <= p_hi; ++p) {
+            const int r = h - (p * S - pad);
+            if (r < 0 || r >= K) continue;
+            for (int q = q_lo; q <= q_hi; ++q) {
+                const int s = w - (q * S - pad);
+                if (s < 0 || s >= K) continue;
+                const long o = (((long)n * P + p) * Q + q) * C + cg * 8;
+                float g[8];
+                load8(dy + o, g);
+                const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
+                const uint8_t want = (uint8_t)(r * K + s);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t word = j < 4 ? packed.x : packed.y;
+                    const uint8_t a = (uint8_t)(word >> (8 * (j & 3)));
+                    if (a == want) acc[j] += g[j];
+                }
+            }
+        }
+        store8(dx + (((long)n * H + h) * W + w) * C + cg * 8, acc);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                      T* __restrict__ dx, int N, int H, int W, int C, int P, int Q, int K,
@@ -530,10 +611,23 @@ DDL_API int ddl_maxpool_fwd(int dtype, const void* x, void* y, uint8_t* idx, int
                                                                      K, S, pad)));
     DDL_RETURN_LAUNCH();
 }
+// DDL_POOL_ROWS=0: the flat-index stem pooling kernels (A/B timing)
+static bool rows_form_enabled() {
+    static const bool on = [] { const char* e = getenv("DDL_POOL_ROWS"); return !(e && e[0] == '0'); }();
+    return on;
+}
 DDL_API int ddl_bn_relu_maxpool(int dtype, const void* x, const float* scale, const float* shift, void* y,
                                 uint8_t* idx, uint8_t* mask, int N, int H, int W, int C, int P, int Q, hipStream_t st) {
     if (C % 8 || H != 2 * P || W != 2 * Q) return -1;
     const long tot = (long)N * P * Q * (C / 8);
+    if ((long)N * P < (1L << 31) && rows_form_enabled()) {
+        DISPATCH_T(dtype,
+                   (bn_relu_maxpool_rows_k<bf16_t><<<N * P, 256, 0, st>>>((const bf16_t*)x, scale, shift, (bf16_t*)y,
+                                                                          idx, mask, H, W, C, P, Q)),
+                   (bn_relu_maxpool_rows_k<float><<<N * P, 256, 0, st>>>((const float*)x, scale, shift, (float*)y, idx,
+                                                                         mask, H, W, C, P, Q)));
+        DDL_RETURN_LAUNCH();
+    }
     DISPATCH_T(dtype,
                (bn_relu_maxpool_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)x, scale, shift, (bf16_t*)y,
                                                                           idx, mask, N, H, W, C, P, Q)),
@@ -545,6 +639,14 @@ DDL_API int ddl_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void*
                             int Q, int K, int S, int pad, hipStream_t st) {
     if (C % 8) return -1;
     const long tot = (long)N * H * W * (C / 8);
+    if ((long)N * H < (1L << 31) && rows_form_enabled()) {
+        DISPATCH_T(dtype,
+                   (maxpool_bwd_rows_k<bf16_t><<<N * H, 256, 0, st>>>((const bf16_t*)dy, idx, (bf16_t*)dx, H, W, C, P, Q,
+                                                                      K, S, pad)),
+                   (maxpool_bwd_rows_k<float><<<N * H, 256, 0, st>>>((const float*)dy, idx, (float*)dx, H, W, C, P, Q, K,
+                                                                     S, pad)));
+        DDL_RETURN_LAUNCH();
+    }
     DISPATCH_T(dtype,
                (maxpool_bwd_k<bf16_t><<<grid_for(tot), 256, 0, st>>>((const bf16_t*)dy, idx, (bf16_t*)dx, N, H, W, C,
                                                                       P, Q, K, S, pad)),
