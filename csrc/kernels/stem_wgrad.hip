@@ -1,0 +1,239 @@
+// Weight gradient of the ResNet stem (7x7 / stride-2 conv of the RGB image), computed on its
+// space-to-depth form (ops/_native_conv.py _StemConvS2D): the stride-1 4x4 convolution of
+// xs [N, P + 3, Q + 3, 16] (2x2 pixel blocks, 16 channels) giving dy [N, P, Q, 64], so
+//   dWs[k][r][s][c] = sum over (n, p, q) of dy[n][p][q][k] * xs[n][p + r][q + s][c].
+// As an implicit GEMM this is 64 x 256 x N*P*Q (3.2M pixels at batch 256): the CONVW kernel
+// gathers the 16 taps of every pixel (16 x 512 B of xs per 16 pixels) and split-K-reduces
+// 64 x 256 slabs -- it ran at ~320 us against ~90 us of HBM traffic (dy 411 MB + xs 108 MB).
+//
+// Here each workgroup (4 waves, one per CU: 144 KB of LDS) is persistent over a run of output
+// row pairs (n, p0), p0 even:
+//   * a stage holds dy rows p0, p0 + 1 (2 Q pixels x 128 B, one contiguous block of HBM) and
+//     xs rows p0 .. p0 + 4 (5 x (Q + 3) x 32 B, contiguous too), brought in by LDS-DMA as 48
+//     1-KB wave instructions (12 per wave, zero-page filler past the data), two stages in
+//     flight in a 3-slot ring;
+//   * the 16 taps are 16 shifted fragment reads of the same xs rows (no im2col): a 32-deep
+//     k-step is two 16-pixel segments (ds_read_b64_tr_b16 "lo" = segment 2ks, "hi" = 2ks + 1),
+//     a tap (r, s) is the byte offset (r (Q + 3) + s) * 32 into the row block;
+//   * wave w owns tap row r = w (4 taps x 16 channels) for all 64 output channels: 4 x 4
+//     v_mfma_f32_16x16x32_bf16 tiles per k-step, accumulated over all its tiles;
+//   * dy images use a 16-byte chunk swizzle c ^ 2 ((row >> 1) & 3), which spreads a segment's
+//     16 rows over all 32-byte bank slots twice (a conflict-free transposed read); xs reads
+//     are 512 contiguous bytes per instruction, conflict-free unswizzled;
+//   * one fp32 partial [64][256] per workgroup; stem_wgrad_reduce_k sums them and writes the
+//     gradient straight in the stem weight's layout [64][R][S][C] (the inverse space-to-depth
+//     of the tap/channel index), accumulating into the gradient sink.
+// Reference behaviour: the stem conv of torchvision's resnet50 (reference: SURVEY.md §2.3 --
+// the cuDNN weight-gradient kernel under loss.backward()).
+#include "ddl_common.h"
+
+namespace {
+
+constexpr int SK = 64;                 // output channels
+constexpr int SC = 16;                 // space-to-depth channels
+constexpr int NT = 256;
+constexpr int NI = 12;                 // LDS-DMA instructions per wave per stage
+constexpr int STAGE = 4 * NI * 1024;   // 48 KB
+constexpr int XS_OFF = 28672;          // xs block offset in a stage (dy block: 2 Q x 128 B, Q <= 112)
+constexpr int NSTAGE = 3;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ uint4 g_stem_zero[2];       // zero page for the filler lanes (never written)
+
+struct StemWParams {
+    const bf16_t* xs;      // [N, P + 3, Q + 3, 16]
+    const bf16_t* dy;      // [N, P, Q, 64]
+    float* part;           // [gridDim.x][64][256]
+    int P, tiles, chunk;   // tiles = N * P / 2 row pairs; [b * chunk, (b + 1) * chunk) per workgroup
+};
+
+__device__ __forceinline__ int dswz(int row) { return 2 * ((row >> 1) & 3); }
+
+// transposing LDS read the compiler does not track: the caller places the lgkmcnt waits
+__device__ __forceinline__ s16x4 ds_read_tr(uint32_t addr) {
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+__device__ __forceinline__ bf16x8 tr_frag(uint32_t a, uint32_t b) {
+    const s16x4 lo = ds_read_tr(a), hi = ds_read_tr(b);
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int QS>
+__global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
+    constexpr int Q = 16 * QS, WX = Q + 3;
+    constexpr int DYCH = 16 * Q;         // 16-byte chunks of dy per tile
+    constexpr int XSCH = 10 * WX;        // 16-byte chunks of xs per tile (5 rows)
+    static_assert(DYCH * 16 <= XS_OFF && XS_OFF + XSCH * 16 <= STAGE, "stage layout");
+    __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, pq = lane & 3;
+    const int HP = p.P >> 1, HX = p.P + 3;
+    const int t0 = blockIdx.x * p.chunk, nt = min(p.tiles, t0 + p.chunk) - t0;
+
+    // chunk u = 64 d + lane of wave instruction d = wv + 4 k lands at stage byte 16 u
+    auto stage = [&](int T, int slot) {
+        const int n = T / HP, p0 = (T - n * HP) * 2;
+        const bf16_t* dyt = p.dy + ((long)n * p.P + p0) * Q * SK;
+        const bf16_t* xst = p.xs + ((long)n * HX + p0) * WX * SC;
+        char* base = smem + slot * STAGE;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int d = wv + 4 * k, u = d * 64 + lane;
+            const bf16_t* src = (const bf16_t*)g_stem_zero;
+            if (u < DYCH) {
+                const int row = u >> 3;
+                src = dyt + row * SK + (((u & 7) ^ dswz(row)) << 3);
+            } else if (u >= XS_OFF / 16 && u < XS_OFF / 16 + XSCH) {
+                src = xst + (u - XS_OFF / 16) * 8;
+            }
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + d * 1024), 16, 0, 0);
+        }
+    };
+
+    // per-lane tr-read offsets.  dy (B operand, columns = output channels): segment row 4 g + q4,
+    // chunk 2 i + (pq >> 1) swizzled (the swizzle only sees row bits 1..2: the same for the hi
+    // segment, +16 rows, and every k-step, +32 rows).  xs (A operand, columns = the 16 channels
+    // of one tap): pixel 4 g + q4 of the segment, 8 pq bytes in; tap row r = wv.
+    uint32_t ao[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + q4;
+        ao[i] = r * 128 + (((2 * i + (pq >> 1)) ^ dswz(r)) << 4) + (pq & 1) * 8;
+    }
+    const uint32_t bo = XS_OFF + (4 * g + q4) * 32 + pq * 8 + wv * WX * 32;
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[s][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+    if (nt > 0) stage(t0, 0);
+    if (nt > 1) stage(t0 + 1, 1);
+    for (int T = 0; T < nt; ++T) {
+        // this tile's stage landed (the next one, if issued, may stay in flight)
+        if (T + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // every wave's reads of the slot recycled below finished before this barrier (lgkmcnt(0)
+        // ahead of the last k-step's MFMAs)
+        __builtin_amdgcn_s_barrier();
+        if (T + 2 < nt) stage(t0 + T + 2, (T + 2) % NSTAGE);
+        const uint32_t sb = lds0 + (T % NSTAGE) * STAGE;
+        bf16x8 fa[2][4], fb[2][4];
+        auto read_ks = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[4]) {
+            const uint32_t da = sb + ks * 4096;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[i] = tr_frag(da + ao[i], da + ao[i] + 2048);
+            // segment starts (pixel 32 ks and 32 ks + 16 of the row pair) in the xs row block
+            const int pa = 32 * ks, pb = pa + 16;
+            const int ra = pa / Q, rb = pb / Q;
+            const uint32_t xa = sb + bo + (ra * WX + pa - ra * Q) * 32;
+            const uint32_t xb = sb + bo + (rb * WX + pb - rb * Q) * 32;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) a[s] = tr_frag(xa + s * 32, xb + s * 32);
+        };
+        read_ks(0, fa[0], fb[0]);
+#pragma unroll
+        for (int ks = 0; ks < QS; ++ks) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            const int c = ks & 1;
+            if (ks + 1 < QS) read_ks(ks + 1, fa[c ^ 1], fb[c ^ 1]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[s][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c][s], fb[c][i], acc[s][i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // lane holds dWs[k = 16 i + (lane & 15)][tap 4 wv + s][channels 4 g .. 4 g + 3]
+    float* out = p.part + (long)blockIdx.x * SK * 256 + (lane & 15) * 256 + (4 * wv) * 16 + 4 * g;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(out + i * 16 * 256 + s * 16) = acc[s][i];
+}
+
+// dw[k][rr][ss][c] (+)= sum_b part[b][k][col], col = tap (rr / 2, ss / 2) * 16 + space-to-depth
+// channel ((rr & 1) * 2 + (ss & 1)) * 4 + c.  Block: 64 columns of one k x 4 partial groups.
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_k(const float* __restrict__ part, int G, void* out, int R,
+                                                           int S, int C, int out_f32, int accumulate) {
+    __shared__ float red[4][64];
+    const int t = threadIdx.x & 63, bg = threadIdx.x >> 6;
+    const int k = blockIdx.x >> 2, col = (blockIdx.x & 3) * 64 + t;
+    const float* src = part + (long)k * 256 + col;
+    float s0 = 0.f, s1 = 0.f;
+    int b = bg;
+    for (; b + 4 < G; b += 8) {
+        s0 += src[(long)b * SK * 256];
+        s1 += src[(long)(b + 4) * SK * 256];
+    }
+    if (b < G) s0 += src[(long)b * SK * 256];
+    red[bg][t] = s0 + s1;
+    __syncthreads();
+    if (bg != 0) return;
+    const float v = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+    const int tap = col >> 4, sub = (col >> 2) & 3, c = col & 3;
+    const int rr = 2 * (tap >> 2) + (sub >> 1), ss = 2 * (tap & 3) + (sub & 1);
+    if (rr >= R || ss >= S || c >= C) return;
+    const long o = (((long)k * R + rr) * S + ss) * C + c;
+    if (out_f32) {
+        float* d = (float*)out + o;
+        *d = accumulate ? *d + v : v;
+    } else {
+        bf16_t* d = (bf16_t*)out + o;
+        *d = f2bf(accumulate ? bf2f(*d) + v : v);
+    }
+}
+
+template <int QS>
+void launch_stem(const StemWParams& p, int g, hipStream_t st) {
+    hipLaunchKernelGGL(stem_wgrad_k<QS>, dim3(g), dim3(NT), 0, st, p);
+}
+
+}  // namespace
+
+// Stem weight gradient from the space-to-depth operands: xs [N, P + 3, Q + 3, 16], dy [N, P, Q, 64]
+// (bf16, contiguous, 16-byte aligned), P even, Q % 16 == 0, 16 <= Q <= 112.  dw: the stem weight's
+// gradient [64][R][S][C] (R, S <= 8, C <= 4; bf16 or fp32; accumulate: +=).  ws: >= grid * 64 * 256
+// floats (grid <= 0: 256).  Returns 0, -1 when the shape is not covered (nothing launched), or
+// -2 - hipError.
+DDL_API long ddl_stem_wgrad_ws(int grid) { return (long)(grid > 0 ? grid : 256) * SK * 256; }
+
+DDL_API int ddl_stem_wgrad(const void* xs, const void* dy, void* dw, int N, int P, int Q, int K, int R, int S, int C,
+                           float* ws, long ws_elems, int accumulate, int out_f32, int grid, hipStream_t stream) {
+    if (K != SK || N < 1 || P < 2 || P % 2 || Q % 16 || Q < 16 || Q > 112 || R < 1 || R > 8 || S < 1 || S > 8 ||
+        C < 1 || C > 4 || ((uintptr_t)xs & 15) || ((uintptr_t)dy & 15) || !ws)
+        return -1;
+    StemWParams p{};
+    p.xs = (const bf16_t*)xs;
+    p.dy = (const bf16_t*)dy;
+    p.P = P;
+    p.tiles = N * (P / 2);
+    int g = grid > 0 ? grid : 256;
+    g = std::min(g, p.tiles);
+    p.chunk = (p.tiles + g - 1) / g;
+    g = (p.tiles + p.chunk - 1) / p.chunk;
+    if (ws_elems < (long)g * SK * 256) return -1;
+    p.part = ws;
+    switch (Q / 16) {
+        case 1: launch_stem<1>(p, g, stream); break;
+        case 2: launch_stem<2>(p, g, stream); break;
+        case 3: launch_stem<3>(p, g, stream); break;
+        case 4: launch_stem<4>(p, g, stream); break;
+        case 5: launch_stem<5>(p, g, stream); break;
+        case 6: launch_stem<6>(p, g, stream); break;
+        default: launch_stem<7>(p, g, stream); break;
+    }
+    hipLaunchKernelGGL(stem_wgrad_reduce_k, dim3(SK * 4), dim3(256), 0, stream, (const float*)ws, g, dw, R, S, C,
+                       out_f32, accumulate);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -2 - (int)e;
+}

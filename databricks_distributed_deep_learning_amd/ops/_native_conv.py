@@ -553,6 +553,38 @@ def _s2d_weight_grad(dws, w_shape):
     return d[:, :R, :S, :C]
 
 
+_STEM_WGRAD = os.environ.get("DDL_STEM_WGRAD", "1") != "0"
+
+
+def _stem_wgrad_ok(xs, dy, ws_shape, w_shape) -> bool:
+    """Shapes the direct stem weight-gradient kernel (stem_wgrad.hip) covers."""
+    if not (_STEM_WGRAD and xs.is_cuda and dy.is_cuda):
+        return False
+    N, Hx, Wx, Cs = xs.shape
+    _, P, Q, K = dy.shape
+    return (tuple(ws_shape) == (64, 4, 4, 16) and Cs == 16 and K == 64 and Hx == P + 3 and Wx == Q + 3
+            and P % 2 == 0 and Q % 16 == 0 and 16 <= Q <= 112 and w_shape[1] <= 8 and w_shape[2] <= 8
+            and w_shape[3] <= 4 and xs.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+            and xs.is_contiguous() and dy.is_contiguous() and xs.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0)
+
+
+def _stem_wgrad(xs, dy, dw, accumulate, grid=0):
+    """Stem weight gradient straight from the space-to-depth operands into ``dw`` [64, R, S, C]
+    (the original weight layout; += with ``accumulate``): per-workgroup fp32 partials of the
+    4x4x16 taps + one reduce that also undoes the space-to-depth (stem_wgrad.hip)."""
+    N, _, _, _ = xs.shape
+    _, P, Q, _ = dy.shape
+    K, R, S, C = dw.shape
+    g = grid if grid > 0 else 256
+    ws = torch.empty(g * 64 * 256, dtype=torch.float32, device=xs.device)
+    rc = _lib.fn("ddl_stem_wgrad")(xs.data_ptr(), dy.data_ptr(), dw.data_ptr(), N, P, Q, K, R, S, C, ws.data_ptr(),
+                                   ws.numel(), int(accumulate), int(dw.dtype == torch.float32), int(grid),
+                                   _lib.stream())
+    if rc != 0:
+        raise RuntimeError(f"ddl_stem_wgrad failed: {rc}")
+    return dw
+
+
 class _StemConvS2D(torch.autograd.Function):
     """Stride-2 convolution of a <=4-channel image (the ResNet stem, 7x7/2 on RGB) as a
     stride-1 convolution of its 2x2 space-to-depth transform: 16 channels (16-byte
@@ -583,6 +615,16 @@ class _StemConvS2D(torch.autograd.Function):
             _, P, Q, _ = dy.shape
             if xs.shape[1] - ctx.ws_shape[1] + 1 != P or xs.shape[2] - ctx.ws_shape[2] + 1 != Q:
                 xs = xs[:, :P + ctx.ws_shape[1] - 1, :Q + ctx.ws_shape[2] - 1].contiguous()
+            if _stem_wgrad_ok(xs, dy, ctx.ws_shape, ctx.w_shape):
+                sink = grad_sink(ctx.w_param)
+                if sink is not None and tuple(sink.shape) == tuple(ctx.w_shape) and sink.is_contiguous() \
+                        and sink.dtype in (torch.bfloat16, torch.float32):
+                    _stem_wgrad(xs, dy, sink, accumulate=True)
+                    grad_ready(ctx.w_param)
+                    return None, None, None, None
+                dw = torch.empty(ctx.w_shape, dtype=dy.dtype, device=dy.device)
+                _stem_wgrad(xs, dy, dw, accumulate=False)
+                return None, dw, None, None
             dws = _wgrad(dy, xs, ctx.ws_shape, 1, 0)
             g = _s2d_weight_grad(dws, ctx.w_shape)
             sink = grad_sink(ctx.w_param)

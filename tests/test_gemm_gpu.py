@@ -372,7 +372,7 @@ def test_ffn_dgelu_handoff(M):
         assert _rel_err(t.grad, r.grad) < 3e-2, name
 
 
-@pytest.mark.parametrize("H,W", [(224, 224), (57, 61)])
+@pytest.mark.parametrize("H,W", [(224, 224), (57, 61), (128, 96)])
 def test_stem_space_to_depth(H, W):
     """7x7/2 RGB stem through the space-to-depth path: forward and weight gradient
     against fp32 F.conv2d (odd extents exercise the padded block row / column)."""
@@ -390,6 +390,32 @@ def test_stem_space_to_depth(H, W):
     y.backward(dy.to(torch.bfloat16))
     yr.backward(dy)
     assert _rel_err(w.grad, wr.grad.permute(0, 2, 3, 1)) < 2e-2
+
+
+@pytest.mark.parametrize("N,P,Q,grid", [(2, 8, 112, 0), (3, 6, 64, 4), (1, 4, 16, 0), (2, 112, 112, 7)])
+@pytest.mark.parametrize("out_dtype,accumulate", [(torch.bfloat16, False), (torch.float32, True)])
+def test_stem_wgrad_kernel(N, P, Q, grid, out_dtype, accumulate):
+    """Direct stem weight gradient (stem_wgrad.hip) on space-to-depth operands against the fp32
+    tap-by-tap reference, written in the original [64, 7, 7, 3] layout; grids that split the
+    row pairs unevenly, several row widths (tile templates), accumulate into an fp32 sink."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    torch.manual_seed(P * Q + N)
+    xs = torch.randn(N, P + 3, Q + 3, 16, device=dev).to(torch.bfloat16)
+    dy = torch.randn(N, P, Q, 64, device=dev).to(torch.bfloat16)
+    assert NC._stem_wgrad_ok(xs, dy, (64, 4, 4, 16), (64, 7, 7, 3))
+    ref = torch.empty(64, 4, 4, 16, device=dev)
+    xf, df = xs.float(), dy.float()
+    for r in range(4):
+        for s in range(4):
+            ref[:, r, s] = torch.einsum("npqk,npqc->kc", df, xf[:, r:r + P, s:s + Q])
+    ref = NC._s2d_weight_grad(ref, (64, 7, 7, 3))
+    base = torch.randn(64, 7, 7, 3, device=dev).to(out_dtype) if accumulate else None
+    dw = base.clone() if accumulate else torch.empty(64, 7, 7, 3, device=dev, dtype=out_dtype)
+    NC._stem_wgrad(xs, dy, dw, accumulate, grid=grid)
+    torch.cuda.synchronize()
+    want = ref + base.float() if accumulate else ref
+    assert _rel_err(dw, want) < 1e-2
 
 
 @pytest.mark.parametrize("splits", [8, 32, 64])
