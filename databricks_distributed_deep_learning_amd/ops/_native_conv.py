@@ -585,6 +585,39 @@ def _stem_wgrad(xs, dy, dw, accumulate, grid=0):
     return dw
 
 
+_STEM_FWD = os.environ.get("DDL_STEM_FWD", "1") != "0"
+
+
+def _stem_fwd_ok(xs, ws) -> bool:
+    """Shapes the direct stem forward kernel (stem_conv.hip) covers: output P x Q with P % 4 == 0,
+    Q % 16 == 0, 16 <= Q <= 112, 64 channels."""
+    if not (_STEM_FWD and xs.is_cuda):
+        return False
+    N, Hx, Wx, Cs = xs.shape
+    P, Q = Hx - 3, Wx - 3
+    return (tuple(ws.shape) == (64, 4, 4, 16) and Cs == 16 and P >= 4 and P % 4 == 0 and Q % 16 == 0
+            and 16 <= Q <= 112 and xs.dtype == torch.bfloat16 and ws.dtype == torch.bfloat16
+            and xs.is_contiguous() and ws.is_contiguous() and xs.data_ptr() % 16 == 0 and ws.data_ptr() % 16 == 0)
+
+
+def _stem_fwd(xs, ws, stats=None, grid=0):
+    """Stem forward on the space-to-depth operands (stem_conv.hip): y [N, P, Q, 64]; ``stats``
+    (ops.bridge.BNStats) receives the BatchNorm partial sums of y from the kernel."""
+    N, Hx, Wx, _ = xs.shape
+    P, Q = Hx - 3, Wx - 3
+    y = torch.empty(N, P, Q, 64, dtype=xs.dtype, device=xs.device)
+    use_stats = STATS_EPILOGUE and stats is not None
+    g = grid if grid > 0 else 256
+    part = torch.empty(g * 2 * 64, dtype=torch.float32, device=xs.device) if use_stats else None
+    rc = _lib.fn("ddl_stem_fwd")(xs.data_ptr(), ws.data_ptr(), y.data_ptr(), N, P, Q, 64, _lib.p(part), int(grid),
+                                 _lib.stream())
+    if rc < 0:
+        raise RuntimeError(f"ddl_stem_fwd failed: {rc}")
+    if part is not None:
+        stats.set(y, part, rc)
+    return y
+
+
 class _StemConvS2D(torch.autograd.Function):
     """Stride-2 convolution of a <=4-channel image (the ResNet stem, 7x7/2 on RGB) as a
     stride-1 convolution of its 2x2 space-to-depth transform: 16 channels (16-byte
@@ -600,7 +633,7 @@ class _StemConvS2D(torch.autograd.Function):
         ctx.ws_shape = ws.shape
         ctx.w_shape = w.shape
         # output extent: (H + 2p - R) / 2 + 1 = s2d extent - R2 + 1 for R = 2 R2 - 1
-        y = _fwd(xs, ws, 1, 0, stats=stats)
+        y = _stem_fwd(xs, ws, stats) if _stem_fwd_ok(xs, ws) else _fwd(xs, ws, 1, 0, stats=stats)
         N, H, W_, _ = x.shape
         K, R, S, _ = w.shape
         P, Q = (H + 2 * pad - R) // 2 + 1, (W_ + 2 * pad - S) // 2 + 1

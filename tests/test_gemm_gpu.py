@@ -392,6 +392,34 @@ def test_stem_space_to_depth(H, W):
     assert _rel_err(w.grad, wr.grad.permute(0, 2, 3, 1)) < 2e-2
 
 
+@pytest.mark.parametrize("N,P,Q,grid", [(2, 8, 112, 0), (3, 12, 64, 5), (1, 4, 16, 0), (2, 112, 112, 7),
+                                        (1, 8, 48, 0)])
+@pytest.mark.parametrize("with_stats", [False, True])
+def test_stem_fwd_kernel(N, P, Q, grid, with_stats):
+    """Direct stem forward (stem_conv.hip) on space-to-depth operands against fp32 F.conv2d,
+    and its BatchNorm partial sums against the sums of the stored bf16 output."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    torch.manual_seed(P + Q + N)
+    xs = torch.randn(N, P + 3, Q + 3, 16, device=dev).to(torch.bfloat16)
+    ws = (torch.randn(64, 4, 4, 16, device=dev) * 0.1).to(torch.bfloat16)
+    assert NC._stem_fwd_ok(xs, ws)
+
+    class Rec:
+        def set(self, y, part, rows):
+            self.part, self.rows = part, rows
+    rec = Rec() if with_stats else None
+    y = NC._stem_fwd(xs, ws, rec, grid=grid)
+    ref = F.conv2d(xs.float().permute(0, 3, 1, 2), ws.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    assert _rel_err(y, ref) < 1e-2
+    if with_stats:
+        part = rec.part[:rec.rows * 128].view(rec.rows, 2, 64).sum(0)
+        yf = y.float().reshape(-1, 64)
+        torch.testing.assert_close(part[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.shape[0] ** 0.5)
+        torch.testing.assert_close(part[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
 @pytest.mark.parametrize("N,P,Q,grid", [(2, 8, 112, 0), (3, 6, 64, 4), (1, 4, 16, 0), (2, 112, 112, 7)])
 @pytest.mark.parametrize("out_dtype,accumulate", [(torch.bfloat16, False), (torch.float32, True)])
 def test_stem_wgrad_kernel(N, P, Q, grid, out_dtype, accumulate):
