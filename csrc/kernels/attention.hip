@@ -57,9 +57,16 @@ __device__ __forceinline__ int swz_row(int r, int c) { return c ^ ((r >> 1) & 7)
 // rows on the same slots for the tr reads (2-way conflicts: ~32 % extra LDS cycles).
 __device__ __forceinline__ int swz_tr(int r, int c) { return c ^ (2 * ((r >> 1) & 3)); }
 
-template <bool TR>
+// dS^T images of the fused backward kernels: written as 8-byte pieces, one key row per lane (16 rows
+// x one chunk per half-wave pass) and read transposed (8 rows x 2 chunks per pass).  swz_tr repeats
+// its pattern every 8 rows, so rows r and r + 8 of a write pass collided (2-way: the 16.7 % LDS
+// bank conflicts of attn_bwd_fused_k); bit 3 of the row in the chunk's low bit separates them and
+// keeps the transposed reads conflict free.
+__device__ __forceinline__ int swz_ds(int r, int c) { return c ^ ((2 * ((r >> 1) & 3)) | ((r >> 3) & 1)); }
+
+template <bool TR, bool DS = false>
 __device__ __forceinline__ int lds_off(int r, int c) {
-    return r * ROWB + ((TR ? swz_tr(r, c) : swz_row(r, c)) << 4);
+    return r * ROWB + ((TR ? (DS ? swz_ds(r, c) : swz_tr(r, c)) : swz_row(r, c)) << 4);
 }
 
 // fragment: rows rbase..+15 (lane&15), k = 32kk + 8(lane>>4) + 0..7, from a row image
@@ -73,14 +80,14 @@ __device__ __forceinline__ bf16x8 frag_rows(const char* lds, int rbase, int kk) 
 // transposed fragment with the permuted k order used for accumulator operands:
 // lane l gets column cbase + (l&15) of rows  kb + 16h + 4g + {0..3}, h = 0,1
 // (kb = 32 s), i.e. element j <-> row kb + 16 (j>>2) + 4 g + (j&3).
-template <bool TR>
+template <bool TR, bool DS = false>
 __device__ __forceinline__ bf16x8 frag_tr(const char* lds, int kb, int cbase) {
     const int l = threadIdx.x & 63;
     const int g = l >> 4, q = (l >> 2) & 3, p = l & 3;
     const int col = cbase + 4 * p;
     const int ra = kb + 4 * g + q, rb = ra + 16;
-    const char* pa = lds + lds_off<TR>(ra, col >> 3) + (p & 1) * 8;
-    const char* pb = lds + lds_off<TR>(rb, col >> 3) + (p & 1) * 8;
+    const char* pa = lds + lds_off<TR, DS>(ra, col >> 3) + (p & 1) * 8;
+    const char* pb = lds + lds_off<TR, DS>(rb, col >> 3) + (p & 1) * 8;
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pa);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pb);
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -1014,7 +1021,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
             const int q0 = 16 * c + 4 * g;             // block c = (qc, j) = (c / 2, c % 2)
             char* img = q0 < 64 ? sT0 : sT1;
             const int qq = q0 & 63;
-            *reinterpret_cast<uint2*>(img + lds_off<true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[c];
+            *reinterpret_cast<uint2*>(img + lds_off<true, true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[c];
         }
     }
     __syncthreads();
@@ -1031,7 +1038,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
             if (!FULL && st >= nkc) break;
-            const bf16x8 sf = frag_tr<true>(img, 32 * st, cb);
+            const bf16x8 sf = frag_tr<true, true>(img, 32 * st, cb);
 #pragma unroll
             for (int db = 0; db < 4; ++db)
                 dq[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sK, 32 * st, 16 * db), sf, dq[db], 0, 0, 0);
@@ -1425,7 +1432,7 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
             const int q0 = 16 * c + 4 * g;
             char* img = q0 < 64 ? sT0 : sT1;
             const int qq = q0 & 63;
-            *reinterpret_cast<uint2*>(img + lds_off<true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[8 * half + c];
+            *reinterpret_cast<uint2*>(img + lds_off<true, true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[8 * half + c];
         }
         __syncthreads();
         const int qblk = 8 * half + qsub;
@@ -1439,7 +1446,7 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
 #pragma unroll
             for (int st = 0; st < 8; ++st) {
                 if (st < nch) {
-                    const bf16x8 sf = frag_tr<true>(img, 32 * st, cb);
+                    const bf16x8 sf = frag_tr<true, true>(img, 32 * st, cb);
 #pragma unroll
                     for (int i = 0; i < 2; ++i)
                         dq[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<true>(sK, 32 * st, 32 * dh + 16 * i),

@@ -74,7 +74,7 @@ def test_attention_fwd_bwd(B, S, H, masked):
     assert gerr < 3e-2 * q32.grad.abs().max().item() + 1e-2, gerr
 
 
-@pytest.mark.parametrize("S", [96, 97, 197, 256])   # odd S: pairs of score indices straddle rows; > 128: medium kernels
+@pytest.mark.parametrize("S", [96, 97, 197, 256, 300, 333])   # odd S: pairs of score indices straddle rows; > 128: medium kernels; > 256: tiled
 def test_attention_dropout_mask_parity(S):
     dev = gpu_device()
     from databricks_distributed_deep_learning_amd.ops import _native_attention as NA
