@@ -366,9 +366,9 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
     if constexpr (STATS) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        float* red = reinterpret_cast<float*>(smem);
-        if (tid < 2 * SK) red[tid] = 0.f;
-        __syncthreads();
+        // per-wave slots summed in wave order (LDS float atomics from four waves would make the
+        // statistics -- and training -- differ run to run in the last bits)
+        float* red = reinterpret_cast<float*>(smem);   // [wave][2][64]
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -376,12 +376,13 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
                 const float a = row16_sum(st_s[j][e]), b = row16_sum(st_q[j][e]);
                 if (r16 == 0) {
                     const int col = 32 * (j >> 1) + 8 * g + 4 * (j & 1) + e;
-                    atomicAdd(&red[col], a);
-                    atomicAdd(&red[SK + col], b);
+                    red[wv * 2 * SK + col] = a;
+                    red[wv * 2 * SK + SK + col] = b;
                 }
             }
         __syncthreads();
-        if (tid < 2 * SK) p.colstats[(long)blockIdx.x * 2 * SK + tid] = red[tid];
+        if (tid < 2 * SK)
+            p.colstats[(long)blockIdx.x * 2 * SK + tid] = ((red[tid] + red[2 * SK + tid]) + red[4 * SK + tid]) + red[6 * SK + tid];
     }
 }
 
