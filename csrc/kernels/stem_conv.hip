@@ -7,16 +7,18 @@
 // ---- forward
 // The implicit GEMM (M = 3.2M pixels, N = 64, K = 256) ran at ~285 us against ~90 us of HBM
 // traffic (y 411 MB + xs 108 MB): 64-wide tiles re-stage the weights per tile and gather every
-// xs pixel 16 times.  stem_fwd_k keeps the whole weight in registers (each wave: 8 k-steps x 4
-// 16-channel blocks of A fragments) and is persistent over output row quads (n, p0):
-//   * a stage holds xs rows p0 .. p0 + 6 (7 rows of 128 pixel slots x 32 B, LDS-DMA, 7 wave
-//     instructions per wave; 3-slot ring, two stages in flight); the 16-byte halves of a pixel
-//     are swapped on odd 8-pixel groups so a fragment read (16 consecutive pixels, one half) is
-//     conflict-free at any tap shift;
-//   * wave w computes output row p0 + w: per 16-pixel block, 8 ds_read_b128 (tap pair x channel
-//     half = one 32-deep k-step) and 32 v_mfma_f32_16x16x32_bf16 with the weight as the A operand,
-//     so a lane ends with 16 channels of one pixel: two 16-byte stores, 64 contiguous bytes per
-//     pixel per instruction (the weight rows are permuted to make them consecutive);
+// xs pixel 16 times.  stem_fwd_k keeps the weight in registers (each wave: 8 k-steps x 2
+// 16-channel blocks of A fragments) and is persistent over output row quads (n, p0), 8 waves
+// (two per SIMD) per workgroup:
+//   * a stage holds xs rows p0 .. p0 + 6 (7 rows of 128 pixel slots x 32 B, plus a zero-page
+//     filler row: 4 LDS-DMA instructions per wave; 3-slot ring, two stages in flight); the
+//     16-byte halves of a pixel are swapped on odd 8-pixel groups so a fragment read (16
+//     consecutive pixels, one half) is conflict-free at any tap shift;
+//   * wave w computes output row p0 + (w & 3), channels 32 (w >> 2) .. +31: per 16-pixel block,
+//     8 ds_read_b128 (tap pair x channel half = one 32-deep k-step) and 16 v_mfma_f32_16x16x32_bf16
+//     with the weight as the A operand, so a lane ends with 8 consecutive channels of one pixel:
+//     one 16-byte store, 64 contiguous bytes per pixel per instruction (the weight rows are
+//     permuted to make them consecutive);
 //   * optional BatchNorm statistics of the stored (bf16-rounded) output: per-lane sums over the
 //     workgroup's pixels, one [2][64] partial row per workgroup (the contract of conv3x3.hip).
 //
@@ -26,17 +28,17 @@
 // gathers the 16 taps of every pixel (16 x 512 B of xs per 16 pixels) and split-K-reduces
 // 64 x 256 slabs -- it ran at ~320 us against ~90 us of HBM traffic (dy 411 MB + xs 108 MB).
 //
-// Here each workgroup (4 waves, one per CU: 144 KB of LDS) is persistent over a run of output
-// row pairs (n, p0), p0 even:
+// Here each workgroup (8 waves, one workgroup per CU: 144 KB of LDS) is persistent over a run of
+// output row pairs (n, p0), p0 even:
 //   * a stage holds dy rows p0, p0 + 1 (2 Q pixels x 128 B, one contiguous block of HBM) and
 //     xs rows p0 .. p0 + 4 (5 x (Q + 3) x 32 B, contiguous too), brought in by LDS-DMA as 48
-//     1-KB wave instructions (12 per wave, zero-page filler past the data), two stages in
+//     1-KB wave instructions (6 per wave, zero-page filler past the data), two stages in
 //     flight in a 3-slot ring;
 //   * the 16 taps are 16 shifted fragment reads of the same xs rows (no im2col): a 32-deep
 //     k-step is two 16-pixel segments (ds_read_b64_tr_b16 "lo" = segment 2ks, "hi" = 2ks + 1),
 //     a tap (r, s) is the byte offset (r (Q + 3) + s) * 32 into the row block;
-//   * wave w owns tap row r = w (4 taps x 16 channels) for all 64 output channels: 4 x 4
-//     v_mfma_f32_16x16x32_bf16 tiles per k-step, accumulated over all its tiles;
+//   * wave w owns taps (w >> 1, 2 (w & 1) + {0, 1}) (2 taps x 16 channels) for all 64 output
+//     channels: 2 x 4 v_mfma_f32_16x16x32_bf16 tiles per k-step, accumulated over all its tiles;
 //   * dy images use a 16-byte chunk swizzle c ^ 2 ((row >> 1) & 3), which spreads a segment's
 //     16 rows over all 32-byte bank slots twice (a conflict-free transposed read); xs reads
 //     are 512 contiguous bytes per instruction, conflict-free unswizzled;
@@ -51,9 +53,10 @@ namespace {
 
 constexpr int SK = 64;                 // output channels
 constexpr int SC = 16;                 // space-to-depth channels
-constexpr int NT = 256;
-constexpr int NI = 12;                 // LDS-DMA instructions per wave per stage
-constexpr int STAGE = 4 * NI * 1024;   // 48 KB
+constexpr int NWV = 8;                 // waves per workgroup (two per SIMD)
+constexpr int NT = 64 * NWV;
+constexpr int NI = 6;                  // LDS-DMA instructions per wave per stage (weight gradient)
+constexpr int STAGE = NWV * NI * 1024; // 48 KB
 constexpr int XS_OFF = 28672;          // xs block offset in a stage (dy block: 2 Q x 128 B, Q <= 112)
 constexpr int NSTAGE = 3;
 
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
     const int HP = p.P >> 1, HX = p.P + 3;
     const int t0 = blockIdx.x * p.chunk, nt = min(p.tiles, t0 + p.chunk) - t0;
 
-    // chunk u = 64 d + lane of wave instruction d = wv + 4 k lands at stage byte 16 u
+    // chunk u = 64 d + lane of wave instruction d = wv + 8 k lands at stage byte 16 u
     auto stage = [&](int T, int slot) {
         const int n = T / HP, p0 = (T - n * HP) * 2;
         const bf16_t* dyt = p.dy + ((long)n * p.P + p0) * Q * SK;
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
         char* base = smem + slot * STAGE;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
-            const int d = wv + 4 * k, u = d * 64 + lane;
+            const int d = wv + NWV * k, u = d * 64 + lane;
             const bf16_t* src = (const bf16_t*)g_stem_zero;
             if (u < DYCH) {
                 const int row = u >> 3;
@@ -118,18 +121,19 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
     // per-lane tr-read offsets.  dy (B operand, columns = output channels): segment row 4 g + q4,
     // chunk 2 i + (pq >> 1) swizzled (the swizzle only sees row bits 1..2: the same for the hi
     // segment, +16 rows, and every k-step, +32 rows).  xs (A operand, columns = the 16 channels
-    // of one tap): pixel 4 g + q4 of the segment, 8 pq bytes in; tap row r = wv.
+    // of one tap): pixel 4 g + q4 of the segment, 8 pq bytes in; wave w: tap row w >> 1, tap
+    // columns 2 (w & 1) + {0, 1}.
     uint32_t ao[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int r = 4 * g + q4;
         ao[i] = r * 128 + (((2 * i + (pq >> 1)) ^ dswz(r)) << 4) + (pq & 1) * 8;
     }
-    const uint32_t bo = XS_OFF + (4 * g + q4) * 32 + pq * 8 + wv * WX * 32;
+    const uint32_t bo = XS_OFF + (4 * g + q4) * 32 + pq * 8 + (wv >> 1) * WX * 32 + 2 * (wv & 1) * 32;
 
-    f32x4 acc[4][4];
+    f32x4 acc[2][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[s][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -145,8 +149,8 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
         __builtin_amdgcn_s_barrier();
         if (T + 2 < nt) stage(t0 + T + 2, (T + 2) % NSTAGE);
         const uint32_t sb = lds0 + (T % NSTAGE) * STAGE;
-        bf16x8 fa[2][4], fb[2][4];
-        auto read_ks = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[4]) {
+        bf16x8 fa[2][2], fb[2][4];
+        auto read_ks = [&](int ks, bf16x8 (&a)[2], bf16x8 (&b)[4]) {
             const uint32_t da = sb + ks * 4096;
 #pragma unroll
             for (int i = 0; i < 4; ++i) b[i] = tr_frag(da + ao[i], da + ao[i] + 2048);
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
             const uint32_t xa = sb + bo + (ra * WX + pa - ra * Q) * 32;
             const uint32_t xb = sb + bo + (rb * WX + pb - rb * Q) * 32;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) a[s] = tr_frag(xa + s * 32, xb + s * 32);
+            for (int s = 0; s < 2; ++s) a[s] = tr_frag(xa + s * 32, xb + s * 32);
         };
         read_ks(0, fa[0], fb[0]);
 #pragma unroll
@@ -166,17 +170,17 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
             const int c = ks & 1;
             if (ks + 1 < QS) read_ks(ks + 1, fa[c ^ 1], fb[c ^ 1]);
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
+            for (int s = 0; s < 2; ++s)
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     acc[s][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c][s], fb[c][i], acc[s][i], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // lane holds dWs[k = 16 i + (lane & 15)][tap 4 wv + s][channels 4 g .. 4 g + 3]
-    float* out = p.part + (long)blockIdx.x * SK * 256 + (lane & 15) * 256 + (4 * wv) * 16 + 4 * g;
+    // lane holds dWs[k = 16 i + (lane & 15)][tap 2 wv + s][channels 4 g .. 4 g + 3]
+    float* out = p.part + (long)blockIdx.x * SK * 256 + (lane & 15) * 256 + (2 * wv) * 16 + 4 * g;
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(out + i * 16 * 256 + s * 16) = acc[s][i];
 }
@@ -220,9 +224,9 @@ void launch_stem(const StemWParams& p, int g, hipStream_t st) {
 
 // ====================================================================== forward
 constexpr int FROW = 4096;             // LDS row image: 128 pixel slots x 32 B
-constexpr int FROWS = 7;               // xs rows per stage (4 output rows + 3)
-constexpr int FSTAGE = FROWS * FROW;   // 28 KB
-constexpr int FNI = FROWS * FROW / 1024 / 4;   // LDS-DMA instructions per wave per stage (7)
+constexpr int FROWS = 8;               // xs rows per stage: 4 output rows + 3, and a zero-page filler row
+constexpr int FSTAGE = FROWS * FROW;   // 32 KB
+constexpr int FNI = FSTAGE / 1024 / NWV;   // LDS-DMA instructions per wave per stage (4)
 
 struct StemFParams {
     const bf16_t* xs;      // [N, P + 3, Q + 3, 16]
@@ -251,38 +255,38 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <int QS, bool STATS>
 __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
     constexpr int Q = 16 * QS, WX = Q + 3;
-    constexpr int NST = 2 * QS;          // 16-byte stores per wave per tile
+    constexpr int NST = QS;              // 16-byte stores per wave per tile
     static_assert(WX <= 128, "row image");
     __shared__ __attribute__((aligned(16))) char smem[NSTAGE * FSTAGE];
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
+    const int orow = wv & 3, ch = wv >> 2;   // wave: output row p0 + orow, channels 32 ch .. + 31
     const int QP = p.P >> 2, HX = p.P + 3;
     const int t0 = blockIdx.x * p.chunk, nt = min(p.tiles, t0 + p.chunk) - t0;
 
-    // weight fragments (A operand): row m of channel block j is output channel
-    // 32 (j >> 1) + 8 (m >> 2) + 4 (j & 1) + (m & 3); k-step t covers taps 2t, 2t + 1 (g >> 1) and
-    // channel half g & 1
-    bf16x8 wf[8][4];
+    // weight fragments (A operand): row m of channel block j (of the wave's half) is output channel
+    // 32 ch + 8 (m >> 2) + 4 j + (m & 3); k-step t covers taps 2t, 2t + 1 (g >> 1) and channel half g & 1
+    bf16x8 wf[8][2];
 #pragma unroll
     for (int t = 0; t < 8; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = 32 * (j >> 1) + 8 * (r16 >> 2) + 4 * (j & 1) + (r16 & 3);
+        for (int j = 0; j < 2; ++j) {
+            const int c = 32 * ch + 8 * (r16 >> 2) + 4 * j + (r16 & 3);
             wf[t][j] = *reinterpret_cast<const bf16x8*>(p.w + c * 256 + (2 * t + (g >> 1)) * 16 + 8 * (g & 1));
         }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // chunk u = 64 d + lane (d = wv + 4 k) of a stage: row u >> 8, pixel slot (u >> 1) & 127, stored
-    // half u & 1 = data half ^ bit 3 of the slot
+    // chunk u = 64 d + lane (d = wv + 8 k) of a stage: row u >> 8, pixel slot (u >> 1) & 127, stored
+    // half u & 1 = data half ^ bit 3 of the slot; row 7 is a zero-page filler (4 instructions per wave)
     auto stage = [&](int T, int slot) {
         const int n = T / QP, p0 = (T - n * QP) * 4;
         const bf16_t* xst = p.xs + ((long)n * HX + p0) * WX * SC;
         char* base = smem + slot * FSTAGE;
 #pragma unroll
         for (int k = 0; k < FNI; ++k) {
-            const int d = wv + 4 * k, u = d * 64 + lane;
+            const int d = wv + NWV * k, u = d * 64 + lane;
             const int row = u >> 8, px = (u >> 1) & 127, h = (u & 1) ^ ((px >> 3) & 1);
-            const bf16_t* src = px < WX ? xst + (row * WX + px) * SC + 8 * h : (const bf16_t*)g_stem_zero;
+            const bf16_t* src = px < WX && row < 7 ? xst + (row * WX + px) * SC + 8 * h : (const bf16_t*)g_stem_zero;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + d * 1024), 16, 0, 0);
         }
     };
@@ -295,9 +299,9 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
         off[tp] = x * 32 + (((g & 1) ^ ((x >> 3) & 1)) << 4);
     }
 
-    float st_s[4][4], st_q[4][4];
+    float st_s[2][4], st_q[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) st_s[j][e] = st_q[j][e] = 0.f;
 
@@ -314,8 +318,8 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
         __builtin_amdgcn_s_barrier();
         if (T + 2 < nt) stage(t0 + T + 2, (T + 2) % NSTAGE);
         const int TT = t0 + T, n = TT / QP, p0 = (TT - n * QP) * 4;
-        bf16_t* yrow = p.y + (((long)n * p.P + p0 + wv) * Q + r16) * SK + 8 * g;
-        const uint32_t rb = lds0 + (T % NSTAGE) * FSTAGE + wv * FROW;
+        bf16_t* yrow = p.y + (((long)n * p.P + p0 + orow) * Q + r16) * SK + 32 * ch + 8 * g;
+        const uint32_t rb = lds0 + (T % NSTAGE) * FSTAGE + orow * FROW;
         const uint32_t ra[2] = {rb + off[0], rb + off[1]};
         bf16x8 fb[2][8];
         auto read_mb = [&](auto mbc, bf16x8 (&b)[8]) {
@@ -332,19 +336,19 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
             __builtin_amdgcn_sched_barrier(0);
             constexpr int c = mb & 1;
             if constexpr (mb + 1 < QS) read_mb(std::integral_constant<int, mb + 1>{}, fb[c ^ 1]);
-            f32x4 acc[4];
+            f32x4 acc[2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < 2; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < 8; ++t)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 2; ++j)
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][j], fb[c][t], acc[j], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            // lane: pixel 16 mb + r16, channels 8 g + 4 (j & 1) + e (+32 for j >= 2)
-            uint32_t pk[4][2];
+            // lane: pixel 16 mb + r16, channels 32 ch + 8 g + 4 j + e
+            uint32_t pk[2][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 2; ++j) {
                 pk[j][0] = pack2bf(acc[j][0], acc[j][1]);
                 pk[j][1] = pack2bf(acc[j][2], acc[j][3]);
                 if constexpr (STATS) {
@@ -359,25 +363,24 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
             }
             bf16_t* dst = yrow + mb * 16 * SK;
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
-            *reinterpret_cast<uint4*>(dst + 32) = make_uint4(pk[2][0], pk[2][1], pk[3][0], pk[3][1]);
             __builtin_amdgcn_sched_barrier(0);
         });
     }
     if constexpr (STATS) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        // per-wave slots summed in wave order (LDS float atomics from four waves would make the
+        // per-row slots summed in row order (LDS float atomics from four waves would make the
         // statistics -- and training -- differ run to run in the last bits)
-        float* red = reinterpret_cast<float*>(smem);   // [wave][2][64]
+        float* red = reinterpret_cast<float*>(smem);   // [output row][2][64]
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const float a = row16_sum(st_s[j][e]), b = row16_sum(st_q[j][e]);
                 if (r16 == 0) {
-                    const int col = 32 * (j >> 1) + 8 * g + 4 * (j & 1) + e;
-                    red[wv * 2 * SK + col] = a;
-                    red[wv * 2 * SK + SK + col] = b;
+                    const int col = 32 * ch + 8 * g + 4 * j + e;
+                    red[orow * 2 * SK + col] = a;
+                    red[orow * 2 * SK + SK + col] = b;
                 }
             }
         __syncthreads();
