@@ -74,6 +74,7 @@ struct DuoParams {
     int splits, kt_per_split;
     bf16_t* ws;
     int accumulate;
+    int nt_store;       // DDL_DUO_NT bits (A/B timing): 1 = the pre-activation (aux) image, 2 = C, stored non-temporal
 };
 
 __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5); }
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
     }
     // whole-row stores of the image: wave w takes rows 4 it + (l >> 4) of its 64-row quarter, lane
     // chunk l & 15 (16 B); 16 instructions per wave, each 4 rows x 256 B
-    auto store_image = [&](bf16_t* dst, long ld, uint32_t bytes, bool acc_c) {
+    auto store_image = [&](bf16_t* dst, long ld, uint32_t bytes, bool acc_c, bool nt = false) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         BARRIER();
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)bytes, 0x00020000);
@@ -463,7 +464,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
                 for (int e = 0; e < 4; ++e)
                     v[e] = pack2bf(lo_f(v[e]) + lo_f(o[e]), hi_f(v[e]) + hi_f(o[e]));
             }
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+            if (nt) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);   // cache policy: nt
+            else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
         }
     };
     if (p.splits > 1) {            // bf16 partial tile of this split
@@ -471,7 +473,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
         return;
     }
     if (EK == E_GELU && p.aux) {
-        store_image(p.aux, p.ldc, cbytes, false);
+        store_image(p.aux, p.ldc, cbytes, false, (p.nt_store & 1) != 0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         BARRIER();                                     // every image read done before it is rewritten
 #pragma unroll
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
             for (int j = 0; j < 4; ++j)
                 *reinterpret_cast<uint2*>(smem + img_off(i, j)) = make_uint2(yk[i][j][0], yk[i][j][1]);
     }
-    store_image(p.C, p.ldc, cbytes, p.accumulate != 0);
+    store_image(p.C, p.ldc, cbytes, p.accumulate != 0, (p.nt_store & 2) != 0);
 }
 
 // split-K reduce of the weight-gradient path: C (+)= sum of the bf16 partial tiles, 8 columns per
@@ -572,6 +574,11 @@ DDL_API int ddl_gemm_duo(int mode, const void* A, long lda, const void* B, long 
     p.bias = (const bf16_t*)bias; p.res = (const bf16_t*)res; p.aux = (bf16_t*)aux; p.colstats = colstats;
     p.bn_mask = bn.mask; p.bn_mean = bn.mean; p.bn_istd = bn.istd;
     p.splits = 1;
+    // default 1: the pre-activation (read again only by the backward) leaves non-temporal --
+    // BERT-base +0.25-0.35 % same-box (profiles/duo_nt_ab.log); the GELU output (the next GEMM's
+    // operand) keeps the default policy
+    static const int nt_bits = getenv("DDL_DUO_NT") ? atoi(getenv("DDL_DUO_NT")) : 1;
+    p.nt_store = nt_bits;
     p.kt_per_split = K / DBK;
     p.tiles_m = (M + TM - 1) / TM;
     p.tiles_n = N / TN;
