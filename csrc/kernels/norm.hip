@@ -1091,12 +1091,13 @@ __global__ __launch_bounds__(1024) void ln_colsum_k(const float* __restrict__ pa
 // the slice rows stays one round trip of 16 row lanes x 8 (ws holds S x 2C floats)
 static int fin_slices(int nblk) { return std::max(1, std::min(128, (nblk + FIN_RPS - 1) / FIN_RPS)); }
 static int fin_rps(int nblk) { return (nblk + fin_slices(nblk) - 1) / fin_slices(nblk); }
-// Measured in-model (profiles/kernels_r50.md, round 5): the merged launch takes 7.6-8.3 us -- its
-// two agent-scope fences cost about what the saved round trips gain -- so it replaces only the
-// TWO launches of the collapse path (> COLLAPSE_OVER rows: 5 + 6.7 us); up to that the single
-// finalize workgroup reads every row itself.  DDL_BN_MERGED_FIN=0: never, =2: always (A/B).
+// The merged launch took 7.6-8.3 us against 6.7 us for one finalize workgroup on <= 512 rows in
+// the round-5 kernel tables, but whole-step A/B prefers it for every row count: ResNet-50 +0.3 %
+// same-box, BERT-base neutral (profiles/merged_fin_ab.log) -- the single workgroup's long tail
+// delays the dependent apply launch.  DDL_BN_MERGED_FIN=0: never, =1: above 512 rows only, 2:
+// always (default).
 static int merged_mode() {
-    static const int m = [] { const char* e = getenv("DDL_BN_MERGED_FIN"); return e ? atoi(e) : 1; }();
+    static const int m = [] { const char* e = getenv("DDL_BN_MERGED_FIN"); return e ? atoi(e) : 2; }();
     return m;
 }
 static bool merged_finalize(int nblk) {
