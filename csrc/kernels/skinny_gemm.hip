@@ -56,7 +56,7 @@ struct SkParams {
 };
 
 __device__ __forceinline__ void glds(const bf16_t* g, char* dst) {
-    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 2);   // nt: streamed once
 }
 __device__ __forceinline__ bf16x8 ds_read16(uint32_t addr) {
     bf16x8 v;

@@ -53,7 +53,7 @@ struct StParams {
 };
 
 __device__ __forceinline__ void glds(const void* g, char* dst, int bytes) {
-    if (bytes == 16) __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 16, 0, 0);
+    if (bytes == 16) __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 16, 0, 2);   // nt: streamed once
     else __builtin_amdgcn_global_load_lds(g, (lds_void*)dst, 4, 0, 0);
 }
 __device__ __forceinline__ bf16x8 ds_read16(uint32_t addr) {
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(512, 1) void stream_wgrad_k(WgParams p) {
             const int col = (isA ? pnl : pnl - PA) * 128 + 8 * c;
             const bool ok = k < k1 && col < (isA ? M : N);
             const bf16_t* src = ok ? (isA ? p.A + k * p.lda + col : p.B + k * p.ldb + col) : p.zero;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + pnl * PANEL + q * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + pnl * PANEL + q * 1024), 16, 0, 2);
         }
     };
     f32x4 acc[FI][FJ];
