@@ -75,7 +75,7 @@ __device__ __forceinline__ bf16x8 ds_read16(uint32_t addr) {
 }
 
 __device__ __forceinline__ void glds(const bf16_t* g, char* dst) {
-    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 2);   // nt: rows are staged once
 }
 
 // LDS-DMA of input row h of image n into ring slot `slot`: W/8 wave instructions of

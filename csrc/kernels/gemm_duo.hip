@@ -81,6 +81,8 @@ __device__ __forceinline__ int swz_kc(int b) { return b ^ (((b >> 9) & 1) << 5);
 __device__ __forceinline__ int swz_ko(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
 __device__ __forceinline__ void glds(const bf16_t* g, char* dst) {
+    // (default cache policy: the implicit-GEMM convolution re-reads every input pixel once per tap
+    // -- the non-temporal policy cost ResNet-50 2 %, profiles/dma_nt_ab.log)
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)dst, 16, 0, 0);
 }
 __device__ __forceinline__ s16x4 ds_read_tr(lds_v4* __restrict__ p) {

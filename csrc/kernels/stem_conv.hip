@@ -114,7 +114,7 @@ __global__ __launch_bounds__(NT, 1) void stem_wgrad_k(StemWParams p) {
             } else if (u >= XS_OFF / 16 && u < XS_OFF / 16 + XSCH) {
                 src = xst + (u - XS_OFF / 16) * 8;
             }
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + d * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + d * 1024), 16, 0, 2);   // nt
         }
     };
 
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(NT, 1) void stem_fwd_k(StemFParams p) {
             const int d = wv + NWV * k, u = d * 64 + lane;
             const int row = u >> 8, px = (u >> 1) & 127, h = (u & 1) ^ ((px >> 3) & 1);
             const bf16_t* src = px < WX && row < 7 ? xst + (row * WX + px) * SC + 8 * h : (const bf16_t*)g_stem_zero;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + d * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(base + d * 1024), 16, 0, 2);   // nt
         }
     };
     // B fragment (pixels = columns): lane reads pixel 16 mb + r16 + s of tap row r, s = 2 (t & 1) +
