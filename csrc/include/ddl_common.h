@@ -43,6 +43,25 @@ __device__ __forceinline__ void load8(const bf16_t* p, float* v) {
         v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
 }
+// the same load with the non-temporal cache policy: for a pass that is the LAST reader of a tensor
+// too large for the caches to keep anyway
+__device__ __forceinline__ void load8_nt(const bf16_t* p, float* v) {
+    typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
+    const u32v4 u = __builtin_nontemporal_load(reinterpret_cast<const u32v4*>(p));
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+__device__ __forceinline__ void load8_nt(const float* p, float* v) {
+    typedef float f32v4 __attribute__((ext_vector_type(4)));
+    const f32v4 a = __builtin_nontemporal_load(reinterpret_cast<const f32v4*>(p));
+    const f32v4 b = __builtin_nontemporal_load(reinterpret_cast<const f32v4*>(p) + 1);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 __device__ __forceinline__ void store8(bf16_t* p, const float* v) {
     uint4 u;
     u.x = pack2bf(v[0], v[1]);

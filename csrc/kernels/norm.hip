@@ -451,9 +451,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_rows_k(const T* __restrict__
         float g[4][8], xv[4][8];
         uint32_t bits[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            load8(dy + (r + u * rs) * C + cg * 8, g[u]);
-            load8(x + (r + u * rs) * C + cg * 8, xv[u]);
+        for (int u = 0; u < 4; ++u) {   // the last reads of dy and x: non-temporal
+            load8_nt(dy + (r + u * rs) * C + cg * 8, g[u]);
+            load8_nt(x + (r + u * rs) * C + cg * 8, xv[u]);
             bits[u] = RELU ? mask[(r + u * rs) * tpr + cg] : 0xffu;
         }
 #pragma unroll
