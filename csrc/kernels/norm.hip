@@ -187,9 +187,9 @@ __global__ __launch_bounds__(256) void bn_apply_rows_k(const T* __restrict__ x, 
     for (; r + 3 * rs < M; r += 4 * rs) {
         float v[4][8], rv[4][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            load8(x + (r + u * rs) * C + cg * 8, v[u]);
-            if (RES) load8(res + (r + u * rs) * C + cg * 8, rv[u]);
+        for (int u = 0; u < 4; ++u) {   // non-temporal: read again only by the backward, much later
+            load8_nt(x + (r + u * rs) * C + cg * 8, v[u]);
+            if (RES) load8_nt(res + (r + u * rs) * C + cg * 8, rv[u]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) one(v[u], rv[u], r + u * rs);
@@ -243,9 +243,9 @@ __global__ __launch_bounds__(256) void bn_apply2_rows_k(const T* __restrict__ x,
     for (; r + 3 * rs < M; r += 4 * rs) {
         float v[4][8], rv[4][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            load8(x + (r + u * rs) * C + cg * 8, v[u]);
-            load8(x2 + (r + u * rs) * C + cg * 8, rv[u]);
+        for (int u = 0; u < 4; ++u) {   // non-temporal: read again only by the backward, much later
+            load8_nt(x + (r + u * rs) * C + cg * 8, v[u]);
+            load8_nt(x2 + (r + u * rs) * C + cg * 8, rv[u]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) one(v[u], rv[u], r + u * rs);
