@@ -324,8 +324,8 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_partial_k(const T* __restrict__ 
 #pragma unroll 2
     for (long r = r0 + rr; r < r1; r += rpi) {
         float g[8], xv[8];
-        load8(dy + r * C + cg * 8, g);
-        load8(x + r * C + cg * 8, xv);
+        load8_nt(dy + r * C + cg * 8, g);
+        load8_nt(x + r * C + cg * 8, xv);
         const uint32_t bits = RELU ? mask[r * tpr + cg] : 0xffu;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
