@@ -191,7 +191,8 @@ def test_stem_bn_relu_maxpool(shape, fused_bwd, monkeypatch):
     torch.testing.assert_close(res[0][5], res[1][5])
 
 
-@pytest.mark.parametrize("nblk,C", [(300, 64), (3000, 512), (1057, 2048), (128, 256), (129, 64), (20000, 64)])
+@pytest.mark.parametrize("nblk,C", [(300, 64), (3000, 512), (1057, 2048), (128, 256), (129, 64), (20000, 64), (1, 64),
+                                    (2, 256), (5, 2048), (64, 128)])
 def test_bn_finalize_from_many_partial_rows(nblk, C):
     """Many GEMM-epilogue partial rows -> BatchNorm forward statistics and backward coefficients
     (the merged multi-workgroup finalize: 128-row slices + last-arriver combine; 129 rows = a
