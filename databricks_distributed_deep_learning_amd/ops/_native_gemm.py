@@ -389,7 +389,10 @@ _TUNE = os.environ.get("DDL_GEMM_TUNE", "1") != "0"
 _PREFER = os.environ.get("DDL_GEMM_PREFER", "swg:1.3")
 _TUNE_ROUNDS = max(1, int(os.environ.get("DDL_GEMM_TUNE_ROUNDS", "5")))   # interleaved timing rounds per candidate
 _TUNE_COLD = os.environ.get("DDL_GEMM_TUNE_COLD", "1") != "0"             # time candidates from evicted caches
-_ONLINE = os.environ.get("DDL_GEMM_TUNE_ONLINE", "0") == "1"              # in-model tuning during warm-up (opt-in)
+# in-model tuning during warm-up: "1" always, "0" never, unset: the caller's default (the trainer turns it
+# on for transformer models, whose GEMM operands stay cache-resident in-model -- see online_tuning)
+_ONLINE_ENV = os.environ.get("DDL_GEMM_TUNE_ONLINE")
+_ONLINE = _ONLINE_ENV == "1"
 # optional persistent cache (JSON): later processes skip the timing runs
 _CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
 
@@ -584,9 +587,13 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
 # compute stream, read back once per step) and keeps the one with the lowest median in-model time.
 # It was built when the isolated tuner kept the BERT-base weight-gradient GEMMs on the 128x128
 # kernel; the cause turned out to be register spills in the 256x256 kernel's TN loop
-# (profiles/gemm_spills_r04.md), and with those fixed both tuners pick the same plan.  It stays off
-# by default because the candidates differ in split-K summation order: warm-up steps then round
-# differently than in a process whose tune cache is already warm (runs are not bit-reproducible).
+# (profiles/gemm_spills_r04.md).  Round 5: the isolated tuner times every candidate on COLD caches,
+# which is right for ResNet's 100-411 MB activations but not for transformer GEMMs, whose operands stay
+# in the 256 MB last-level cache in-model: in-model tuning picks plans worth +2.2 % on BERT-base
+# (and -0.7 % on ResNet-50; profiles/online_tune_ab.log).  The trainer therefore turns it on for
+# transformer models (default=True below) and leaves CNNs on the isolated tuner.  The price: warm-up
+# steps cycle through candidates with different split-K summation orders, so those steps round
+# differently than in a process whose tune cache is already warm.
 _online_active = False
 _online: dict = {}          # key -> {"cands": [...], "n": calls, "pending": [(cand, e0, e1)], "samples": {}}
 _online_last = None         # (key, cand) of the call _choose just routed online
@@ -599,13 +606,15 @@ def online_stats() -> dict:
 
 
 @contextlib.contextmanager
-def online_tuning(enabled: bool = True):
+def online_tuning(enabled: bool = True, default: bool = False):
     """Tune untuned GEMM signatures from their in-model calls inside the block (the trainer's
     warm-up steps); call :func:`online_collect` after each step.  On exit every signature seen
-    gets its in-model argmin (:func:`online_finish`)."""
+    gets its in-model argmin (:func:`online_finish`).  ``default``: whether to tune in-model when
+    DDL_GEMM_TUNE_ONLINE is unset (the trainer passes True for transformer models)."""
     global _online_active
     prev = _online_active
-    _online_active = bool(enabled) and _TUNE and _ONLINE and torch.cuda.is_available()
+    want = _ONLINE or (_ONLINE_ENV is None and default)
+    _online_active = bool(enabled) and _TUNE and want and torch.cuda.is_available()
     try:
         yield
     finally:

@@ -266,10 +266,11 @@ class Trainer:
         steps = c.steps if steps is None else steps
         warmup = c.warmup_steps if warmup is None else warmup
         self.model.train()
-        # DDL_GEMM_TUNE_ONLINE=1: untuned GEMM signatures pick their kernels from their own calls
-        # in these warm-up steps (ops/_native_gemm.py online_tuning); otherwise a no-op
+        # untuned GEMM signatures of transformer models pick their kernels from their own calls in
+        # these warm-up steps (ops/_native_gemm.py online_tuning; DDL_GEMM_TUNE_ONLINE=0/1 overrides)
         from ..ops import _native_gemm
-        with _native_gemm.online_tuning(enabled=self.device.type == "cuda"):
+        transformer = c.model.startswith(("bert", "vit", "gpt", "t5", "roberta"))
+        with _native_gemm.online_tuning(enabled=self.device.type == "cuda", default=transformer):
             for _ in range(warmup):
                 self.train_step()
                 _native_gemm.online_collect()
