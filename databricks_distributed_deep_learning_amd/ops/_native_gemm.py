@@ -595,6 +595,7 @@ def _tune(key, mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, conv_arr, 
 # steps cycle through candidates with different split-K summation orders, so those steps round
 # differently than in a process whose tune cache is already warm.
 _online_active = False
+_online_max_bytes = float("inf")   # signatures touching more operand + output bytes stay on the isolated tuner
 _online: dict = {}          # key -> {"cands": [...], "n": calls, "pending": [(cand, e0, e1)], "samples": {}}
 _online_last = None         # (key, cand) of the call _choose just routed online
 _online_count = {"tuned": 0, "samples": 0}
@@ -606,21 +607,23 @@ def online_stats() -> dict:
 
 
 @contextlib.contextmanager
-def online_tuning(enabled: bool = True, default: bool = False):
+def online_tuning(enabled: bool = True, default: bool = False, max_mb: float = float("inf")):
     """Tune untuned GEMM signatures from their in-model calls inside the block (the trainer's
     warm-up steps); call :func:`online_collect` after each step.  On exit every signature seen
     gets its in-model argmin (:func:`online_finish`).  ``default``: whether to tune in-model when
-    DDL_GEMM_TUNE_ONLINE is unset (the trainer passes True for transformer models)."""
-    global _online_active
-    prev = _online_active
+    DDL_GEMM_TUNE_ONLINE is unset; ``max_mb``: only signatures whose operands + output stay under
+    it (cache-resident in-model) are tuned in-model, the others on the isolated cold-cache tuner."""
+    global _online_active, _online_max_bytes
+    prev, prev_max = _online_active, _online_max_bytes
     want = _ONLINE or (_ONLINE_ENV is None and default)
     _online_active = bool(enabled) and _TUNE and want and torch.cuda.is_available()
+    _online_max_bytes = max_mb * 2 ** 20
     try:
         yield
     finally:
         if _online_active:
             online_finish()
-        _online_active = prev
+        _online_active, _online_max_bytes = prev, prev_max
 
 
 def online_collect() -> None:
@@ -701,7 +704,8 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
         key = f"{mode}|{M}|{N}|{K}|{lda}|{ldb}|{ldc}|{tuple(conv) if conv is not None else ''}|{int(row_remap)}|" \
               f"{act}|{C.dtype}|{int(bias is not None)}|{int(colstats is not None)}|{int(residual is not None)}"
         choice = _tuned.get(key)
-        if choice is None and online_ok and _online_active and not torch.cuda.is_current_stream_capturing():
+        if choice is None and online_ok and _online_active and not torch.cuda.is_current_stream_capturing() \
+                and (A.numel() + B.numel() + C.numel()) * C.element_size() <= _online_max_bytes:
             global _online_last
             st = _online.get(key)
             if st is None:

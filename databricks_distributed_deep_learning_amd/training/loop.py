@@ -270,7 +270,9 @@ class Trainer:
         # these warm-up steps (ops/_native_gemm.py online_tuning; DDL_GEMM_TUNE_ONLINE=0/1 overrides)
         from ..ops import _native_gemm
         transformer = c.model.startswith(("bert", "vit", "gpt", "t5", "roberta"))
-        with _native_gemm.online_tuning(enabled=self.device.type == "cuda", default=transformer):
+        online_mb = float(os.environ.get("DDL_GEMM_ONLINE_MAX_MB", "inf" if transformer else "0"))
+        with _native_gemm.online_tuning(enabled=self.device.type == "cuda", default=online_mb > 0,
+                                        max_mb=online_mb):
             for _ in range(warmup):
                 self.train_step()
                 _native_gemm.online_collect()
