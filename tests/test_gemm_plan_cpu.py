@@ -97,6 +97,26 @@ def test_online_tuning_commits_in_model_argmin(monkeypatch):
     assert NG._timings.pop(key)[("small", 2)] == 6.0
 
 
+def test_online_tuning_default_and_byte_gate(monkeypatch):
+    """DDL_GEMM_TUNE_ONLINE unset: the caller's default decides (the trainer passes True for
+    transformer models); "0" / "1" override it; max_mb keeps signatures over the gate on the
+    isolated tuner and is restored on exit."""
+    monkeypatch.setattr(NG, "_TUNE", True)
+    monkeypatch.setattr(NG.torch.cuda, "is_available", lambda: True)
+    for env, default, want in ((None, True, True), (None, False, False), ("0", True, False), ("1", False, True)):
+        monkeypatch.setattr(NG, "_ONLINE_ENV", env)
+        monkeypatch.setattr(NG, "_ONLINE", env == "1")
+        with NG.online_tuning(True, default=default, max_mb=64):
+            assert NG._online_active == want, (env, default)
+            assert NG._online_max_bytes == 64 * 2 ** 20
+        assert not NG._online_active and NG._online_max_bytes == float("inf")
+    # the trainer's rule: transformers tune in-model with no gate, CNNs stay on the isolated tuner
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    for preset, online in (("bert_base_ddp", True), ("vit_b16", True), ("resnet50_ddp", False)):
+        m = get_preset(preset).model
+        assert m.startswith(("bert", "vit", "gpt", "t5", "roberta")) == online, m
+
+
 def test_wg_candidate(monkeypatch):
     """The 4-wave weight-gradient kernel is offered for plain TN GEMMs inside its contract
     (M % 256, N % 128, K % 128) -- BERT-base's four weight gradients -- and nowhere else."""
