@@ -487,6 +487,139 @@ __global__ __launch_bounds__(256) void embed_bwd_k(const int64_t* __restrict__ i
         atomicAdd(acc + ids[t] * D + d, to_f(dy[i]));
     }
 }
+// Deterministic embedding backward over the ids sorted stably on the host side (s = sorted ids,
+// pi = their token positions).  One wave per chunk of EMB_CH sorted positions sums every run of equal
+// ids inside the chunk in token order (fp32, 8 columns per lane, column slabs of 512).  A run that
+// starts and ends inside the chunk is written straight into dw; a piece of a run that crosses a chunk
+// edge goes to part[chunk][0] (the chunk's head piece: the run began earlier) or part[chunk][1] (its
+// tail piece: the run begins here and continues), and embed_bwd_join_k adds the pieces in chunk order.
+// No atomics (the same bits every run) and no V x D fp32 buffer to fill and cast.
+constexpr int EMB_CH = 16;
+
+template <typename T>
+__device__ __forceinline__ void emb_row_out(T* __restrict__ dst, const float* a, int accumulate) {
+    float o[8];
+    if (accumulate) {
+        load8(dst, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += a[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = a[j];
+    }
+    store8(dst, o);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_seg_k(const int* __restrict__ s, const int64_t* __restrict__ pi,
+                                                       const T* __restrict__ dy, T* __restrict__ dw,
+                                                       float* __restrict__ part, long n, int D, int accumulate) {
+    const long chunk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long c0 = chunk * EMB_CH;
+    if (c0 >= n) return;                                      // wave-uniform
+    const int cnt = (int)min((long)EMB_CH, n - c0);
+    const int G = D / 8;
+    const bool cont_in = c0 > 0 && s[c0 - 1] == s[c0];        // the chunk's first run began earlier
+    const bool cont_out = c0 + cnt < n && s[c0 + cnt] == s[c0 + cnt - 1];
+    // the chunk's ids and token positions: one vector load (lane j holds position j), then read back
+    // as wave-uniform values per unrolled position -- no scalar-load round trip per position
+    const int sv = lane < cnt ? s[c0 + lane] : -1;
+    const long pv = lane < cnt ? pi[c0 + lane] : 0;
+    const int pv_lo = (int)(uint32_t)pv, pv_hi = (int)(pv >> 32);
+    for (int g0 = 0; g0 < G; g0 += 64) {
+        const int g = g0 + lane;
+        const bool on = g < G;
+        float v[EMB_CH][8];                                   // every row's load in flight at once
+#pragma unroll
+        for (int j = 0; j < EMB_CH; ++j) {
+            // unconditional (a load under a branch waits at the branch's end): positions past the chunk
+            // read token 0's row, idle lanes the last column group -- both valid, both ignored
+            const long row = ((long)__builtin_amdgcn_readlane(pv_hi, j) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane(pv_lo, j);
+            load8(dy + row * D + (on ? g : G - 1) * 8, v[j]);
+        }
+        // pass 1: run sums; a run complete inside the chunk keeps its sum in v[j] (j = its last position)
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int start = 0;
+        uint32_t done = 0;                                    // wave-uniform: bit j = complete run ends at j
+#pragma unroll
+        for (int j = 0; j < EMB_CH; ++j) {
+            if (j < cnt) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] += v[j][e];
+                const int sj = __builtin_amdgcn_readlane(sv, j);
+                const bool last = j == cnt - 1 || __builtin_amdgcn_readlane(sv, j < EMB_CH - 1 ? j + 1 : j) != sj;
+                if (last) {
+                    const bool starts = start > 0 || !cont_in;
+                    const bool ends = j < cnt - 1 || !cont_out;
+                    if (starts && ends) {
+                        done |= 1u << j;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[j][e] = a[e];
+                    } else if (on) {
+                        store8(part + (chunk * 2 + (starts ? 1 : 0)) * D + g * 8, a);
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) a[e] = 0.f;
+                    start = j + 1;
+                }
+            }
+        }
+        // pass 2: the complete runs' rows, every accumulate read in flight before the first store
+        if (on) {
+            float w[EMB_CH][8];
+            if (accumulate) {                                 // unconditional loads (see above): row of
+#pragma unroll                                                    // position 0 where no run ends
+                for (int j = 0; j < EMB_CH; ++j)
+                    load8(dw + (long)__builtin_amdgcn_readlane(sv, ((done >> j) & 1u) ? j : 0) * D + g * 8, w[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < EMB_CH; ++j) {
+                if ((done >> j) & 1u) {
+                    if (accumulate) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[j][e] += w[j][e];
+                    }
+                    store8(dw + (long)__builtin_amdgcn_readlane(sv, j) * D + g * 8, v[j]);
+                }
+            }
+        }
+    }
+}
+
+// One wave per chunk whose tail piece starts a run that continues past the chunk: that piece plus the
+// head pieces of the following chunks, in chunk order, until the run ends.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_join_k(const int* __restrict__ s, T* __restrict__ dw,
+                                                        const float* __restrict__ part, long n, int D, int accumulate) {
+    const long chunk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long c0 = chunk * EMB_CH;
+    if (c0 >= n) return;
+    const long c1 = min(c0 + EMB_CH, n);
+    const int v = s[c1 - 1];
+    if (c1 >= n || s[c1] != v) return;                        // the last run ends in this chunk
+    if (s[c0] == v && c0 > 0 && s[c0 - 1] == v) return;       // ... or began before it
+    const int G = D / 8;
+    const long nch = (n + EMB_CH - 1) / EMB_CH;
+    for (int g0 = 0; g0 < G; g0 += 64) {
+        const int g = g0 + lane;
+        if (g >= G) break;
+        float a[8];
+        load8(part + (chunk * 2 + 1) * D + g * 8, a);
+        for (long c = chunk + 1; c < nch; ++c) {
+            float b[8];
+            load8(part + c * 2 * D + g * 8, b);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] += b[e];
+            const long e1 = min((c + 1) * EMB_CH, n);
+            if (e1 >= n || s[e1] != v) break;                 // the run ends in chunk c
+        }
+        emb_row_out(dw + (long)v * D + g * 8, a, accumulate);
+    }
+}
+
 template <typename TO>
 __global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ x, TO* __restrict__ y, long n, int acc) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -684,6 +817,26 @@ DDL_API int ddl_embedding_bwd(int dtype, const int64_t* ids, const void* dy, flo
     const long n = V * D;
     DISPATCH_T(dtype, (cast_f32_k<bf16_t><<<grid_for(n), 256, 0, st>>>(acc, (bf16_t*)dw, n, accumulate)),
                (cast_f32_k<float><<<grid_for(n), 256, 0, st>>>(acc, (float*)dw, n, accumulate)));
+    DDL_RETURN_LAUNCH();
+}
+// Deterministic form: s / pi = the ids (int32: a radix sort of half the passes) sorted stably and their
+// token positions (int64), n_tok each;
+// part = fp32 workspace of 2 * ceil(n_tok / 16) * D elements (no initialisation needed).  Writes
+// (accumulate: adds to) only the rows of dw whose id occurs; the caller zeroes dw otherwise.
+DDL_API int ddl_embedding_bwd_sorted(int dtype, const int* s, const int64_t* pi, const void* dy, void* dw,
+                                     float* part, long n_tok, int D, int accumulate, hipStream_t st) {
+    if (D % 8 || n_tok <= 0) return -1;
+    const long nch = (n_tok + EMB_CH - 1) / EMB_CH;
+    const long blocks = (nch + 3) / 4;
+    if (blocks >= (1L << 31)) return -1;
+    DISPATCH_T(dtype,
+               (embed_bwd_seg_k<bf16_t><<<(int)blocks, 256, 0, st>>>(s, pi, (const bf16_t*)dy, (bf16_t*)dw, part,
+                                                                      n_tok, D, accumulate)),
+               (embed_bwd_seg_k<float><<<(int)blocks, 256, 0, st>>>(s, pi, (const float*)dy, (float*)dw, part,
+                                                                     n_tok, D, accumulate)));
+    DISPATCH_T(dtype,
+               (embed_bwd_join_k<bf16_t><<<(int)blocks, 256, 0, st>>>(s, (bf16_t*)dw, part, n_tok, D, accumulate)),
+               (embed_bwd_join_k<float><<<(int)blocks, 256, 0, st>>>(s, (float*)dw, part, n_tok, D, accumulate)));
     DDL_RETURN_LAUNCH();
 }
 

@@ -157,6 +157,7 @@ _SIGS = {
     "ddl_avgpool_bwd": [I, P, P, I, I, I, P],
     "ddl_embedding_fwd": [I, P, P, P, L, I, P],
     "ddl_embedding_bwd": [I, P, P, P, P, L, L, I, I, P],
+    "ddl_embedding_bwd_sorted": [I, P, P, P, P, P, L, I, I, P],
     # optim.hip
     "ddl_sgd_step": [I, P, P, I, P, P, P, I, P, F, F, F, I, I, P],
     "ddl_adamw_step": [I, P, P, I, P, P, P, P, I, P, F, F, F, F, F, F, F, P],

@@ -1,9 +1,19 @@
-"""Embedding gather / scatter-add bindings (csrc/kernels/elementwise.hip)."""
+"""Embedding gather / scatter-add bindings (csrc/kernels/elementwise.hip).
+
+The backward sorts the ids (stable) and sums each id's rows in token order with no atomics
+(``ddl_embedding_bwd_sorted``): the same gradient bits on every run, and no V x D fp32 buffer
+to zero and cast.  ``DDL_EMBED_SORTED=0`` restores the fp32-atomic scatter (A/B timing).
+"""
 from __future__ import annotations
+
+import os
 
 import torch
 
 from ._lib import call, dcode, grad_ready, grad_sink, p
+
+
+_SORTED = os.environ.get("DDL_EMBED_SORTED", "1") != "0"
 
 
 class _Embedding(torch.autograd.Function):
@@ -24,10 +34,20 @@ class _Embedding(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         V, D = ctx.wshape
         dy = dy.contiguous()
-        acc = torch.zeros(V, D, dtype=torch.float32, device=dy.device)
         sink = grad_sink(ctx.w_param)
-        dw = sink if sink is not None else torch.empty(V, D, dtype=ctx.wdtype, device=dy.device)
-        call("ddl_embedding_bwd", dcode(dy), p(ids), p(dy), p(acc), p(dw), ids.numel(), V, D, int(sink is not None))
+        n = ids.numel()
+        if _SORTED and n > 0:
+            # untouched rows: the sink keeps its value (accumulate), a fresh gradient starts at zero
+            dw = sink if sink is not None else torch.zeros(V, D, dtype=ctx.wdtype, device=dy.device)
+            # int32 keys (V < 2^31): the radix sort makes half the passes of an int64 one
+            s, pi = torch.sort(ids.view(-1).to(torch.int32), stable=True)
+            part = torch.empty(2 * ((n + 15) // 16) * D, dtype=torch.float32, device=dy.device)
+            call("ddl_embedding_bwd_sorted", dcode(dy), p(s), p(pi), p(dy), p(dw), p(part), n, D,
+                 int(sink is not None))
+        else:
+            acc = torch.zeros(V, D, dtype=torch.float32, device=dy.device)
+            dw = sink if sink is not None else torch.empty(V, D, dtype=ctx.wdtype, device=dy.device)
+            call("ddl_embedding_bwd", dcode(dy), p(ids), p(dy), p(acc), p(dw), n, V, D, int(sink is not None))
         if sink is not None:
             grad_ready(ctx.w_param)
             return None, None

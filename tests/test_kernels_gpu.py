@@ -243,6 +243,67 @@ def test_embedding():
     _close(w.grad, wr.grad, 5e-2, 1e-2)
 
 
+@pytest.mark.parametrize("V,D,n,skew", [
+    (1000, 768, 1024, "uniform"),     # short runs, chunk edges everywhere
+    (30522, 768, 16384, "padding"),   # one id (padding) over ~half the positions: a run across hundreds of chunks
+    (2, 768, 4096, "uniform"),        # token types: two runs of ~2048
+    (50, 1024, 1001, "runs16"),       # runs of exactly one chunk, n not a multiple of 16
+    (7, 64, 37, "uniform"),           # D = 64: one half-used column slab
+])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embedding_backward_sorted_deterministic(V, D, n, skew, dtype):
+    """Sorted segmented-sum embedding backward (ddl_embedding_bwd_sorted): every id's rows summed in
+    token order against fp32 index_add_, including runs that cross many 16-position chunks; the
+    accumulate form adds to a gradient slot and leaves untouched rows alone; two runs are bitwise equal."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops._lib import call, dcode, p
+    torch.manual_seed(1)
+    ids = torch.randint(0, V, (n,), device=dev)
+    if skew == "padding":
+        ids[torch.rand(n, device=dev) < 0.5] = 0
+    elif skew == "runs16":
+        ids = (torch.arange(n, device=dev) // 16) % V
+        ids = ids[torch.randperm(n, device=dev)]
+    dy = torch.randn(n, D, device=dev).to(dtype)
+    ref = torch.zeros(V, D, device=dev, dtype=torch.float64).index_add_(0, ids, dy.double())
+    s, pi = torch.sort(ids.to(torch.int32), stable=True)
+    part = torch.empty(2 * ((n + 15) // 16) * D, dtype=torch.float32, device=dev)
+    outs = []
+    for acc in (0, 0, 1):
+        base = torch.randn(V, D, device=dev).to(dtype) if acc else torch.zeros(V, D, device=dev, dtype=dtype)
+        dw = base.clone()
+        call("ddl_embedding_bwd_sorted", dcode(dy), p(s), p(pi), p(dy), p(dw), p(part), n, D, acc)
+        torch.cuda.synchronize()
+        outs.append((base, dw))
+    assert torch.equal(outs[0][1], outs[1][1])
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    got = outs[0][1].double()
+    assert ((got - ref).abs().max() / ref.abs().max()).item() < tol
+    base, dw = outs[2]
+    touched = torch.zeros(V, dtype=torch.bool, device=dev)
+    touched[ids] = True
+    assert torch.equal(dw[~touched], base[~touched])
+    want = base.double() + ref
+    assert ((dw.double() - want).abs().max() / want.abs().max()).item() < tol
+
+
+def test_embedding_backward_sorted_matches_atomic_path(monkeypatch):
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_embedding as Em
+    torch.manual_seed(2)
+    w = torch.randn(3000, 768, device=dev, dtype=torch.bfloat16)
+    ids = torch.randint(0, 3000, (16, 128), device=dev)
+    ids[:, 100:] = 0
+    g = torch.randn(16, 128, 768, device=dev, dtype=torch.bfloat16)
+    grads = {}
+    for flag in (True, False):
+        monkeypatch.setattr(Em, "_SORTED", flag)
+        ww = w.clone().requires_grad_(True)
+        Em.embedding(ids, ww).backward(g)
+        grads[flag] = ww.grad.float()
+    assert ((grads[True] - grads[False]).abs().max() / grads[False].abs().max()).item() < 1e-2
+
+
 @pytest.mark.parametrize("name", ["sgd", "adamw", "lamb"])
 @pytest.mark.parametrize("pdtype", [torch.float32, torch.bfloat16])
 def test_flat_optimizers_match_torch_path(name, pdtype):
