@@ -72,3 +72,23 @@ def test_attention_bn_ln_bitwise_repeatable():
     xb = torch.randn(8, 28, 28, 256, device=dev).bfloat16()
     rm, rv = torch.zeros(256, device=dev), torch.ones(256, device=dev)
     _same(lambda: ops.batch_norm(xb, g, b, rm.clone(), rv.clone(), True, 0.1, 1e-5, True, None))
+
+
+def test_embedding_backward_bitwise_repeatable():
+    """Word-embedding gradient with heavily repeated ids (padding, [CLS]-like tokens): the sorted
+    segmented sum has no atomics, so the gradient is the same bits every run."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_embedding as Em
+    torch.manual_seed(3)
+    w = torch.randn(30522, 768, device=dev).bfloat16()
+    ids = torch.randint(0, 30522, (64, 128), device=dev)
+    ids[:, 0] = 101
+    ids[:, 90:] = 0
+    g = torch.randn(64, 128, 768, device=dev).bfloat16()
+
+    def run():
+        ww = w.clone().requires_grad_(True)
+        Em.embedding(ids, ww).backward(g)
+        return ww.grad
+
+    _same(run)
