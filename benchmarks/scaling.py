@@ -12,7 +12,8 @@ plus a summary with the weak-scaling efficiency of each N against N=1:
 
 Each run is a fresh set of processes, so every N pays its own GEMM tuning in its
 warm-up steps and nothing from a previous N is cached.  ``--backend gloo`` with
-``--max-visible`` rehearses the sweep on the CPU (tests/test_bench_cpu.py).
+``--max-visible`` rehearses the sweep on the CPU
+(tests/test_launch_cpu.py::test_bench_self_launch_and_scaling_sweep).
 """
 from __future__ import annotations
 

@@ -588,35 +588,72 @@ __global__ __launch_bounds__(256) void embed_bwd_seg_k(const int* __restrict__ s
     }
 }
 
-// One wave per chunk whose tail piece starts a run that continues past the chunk: that piece plus the
-// head pieces of the following chunks, in chunk order, until the run ends.
+// One workgroup per chunk whose tail piece starts a run that continues past the chunk: that piece
+// plus the head pieces of the following chunks, in a fixed order, until the run ends.  Real batches
+// have LONG runs (padding id 0; token-type ids, V = 2, half the batch each: hundreds of chunks), so
+// the run's last chunk is found by a binary search over the sorted ids (log2 n dependent loads, not
+// one per chunk), and the 256 threads split the chunks: thread (r, g) sums column group g of the
+// chunks r, r + R, ... (R = 256 / groups, each thread's loads independent, four in flight), then
+// the R partial sums are added in r order through LDS -- the same bits every run.
 template <typename T>
 __global__ __launch_bounds__(256) void embed_bwd_join_k(const int* __restrict__ s, T* __restrict__ dw,
                                                         const float* __restrict__ part, long n, int D, int accumulate) {
-    const long chunk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    __shared__ float red[256 * 8];
+    __shared__ long s_last;
+    const long chunk = blockIdx.x;
     const long c0 = chunk * EMB_CH;
     if (c0 >= n) return;
     const long c1 = min(c0 + EMB_CH, n);
     const int v = s[c1 - 1];
     if (c1 >= n || s[c1] != v) return;                        // the last run ends in this chunk
     if (s[c0] == v && c0 > 0 && s[c0 - 1] == v) return;       // ... or began before it
-    const int G = D / 8;
-    const long nch = (n + EMB_CH - 1) / EMB_CH;
-    for (int g0 = 0; g0 < G; g0 += 64) {
-        const int g = g0 + lane;
-        if (g >= G) break;
-        float a[8];
-        load8(part + (chunk * 2 + 1) * D + g * 8, a);
-        for (long c = chunk + 1; c < nch; ++c) {
-            float b[8];
-            load8(part + c * 2 * D + g * 8, b);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] += b[e];
-            const long e1 = min((c + 1) * EMB_CH, n);
-            if (e1 >= n || s[e1] != v) break;                 // the run ends in chunk c
+    if (threadIdx.x == 0) {
+        long lo = c1, hi = n;                                 // first position past the run
+        while (lo < hi) {
+            const long mid = (lo + hi) >> 1;
+            if (s[mid] == v) lo = mid + 1;
+            else hi = mid;
         }
-        emb_row_out(dw + (long)v * D + g * 8, a, accumulate);
+        s_last = lo - 1;
+    }
+    __syncthreads();
+    const long cend = s_last / EMB_CH;                        // chunk holding the run's last position
+    const long k = cend - chunk;                              // head pieces: chunks chunk+1 .. cend
+    const int G = D / 8;
+    for (int g0 = 0; g0 < G; g0 += 256) {
+        const int gs = min(256, G - g0);                      // column groups of this slab
+        const int R = 256 / gs;                               // chunk lanes
+        const int r = threadIdx.x / gs, g = g0 + threadIdx.x % gs;
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (r < R) {
+            if (r == 0) load8(part + (chunk * 2 + 1) * D + g * 8, a);
+            long i = 1 + r;
+            for (; i + 3L * R <= k; i += 4L * R) {
+                float b[4][8];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) load8(part + (chunk + i + (long)u * R) * 2 * D + g * 8, b[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) a[e] += b[u][e];
+            }
+            for (; i <= k; i += R) {
+                float b[8];
+                load8(part + (chunk + i) * 2 * D + g * 8, b);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] += b[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = a[e];
+        }
+        __syncthreads();
+        if (r == 0) {
+            for (int rr = 1; rr < R; ++rr)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] += red[(rr * gs + threadIdx.x) * 8 + e];
+            emb_row_out(dw + (long)v * D + g * 8, a, accumulate);
+        }
+        __syncthreads();
     }
 }
 
@@ -828,15 +865,15 @@ DDL_API int ddl_embedding_bwd_sorted(int dtype, const int* s, const int64_t* pi,
     if (D % 8 || n_tok <= 0) return -1;
     const long nch = (n_tok + EMB_CH - 1) / EMB_CH;
     const long blocks = (nch + 3) / 4;
-    if (blocks >= (1L << 31)) return -1;
+    if (nch >= (1L << 31)) return -1;
     DISPATCH_T(dtype,
                (embed_bwd_seg_k<bf16_t><<<(int)blocks, 256, 0, st>>>(s, pi, (const bf16_t*)dy, (bf16_t*)dw, part,
                                                                       n_tok, D, accumulate)),
                (embed_bwd_seg_k<float><<<(int)blocks, 256, 0, st>>>(s, pi, (const float*)dy, (float*)dw, part,
                                                                      n_tok, D, accumulate)));
     DISPATCH_T(dtype,
-               (embed_bwd_join_k<bf16_t><<<(int)blocks, 256, 0, st>>>(s, (bf16_t*)dw, part, n_tok, D, accumulate)),
-               (embed_bwd_join_k<float><<<(int)blocks, 256, 0, st>>>(s, (float*)dw, part, n_tok, D, accumulate)));
+               (embed_bwd_join_k<bf16_t><<<(int)nch, 256, 0, st>>>(s, (bf16_t*)dw, part, n_tok, D, accumulate)),
+               (embed_bwd_join_k<float><<<(int)nch, 256, 0, st>>>(s, (float*)dw, part, n_tok, D, accumulate)));
     DDL_RETURN_LAUNCH();
 }
 

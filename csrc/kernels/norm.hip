@@ -1100,9 +1100,12 @@ static int merged_mode() {
     static const int m = [] { const char* e = getenv("DDL_BN_MERGED_FIN"); return e ? atoi(e) : 2; }();
     return m;
 }
-static bool merged_finalize(int nblk) {
+// (each launch owns one window of TICKET_WIN arrival tickets, one per 64-channel group: wider
+// layers than TICKET_WIN * 64 channels take the collapse + single-pass finalize instead, so a
+// group index can never reach into the next launch's window or past the pool)
+static bool merged_finalize(int nblk, int C) {
     const int m = merged_mode();
-    return m == 2 || (m == 1 && nblk > 512);
+    return (C + 63) / 64 <= TICKET_WIN && (m == 2 || (m == 1 && nblk > 512));
 }
 
 // Partial rows beyond this are first collapsed 32:1 (a single finalize block per
@@ -1136,7 +1139,7 @@ DDL_API int ddl_bn_fwd_from_partials(int dtype, const float* part, int nblk, lon
                                      const void* beta, float* running_mean, float* running_var, float momentum,
                                      float eps, float* save_mean, float* save_invstd, float* scale, float* shift,
                                      float* ws, long ws_elems, hipStream_t st) {
-    if (merged_finalize(nblk)) {
+    if (merged_finalize(nblk, C)) {
         const int S = fin_slices(nblk);
         int* tk = S > 1 ? fin_tickets() : nullptr;
         if (S == 1 || (tk && ws && ws_elems >= (long)S * 2 * C)) {
@@ -1232,7 +1235,7 @@ DDL_API int ddl_bn_apply(int dtype, const void* x, const void* res, const float*
 template <typename T>
 static void bwd_finalize(const float* part, int nblk, float* ws, int C, long M, const T* gamma, const float* invstd,
                          T* dgamma, T* dbeta, float* coef, int acc, hipStream_t st) {
-    if (merged_finalize(nblk)) {
+    if (merged_finalize(nblk, C)) {
         const int S = fin_slices(nblk);
         int* tk = S > 1 ? fin_tickets() : nullptr;
         if (S == 1 || tk) {
@@ -1545,7 +1548,7 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
         default: return -1;
     }
 #undef LNB_ADD
-    if (merged_finalize(nblk)) {
+    if (merged_finalize(nblk, H)) {
         // one launch: 128-row slices + last-arriver combine (ws: the room behind the partial rows)
         const int S = fin_slices(nblk);
         int* tk = S > 1 ? fin_tickets() : nullptr;
@@ -1713,7 +1716,7 @@ DDL_API int ddl_bn_bwd_from_partials(int dtype, const float* part, int nrows, fl
                                      const void* gamma, long M, int C, void* dgamma, void* dbeta, float* coef, void* dx,
                                      void* dres, int acc_params, hipStream_t st) {
     if (!rows_ok(C) || dtype != 1) return -1;
-    if (merged_finalize(nrows) && (fin_slices(nrows) == 1 || (ws && ws_elems >= (long)fin_slices(nrows) * 2 * C))) {
+    if (merged_finalize(nrows, C) && (fin_slices(nrows) == 1 || (ws && ws_elems >= (long)fin_slices(nrows) * 2 * C))) {
         bwd_finalize<bf16_t>(part, nrows, fin_slices(nrows) == 1 ? nullptr : ws, C, M, (const bf16_t*)gamma, invstd,
                              (bf16_t*)dgamma, (bf16_t*)dbeta, coef, acc_params, st);
         bn_bwd_apply_only((const bf16_t*)dz, nullptr, (const bf16_t*)x, mean, invstd, M, C, 0, coef, (bf16_t*)dx,

@@ -28,10 +28,21 @@
 // RCCL.  `api` serialises the API callers among themselves (collective enqueue order); `book`
 // guards the launch bookkeeping (counters, event slots, launch times) and is held only around
 // event records and counter updates, never across an RCCL call; the communicator pointer and
-// the abort flag are atomics, so ddl_comm_abort() swaps the communicator out and calls
-// ncclCommAbort() even while another thread is blocked inside an enqueue (RCCL sets up peer
-// connections on a communicator's first collective: with a dead peer that enqueue can block).
-// A blocked enqueue counts as pending for ddl_comm_oldest_pending_ms() from the moment it began.
+// the abort flag are atomics.
+//
+// Communicator lifetime: every use of the communicator (an enqueue, the watchdog's async-error
+// read) runs inside an in-flight guard (count up, THEN load the pointer); ddl_comm_abort() sets
+// the abort flag, swaps the pointer out, waits until the count is zero and only then calls
+// ncclCommAbort() -- so the communicator is never freed under a thread still using it.  That
+// wait is short because the communicator is created NON-BLOCKING (ncclCommInitRankConfig,
+// blocking = 0): no RCCL call ever blocks (RCCL sets up peer connections on a communicator's
+// first collective; with a dead peer a blocking enqueue would hang inside RCCL), it returns
+// ncclInProgress instead and the engine polls ncclCommGetAsyncError from its own loop, which
+// checks the abort flag between polls and leaves without touching the communicator again.
+// An enqueue in that loop counts as pending for ddl_comm_oldest_pending_ms() from the moment it
+// began.  (DDL_COMM_NONBLOCKING=0, or an RCCL without ncclCommInitRankConfig: blocking mode, where
+// an abort that finds a thread still inside RCCL after 2 s aborts anyway -- the only way to
+// unblock it -- which is the one case not covered.)
 //
 // The reference has no communication layer at all; BASELINE.json
 // mandates "data-parallel all-reduce ... RCCL ring/tree over xGMI ... overlapped
@@ -44,6 +55,7 @@
 #include <chrono>
 #include <thread>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -56,6 +68,7 @@ struct Rccl {
     void* so = nullptr;
     decltype(&ncclGetUniqueId) getUniqueId = nullptr;
     decltype(&ncclCommInitRank) commInitRank = nullptr;
+    decltype(&ncclCommInitRankConfig) commInitRankConfig = nullptr;   // optional: non-blocking mode
     decltype(&ncclCommDestroy) commDestroy = nullptr;
     decltype(&ncclCommAbort) commAbort = nullptr;
     decltype(&ncclAllReduce) allReduce = nullptr;
@@ -99,7 +112,9 @@ bool load_rccl(const char* path) {
            sym(g_rccl.groupStart, "ncclGroupStart") && sym(g_rccl.groupEnd, "ncclGroupEnd") &&
            sym(g_rccl.errorString, "ncclGetErrorString") &&
            (g_rccl.getAsyncError = reinterpret_cast<decltype(&ncclCommGetAsyncError)>(
-                dlsym(g_rccl.so, "ncclCommGetAsyncError")), true);
+                dlsym(g_rccl.so, "ncclCommGetAsyncError")), true) &&
+           (g_rccl.commInitRankConfig = reinterpret_cast<decltype(&ncclCommInitRankConfig)>(
+                dlsym(g_rccl.so, "ncclCommInitRankConfig")), true);
 }
 
 bool ok(ncclResult_t r, const char* what) {
@@ -145,6 +160,8 @@ struct Engine {
     std::atomic<int> injected{0};    // test hook: reported as the async error
     std::atomic<int> stall_ms{0};    // test hook: the next enqueue blocks this long (a dead peer)
     std::atomic<bool> aborted{false};
+    std::atomic<int> inflight{0};    // threads holding the communicator pointer (InUse)
+    bool nonblocking = false;        // created with blocking = 0: RCCL calls return ncclInProgress
     std::mutex api;                  // API callers among themselves; never taken by the watchdog
     std::mutex book;                 // bookkeeping only; never held across an RCCL call
 };
@@ -165,29 +182,64 @@ bool mark_done(Engine* e, long nbytes) {
     return hok(hipEventRecord(e->done[(e->launched - 1) % RING], e->stream), "hipEventRecord");
 }
 
-// The communicator for an enqueue (null once aborted).  The enqueue counts as pending from
-// here until end_enqueue(), so a call that blocks inside RCCL is seen by the watchdog.
-ncclComm_t begin_enqueue(Engine* e) {
+// In-flight guard: counted BEFORE the pointer is loaded, so an abort that swapped the pointer out
+// and then saw the count at zero knows no thread can still reach the old communicator.
+struct InUse {
+    Engine* e;
+    ncclComm_t c;
+    explicit InUse(Engine* en) : e(en) {
+        e->inflight.fetch_add(1);
+        c = e->aborted.load() ? nullptr : e->comm.load();
+    }
+    ~InUse() { e->inflight.fetch_sub(1); }
+    InUse(const InUse&) = delete;
+    InUse& operator=(const InUse&) = delete;
+};
+
+// Mark an enqueue pending (the watchdog sees it from here until end_enqueue()).  In blocking mode
+// the test stall happens here, before the communicator is loaded; in non-blocking mode inside
+// settle(), where a real dead-peer enqueue would spin.
+void begin_enqueue(Engine* e) {
     {
         std::lock_guard<std::mutex> lk(e->book);
         e->in_enqueue = true;
         e->t_enqueue = Clock::now();
     }
-    const int stall = e->stall_ms.exchange(0);
-    if (stall > 0) std::this_thread::sleep_for(std::chrono::milliseconds(stall));
-    ncclComm_t c = e->comm.load();
-    if (!c || e->aborted.load()) {
-        set_err("comm", "communicator aborted");
-        std::lock_guard<std::mutex> lk(e->book);
-        e->in_enqueue = false;
-        return nullptr;
+    if (!e->nonblocking) {
+        const int stall = e->stall_ms.exchange(0);
+        if (stall > 0) std::this_thread::sleep_for(std::chrono::milliseconds(stall));
     }
-    return c;
 }
 
 void end_enqueue(Engine* e) {
     std::lock_guard<std::mutex> lk(e->book);
     e->in_enqueue = false;
+}
+
+// Non-blocking mode: wait until the RCCL call that returned `r` has been accepted (ncclInProgress
+// -> poll the communicator's async state), leaving early -- without touching `c` again -- once
+// the communicator is aborted.  Blocking mode: `r` is final.
+ncclResult_t settle(Engine* e, ncclComm_t c, ncclResult_t r) {
+    if (!e->nonblocking) return r;
+    const int stall = e->stall_ms.exchange(0);        // test hook: "InProgress" for that long
+    const auto until = Clock::now() + std::chrono::milliseconds(stall > 0 ? stall : 0);
+    for (long spin = 0;; ++spin) {
+        if (e->aborted.load()) return ncclInvalidUsage;
+        const bool stalled = stall > 0 && Clock::now() < until;
+        if (!stalled && r != ncclInProgress) return r;
+        if (!stalled && g_rccl.getAsyncError(c, &r) != ncclSuccess) return ncclInternalError;
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::yield();
+    }
+}
+
+bool rccl_ok(Engine* e, ncclComm_t c, ncclResult_t r, const char* what) {
+    r = settle(e, c, r);
+    if (e->aborted.load()) {
+        set_err(what, "communicator aborted");
+        return false;
+    }
+    return ok(r, what);
 }
 
 bool usable(Engine* e) {
@@ -243,7 +295,23 @@ DDL_API void* ddl_comm_create(const char* rccl_path, const char* id_bytes, int w
     ncclUniqueId id;
     std::memcpy(id.internal, id_bytes, NCCL_UNIQUE_ID_BYTES);
     ncclComm_t c = nullptr;
-    if (!ok(g_rccl.commInitRank(&c, world, id, rank), "ncclCommInitRank")) {
+    const char* nb = getenv("DDL_COMM_NONBLOCKING");
+    e->nonblocking = g_rccl.commInitRankConfig && g_rccl.getAsyncError && !(nb && nb[0] == '0');
+    bool good;
+    if (e->nonblocking) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r = g_rccl.commInitRankConfig(&c, world, id, rank, &cfg);
+        while (r == ncclInProgress && c) {
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+            if (g_rccl.getAsyncError(c, &r) != ncclSuccess) r = ncclInternalError;
+        }
+        good = ok(r, "ncclCommInitRankConfig");
+    } else {
+        good = ok(g_rccl.commInitRank(&c, world, id, rank), "ncclCommInitRank");
+    }
+    if (!good) {
+        if (c) g_rccl.commAbort(c);
         hipStreamDestroy(e->stream);
         delete e;
         return nullptr;
@@ -258,10 +326,14 @@ DDL_API int ddl_comm_allreduce(void* h, void* buf, long count, int dtype, int av
     std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    ncclComm_t c = begin_enqueue(e);
-    if (!c) return -4;
-    const bool good = ok(g_rccl.allReduce(buf, buf, (size_t)count, dtype_of(dtype), avg ? ncclAvg : ncclSum, c,
-                                          e->stream), "ncclAllReduce");
+    begin_enqueue(e);
+    bool good;
+    {
+        InUse u(e);
+        if (!u.c) { end_enqueue(e); set_err("comm", "communicator aborted"); return -4; }
+        good = rccl_ok(e, u.c, g_rccl.allReduce(buf, buf, (size_t)count, dtype_of(dtype), avg ? ncclAvg : ncclSum,
+                                                u.c, e->stream), "ncclAllReduce");
+    }
     end_enqueue(e);
     if (!good) return -2;
     return mark_done(e, count * esize(dtype)) ? 0 : -3;
@@ -291,15 +363,20 @@ DDL_API int ddl_comm_allreduce_many(void* h, void** bufs, const long* counts, in
         }
     }
     if (!members) return 0;
-    ncclComm_t c = begin_enqueue(e);
-    if (!c) return -4;
-    bool good = ok(g_rccl.groupStart(), "ncclGroupStart");
-    for (int i = 0; good && i < n; ++i) {
-        if (counts[i] <= 0) continue;
-        good = ok(g_rccl.allReduce(bufs[i], bufs[i], (size_t)counts[i], dtype_of(dtype), avg ? ncclAvg : ncclSum, c,
-                                   e->stream), "ncclAllReduce");
+    begin_enqueue(e);
+    bool good;
+    {
+        InUse u(e);
+        if (!u.c) { end_enqueue(e); set_err("comm", "communicator aborted"); return -4; }
+        good = ok(g_rccl.groupStart(), "ncclGroupStart");
+        for (int i = 0; good && i < n; ++i) {
+            if (counts[i] <= 0) continue;
+            good = ok(g_rccl.allReduce(bufs[i], bufs[i], (size_t)counts[i], dtype_of(dtype),
+                                       avg ? ncclAvg : ncclSum, u.c, e->stream), "ncclAllReduce");
+        }
+        // (in a group the members' results are deferred: ncclGroupEnd's result is the group's)
+        good = rccl_ok(e, u.c, g_rccl.groupEnd(), "ncclGroupEnd") && good;
     }
-    good = ok(g_rccl.groupEnd(), "ncclGroupEnd") && good;
     end_enqueue(e);
     if (!good) return -2;
     // every number of the group completes at the same point of the comm stream
@@ -318,10 +395,14 @@ DDL_API int ddl_comm_broadcast(void* h, void* buf, long count, int dtype, int ro
     std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    ncclComm_t c = begin_enqueue(e);
-    if (!c) return -4;
-    const bool good = ok(g_rccl.broadcast(buf, buf, (size_t)count, dtype_of(dtype), root, c, e->stream),
-                         "ncclBroadcast");
+    begin_enqueue(e);
+    bool good;
+    {
+        InUse u(e);
+        if (!u.c) { end_enqueue(e); set_err("comm", "communicator aborted"); return -4; }
+        good = rccl_ok(e, u.c, g_rccl.broadcast(buf, buf, (size_t)count, dtype_of(dtype), root, u.c, e->stream),
+                       "ncclBroadcast");
+    }
     end_enqueue(e);
     if (!good) return -2;
     return mark_done(e, count * esize(dtype)) ? 0 : -3;
@@ -337,10 +418,14 @@ DDL_API int ddl_comm_reduce_scatter(void* h, const void* send, void* recv, long 
     std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    ncclComm_t c = begin_enqueue(e);
-    if (!c) return -4;
-    const bool good = ok(g_rccl.reduceScatter(send, recv, (size_t)recv_count, dtype_of(dtype),
-                                              avg ? ncclAvg : ncclSum, c, e->stream), "ncclReduceScatter");
+    begin_enqueue(e);
+    bool good;
+    {
+        InUse u(e);
+        if (!u.c) { end_enqueue(e); set_err("comm", "communicator aborted"); return -4; }
+        good = rccl_ok(e, u.c, g_rccl.reduceScatter(send, recv, (size_t)recv_count, dtype_of(dtype),
+                                                    avg ? ncclAvg : ncclSum, u.c, e->stream), "ncclReduceScatter");
+    }
     end_enqueue(e);
     if (!good) return -2;
     return mark_done(e, recv_count * e->world * esize(dtype)) ? 0 : -3;
@@ -353,10 +438,14 @@ DDL_API int ddl_comm_all_gather(void* h, const void* send, void* recv, long send
     std::lock_guard<std::mutex> lk(e->api);
     if (!usable(e)) return -4;
     if (!order_after(e, compute) || !mark_start(e)) return -3;
-    ncclComm_t c = begin_enqueue(e);
-    if (!c) return -4;
-    const bool good = ok(g_rccl.allGather(send, recv, (size_t)send_count, dtype_of(dtype), c, e->stream),
-                         "ncclAllGather");
+    begin_enqueue(e);
+    bool good;
+    {
+        InUse u(e);
+        if (!u.c) { end_enqueue(e); set_err("comm", "communicator aborted"); return -4; }
+        good = rccl_ok(e, u.c, g_rccl.allGather(send, recv, (size_t)send_count, dtype_of(dtype), u.c, e->stream),
+                       "ncclAllGather");
+    }
     end_enqueue(e);
     if (!good) return -2;
     return mark_done(e, send_count * e->world * esize(dtype)) ? 0 : -3;
@@ -402,12 +491,12 @@ DDL_API int ddl_comm_synchronize(void* h) {
 DDL_API int ddl_comm_async_error(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    ncclComm_t c = e->comm.load();
-    if (e->aborted.load() || !c) return -4;
+    InUse u(e);
+    if (!u.c) return -4;
     if (const int inj = e->injected.load()) return inj;
     if (!g_rccl.getAsyncError) return 0;
     ncclResult_t r = ncclSuccess;
-    if (g_rccl.getAsyncError(c, &r) != ncclSuccess) return (int)ncclInternalError;
+    if (g_rccl.getAsyncError(u.c, &r) != ncclSuccess) return (int)ncclInternalError;
     return (r == ncclSuccess || r == ncclInProgress) ? 0 : (int)r;
 }
 
@@ -449,16 +538,34 @@ DDL_API double ddl_comm_collective_ms(void* h, long seq) {
     return ms;
 }
 
-// Failure path from any thread, lock-free: the communicator is swapped out first (later API
-// calls see it gone), then ncclCommAbort (kernels spinning on a dead peer return, the streams
-// drain, an enqueue blocked in connection setup returns); the stream / events stay for destroy.
+// Failure path from any thread, lock-free: the abort flag is set and the communicator swapped
+// out first (later uses see it gone, an enqueue polling in settle() leaves), then -- once no
+// thread holds the old pointer (InUse count zero) -- ncclCommAbort (kernels spinning on a dead
+// peer return, the streams drain); the stream / events stay for destroy.
+void abort_engine(Engine* e) {
+    e->aborted.store(true);
+    ncclComm_t c = e->comm.exchange(nullptr);
+    if (!c) return;
+    const auto t0 = Clock::now();
+    while (e->inflight.load() > 0) {
+        // blocking mode only: a thread stuck INSIDE RCCL never comes back unless the abort runs
+        if (!e->nonblocking && Clock::now() - t0 > std::chrono::seconds(2)) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    g_rccl.commAbort(c);
+}
+
 DDL_API int ddl_comm_abort(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
-    e->aborted.store(true);
-    ncclComm_t c = e->comm.exchange(nullptr);
-    if (c) g_rccl.commAbort(c);
+    abort_engine(e);
     return 0;
+}
+
+// 1: the communicator was created non-blocking (every RCCL call returns promptly; see above)
+DDL_API int ddl_comm_nonblocking(void* h) {
+    Engine* e = static_cast<Engine*>(h);
+    return e && e->nonblocking ? 1 : 0;
 }
 
 // Test hook: make ddl_comm_async_error report `code` (0 clears), as RCCL does for a peer failure.
@@ -471,7 +578,9 @@ DDL_API int ddl_comm_inject_error(void* h, int code) {
 
 // Test hook: the next collective enqueue blocks `ms` milliseconds inside the engine (holding the
 // API lock, as an RCCL enqueue stuck in connection setup to a dead peer does), then fails with -4
-// if the communicator was aborted meanwhile.
+// if the communicator was aborted meanwhile.  Non-blocking mode: the stall is an RCCL call that
+// keeps answering ncclInProgress, polled while the enqueue holds the communicator (InUse), so an
+// abort lands while a real enqueue is in progress.
 DDL_API int ddl_comm_test_stall(void* h, int ms) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return -1;
@@ -489,16 +598,19 @@ DDL_API long ddl_comm_stats(void* h, int which) {
 DDL_API void ddl_comm_destroy(void* h, int abort) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return;
+    // failure path: abort first, lock-free, so an enqueue still polling releases the API lock
+    if (abort) abort_engine(e);
     {
         std::lock_guard<std::mutex> lk(e->api);     // no API call in flight past this point
         e->aborted.store(true);
         ncclComm_t c = e->comm.exchange(nullptr);
         if (c) {
-            if (abort) g_rccl.commAbort(c);
-            else {
-                hipStreamSynchronize(e->stream);
-                g_rccl.commDestroy(c);
-            }
+            while (e->inflight.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
+            hipStreamSynchronize(e->stream);
+            ncclResult_t r = g_rccl.commDestroy(c);
+            // non-blocking: the destroy may finish asynchronously (c stays valid until it reports)
+            while (e->nonblocking && r == ncclInProgress && g_rccl.getAsyncError(c, &r) == ncclSuccess)
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
         }
     }
     for (int i = 0; i < RING; ++i) {

@@ -59,6 +59,7 @@ _SIGS = {
     "ddl_comm_abort": ([P], I),
     "ddl_comm_inject_error": ([P, I], I),
     "ddl_comm_test_stall": ([P, I], I),
+    "ddl_comm_nonblocking": ([P], I),
 }
 _DTYPES = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2, torch.int64: 3, torch.int32: 4}
 
@@ -223,6 +224,13 @@ class NativeComm:
         """Test hook: the next collective call blocks ``ms`` inside the engine, as an RCCL enqueue
         stuck in connection setup to a dead peer does (the watchdog must still see and abort it)."""
         _fn("ddl_comm_test_stall")(self._h, int(ms))
+
+    @property
+    def nonblocking(self) -> bool:
+        """True when the communicator was created non-blocking (RCCL calls never block inside
+        RCCL; an abort waits for no thread stuck there -- ``csrc/runtime/comm.cpp`` header)."""
+        h = getattr(self, "_h", None)
+        return bool(h) and bool(_fn("ddl_comm_nonblocking")(h))
 
     def collective_ms(self, seq: int) -> float:
         """Device time of finished collective ``seq`` (its start / done events), -1 if unknown."""

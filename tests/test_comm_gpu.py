@@ -283,6 +283,52 @@ def test_watchdog_aborts_blocked_enqueue(pg):
     c.close()
 
 
+def test_abort_while_enqueue_holds_communicator(pg):
+    """the abort must never free the communicator under a thread still using it.  In
+    non-blocking mode the stalled enqueue is an RCCL call answering ncclInProgress, polled WHILE
+    the enqueue holds the communicator (in-flight guard): the abort lands in the middle of it,
+    waits for the poller to leave (it checks the abort flag between polls) and only then calls
+    ncclCommAbort -- the enqueue returns CommError within a fraction of its 4 s stall, close()
+    returns, and a second communicator on the same device works afterwards."""
+    import threading
+    import time
+    from databricks_distributed_deep_learning_amd.parallel.comm import CommError, NativeComm
+    c = NativeComm(timeout_s=0)
+    assert c.nonblocking, "RCCL without ncclCommInitRankConfig: blocking mode"
+    x = torch.ones(4096, device=pg)
+    c.all_reduce(x)
+    c.wait()
+    torch.cuda.synchronize()
+    c.stall_next_enqueue(4000)
+    err, done_at = [], []
+
+    def enqueue():
+        try:
+            c.all_reduce(x)
+        except CommError as e:
+            err.append(str(e))
+        done_at.append(time.time())
+
+    t = threading.Thread(target=enqueue)
+    t.start()
+    time.sleep(0.3)                       # the enqueue is now polling with the communicator held
+    assert t.is_alive()
+    t0 = time.time()
+    c.fail("test abort during an enqueue")
+    t_abort = time.time() - t0
+    t.join(timeout=10)
+    assert not t.is_alive() and err, err
+    assert t_abort < 1.0 and done_at[0] - t0 < 1.0, (t_abort, done_at[0] - t0)
+    c.close(abort=True)
+    c2 = NativeComm(timeout_s=0)
+    y = torch.full((1024,), 2.0, device=pg)
+    c2.all_reduce(y)
+    c2.wait()
+    torch.cuda.synchronize()
+    assert float(y[0]) == 2.0
+    c2.close()
+
+
 def test_engine_probe_and_bucket_timings(pg):
     """The startup probe runs on the engine, and the reducer reports per-bucket ring times of
     the last step (world 1: every number exists, bus bandwidth is 0 by the 2(n-1)/n factor)."""

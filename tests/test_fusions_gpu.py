@@ -241,6 +241,42 @@ def test_bn_finalize_from_many_partial_rows(nblk, C):
     assert ((dx.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
 
 
+@pytest.mark.parametrize("C", [4160, 8192])
+def test_bn_finalize_wider_than_ticket_window(C):
+    """a merged finalize launch owns 64 arrival tickets (one per 64 channels).  Layers
+    wider than 4096 channels must take the collapse path instead of indexing past their window
+    (into the next launch's tickets, or past the pool on the last window).  Checked against fp64,
+    then a narrow merged finalize on every remaining window must still be exact and repeatable
+    (a stray ticket would leave a window's counter non-zero and skip a channel group's finish)."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops._lib import call, p
+    torch.manual_seed(7)
+    nblk = 600
+    M = nblk * 128
+    part = torch.rand(nblk, 2 * C, device=dev) * 4.0
+    ws = torch.empty(-(-nblk // 32) * 2 * C, device=dev)
+    gamma = torch.ones(C, device=dev).bfloat16()
+    beta = torch.zeros(C, device=dev).bfloat16()
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    st = torch.empty(4, C, device=dev)
+    call("ddl_bn_fwd_from_partials", 1, p(part), nblk, M, C, p(gamma), p(beta), p(rm), p(rv), 0.1, 1e-5,
+         p(st[0]), p(st[1]), p(st[2]), p(st[3]), p(ws), ws.numel())
+    torch.testing.assert_close(st[0].double(), part.double().sum(0)[:C] / M, rtol=1e-5, atol=1e-6)
+    c2, n2 = 4096, 300
+    part2 = torch.rand(n2, 2 * c2, device=dev)
+    ws2 = torch.empty(-(-n2 // 32) * 2 * c2, device=dev)
+    g2, b2 = torch.ones(c2, device=dev).bfloat16(), torch.zeros(c2, device=dev).bfloat16()
+    want = part2.double().sum(0)[:c2] / (n2 * 128)
+    first = None
+    for _ in range(8192 // 64 + 2):            # every window of the ticket pool, and around again
+        st2 = torch.empty(4, c2, device=dev)
+        call("ddl_bn_fwd_from_partials", 1, p(part2), n2, n2 * 128, c2, p(g2), p(b2), p(torch.zeros(c2, device=dev)),
+             p(torch.ones(c2, device=dev)), 0.1, 1e-5, p(st2[0]), p(st2[1]), p(st2[2]), p(st2[3]), p(ws2), ws2.numel())
+        first = st2.clone() if first is None else first
+        assert torch.equal(st2, first)
+    torch.testing.assert_close(first[0].double(), want, rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("nrows,width,n,acc", [(100, 1536, 768, 1), (777, 64, 64, 0), (2000, 6144, 3072, 1)])
 def test_rows_sum_sink_many_rows(nrows, width, n, acc):
     """Column sums of many partial rows straight into a bf16 gradient slot (a Linear's bias),
