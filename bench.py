@@ -112,22 +112,24 @@ def run_one(model: str, args, world: int):
                       eager_optimizer=os.environ.get("DDL_EAGER_OPTIMIZER", "0") == "1",
                       phase_timing=os.environ.get("DDL_PHASE_TIMING", "1") != "0")
     from databricks_distributed_deep_learning_amd.ops import _native_gemm
-    before = set(_native_gemm.tuned_choices())
-    tr = Trainer(cfg)
-    s = tr.run()
-    tr.close()
-    del tr
-    s["gemm_plan"] = gemm_plan_digest(model, exclude=before)
+    with _native_gemm.plan_usage() as used:
+        tr = Trainer(cfg)
+        s = tr.run()
+        tr.close()
+        del tr
+    s["gemm_plan"] = gemm_plan_digest(model, used)
+    s["plan_source"] = _native_gemm.plan_stats()
     return s
 
 
-def gemm_plan_digest(model: str, exclude=()) -> str:
-    """Hash of the tuned GEMM kernel plan this model ran (every signature it tuned -> (kernel,
-    splits); ``exclude``: signatures an earlier model of this process tuned); the full plan goes to stderr.  Two bench processes whose step times differ can then be told
-    apart by plan (tuner picks) or not (same plan: the cause is elsewhere)."""
+def gemm_plan_digest(model: str, used) -> str:
+    """Hash of the GEMM kernel plan this model ran: every signature it looked up -> (kernel,
+    splits), whether from the committed plan table or tuned in this process; the full plan goes to
+    stderr.  Two bench processes whose step times differ can then be told apart by plan or not
+    (same plan: the cause is elsewhere)."""
     import hashlib
     from databricks_distributed_deep_learning_amd.ops import _native_gemm
-    plan = {k: list(v) for k, v in sorted(_native_gemm.tuned_choices().items()) if k not in exclude}
+    plan = {k: list(v) for k, v in sorted(_native_gemm.current_plan(used).items())}
     if not plan:
         return ""
     text = json.dumps(plan, sort_keys=True)
@@ -217,6 +219,9 @@ def main() -> int:
         },
         "phases_ms": head.get("phases_ms"),
         "gemm_plan": {m: r.get("gemm_plan", "") for m, r in results.items()},
+        # committed plan table (ops/gemm_plans.json) vs tuned: source, table hits, misses (tuned here)
+        "plan_source": {k: v for k, v in (head.get("plan_source") or {}).items()
+                        if k in ("source", "table_hits", "misses", "status", "gemm_src_hash")},
         "bucket_policy": head.get("bucket_policy"),
     }
     if head.get("comm_probe"):

@@ -61,6 +61,39 @@ EXTRA = {"gemm_big.hip": _VGPR_FORM, "conv3x3.hip": _VGPR_FORM, "skinny_gemm.hip
          "stream_gemm.hip": _VGPR_FORM, "gemm_duo.hip": _VGPR_FORM}
 
 
+# Sources whose code decides which GEMM kernel runs fastest for a shape: their hash keys the committed
+# kernel plan table (ops/gemm_plans.json) -- a plan tuned against other GEMM kernels is not used.
+GEMM_SOURCES = ["gemm.hip", "gemm_big.hip", "gemm_duo.hip", "skinny_gemm.hip", "stream_gemm.hip", "conv3x3.hip"]
+
+
+def gemm_src_hash() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for name in GEMM_SOURCES + ["../include/ddl_common.h"]:
+        path = os.path.normpath(os.path.join(CSRC, "kernels", name))
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def buildinfo_obj() -> str:
+    """A host object exporting ddl_gemm_src_hash() (rebuilt whenever that hash changes)."""
+    digest = gemm_src_hash()
+    src = os.path.join(BUILD, "buildinfo.cpp")
+    obj = src + ".o"
+    text = ('extern "C" __attribute__((visibility("default"))) const char* ddl_gemm_src_hash() '
+            f'{{ return "{digest}"; }}\n')
+    old = open(src).read() if os.path.exists(src) else ""
+    if old != text or not os.path.exists(obj):
+        with open(src, "w") as f:
+            f.write(text)
+        r = subprocess.run(["g++", "-O2", "-fPIC", "-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"buildinfo compile failed: {r.stderr}")
+    return obj
+
+
 def compile_one(src, debug=False):
     obj = obj_for(src)
     flags = list(COMMON) + EXTRA.get(os.path.basename(src), [])
@@ -93,7 +126,7 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
             f.result()
             if verbose:
                 print(f"[build]   ok {os.path.relpath(futs[f], ROOT)}", file=sys.stderr)
-    objs = [obj_for(s) for s in srcs]
+    objs = [obj_for(s) for s in srcs] + [buildinfo_obj()]
     newest = max(os.path.getmtime(o) for o in objs)
     if todo or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest:
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp",

@@ -61,6 +61,21 @@ def load() -> Optional[ctypes.CDLL]:
     return _lib
 
 
+def gemm_src_hash() -> Optional[str]:
+    """Hash of the GEMM kernel sources the loaded library was built from (``csrc/build.py``
+    ``gemm_src_hash``), or None for a library built before it was recorded."""
+    lib = load()
+    if lib is None:
+        return None
+    try:
+        fn = lib.ddl_gemm_src_hash
+    except AttributeError:
+        return None
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    return fn().decode()
+
+
 def available() -> bool:
     return load() is not None
 

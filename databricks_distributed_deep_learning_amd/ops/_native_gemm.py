@@ -396,6 +396,91 @@ _ONLINE = _ONLINE_ENV == "1"
 # optional persistent cache (JSON): later processes skip the timing runs
 _CACHE_PATH = os.environ.get("DDL_GEMM_TUNE_CACHE", "")
 
+# ------------------------------------------------------------------ committed kernel plan table
+# A reproducible plan by default (SURVEY §5.4-style determinism for the GEMM plan): ``gemm_plans.json``
+# holds measured (kernel, splits) choices per GEMM signature, keyed by GPU architecture and by the
+# hash of the GEMM kernel sources the library was built from (``csrc/build.py`` gemm_src_hash).  A
+# signature in the table runs its committed plan in every process -- whatever the warm-up count,
+# whichever entry point (bench.py, the train() presets, notebooks) -- so two fresh processes run the
+# same kernels; only a miss is tuned (isolated / in-model tuner, as before).  The table is refreshed
+# from tuning runs by ``scripts/make_plan_table.py``.  DDL_GEMM_PLAN_TABLE=0 disables it, or names
+# another table file.  Precedence: an explicit DDL_GEMM_TUNE_CACHE entry, then the table, then tuning.
+_TABLE_ENV = os.environ.get("DDL_GEMM_PLAN_TABLE", "1")
+_TABLE_PATH = _TABLE_ENV if _TABLE_ENV not in ("0", "1", "") else \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plans.json")
+_table: Optional[dict] = None            # key -> (kind, splits), loaded on first use
+_table_info = {"path": _TABLE_PATH if _TABLE_ENV != "0" else None, "arch": None, "gemm_src_hash": None,
+               "status": "not loaded", "entries": 0}
+_table_hits: set = set()
+_table_misses: set = set()
+_used: Optional[set] = None              # signatures looked up since plan_usage() started
+
+
+def _device_arch() -> str:
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+    except Exception:   # noqa: BLE001 -- no GPU: no table
+        return ""
+
+
+def load_plan_table() -> dict:
+    """The committed plans for this GPU architecture and GEMM-kernel build ({} when the table is
+    disabled, missing, or was tuned against other kernel sources / another architecture)."""
+    global _table
+    if _table is not None:
+        return _table
+    _table = {}
+    if _TABLE_ENV == "0":
+        _table_info["status"] = "disabled"
+        return _table
+    arch, src = _device_arch(), _lib.gemm_src_hash()
+    _table_info.update(arch=arch, gemm_src_hash=src)
+    try:
+        with open(_TABLE_PATH) as f:
+            doc = json.load(f)
+    except (OSError, ValueError) as e:
+        _table_info["status"] = f"unreadable ({type(e).__name__})"
+        return _table
+    ent = doc.get(arch)
+    if not ent:
+        _table_info["status"] = f"no plans for {arch or 'this device'}"
+    elif src is None or ent.get("gemm_src_hash") != src:
+        _table_info["status"] = f"stale (tuned for GEMM sources {ent.get('gemm_src_hash')}, library has {src})"
+    else:
+        _table = {k: (v[0], int(v[1])) for k, v in ent.get("plans", {}).items()}
+        _table_info.update(status="loaded", entries=len(_table))
+    return _table
+
+
+def plan_stats() -> dict:
+    """Where this process's GEMM plan came from: ``source`` = "table" (every signature from the
+    committed table), "table+tuned" (some tuned: ``misses`` counts them) or "tuned"."""
+    hits, miss = len(_table_hits), len(_table_misses)
+    src = "table" if hits and not miss else "table+tuned" if hits else "tuned"
+    return dict(_table_info, source=src, table_hits=hits, misses=miss)
+
+
+@contextlib.contextmanager
+def plan_usage():
+    """Collect the signatures looked up inside the block: ``with plan_usage() as used: ...``."""
+    global _used
+    prev, _used = _used, set()
+    try:
+        yield _used
+    finally:
+        _used = prev
+
+
+def current_plan(keys) -> dict:
+    """(kernel, splits) of each signature in ``keys`` as this process runs it."""
+    tab = load_plan_table()
+    out = {}
+    for k in keys:
+        v = _tuned.get(k) or tab.get(k)
+        if v is not None:
+            out[k] = v
+    return out
+
 
 def _load_cache() -> None:
     if not _CACHE_PATH or not os.path.exists(_CACHE_PATH):
@@ -703,7 +788,15 @@ def _choose(mode, A, lda, B, ldb, C, ldc, M, N, K, bias, act, aux, splits, conv,
     elif _TUNE and not _force_small and C.is_cuda:
         key = f"{mode}|{M}|{N}|{K}|{lda}|{ldb}|{ldc}|{tuple(conv) if conv is not None else ''}|{int(row_remap)}|" \
               f"{act}|{C.dtype}|{int(bias is not None)}|{int(colstats is not None)}|{int(residual is not None)}"
+        if _used is not None:
+            _used.add(key)
         choice = _tuned.get(key)
+        if choice is None:
+            choice = load_plan_table().get(key)
+            if choice is not None:
+                _table_hits.add(key)
+            else:
+                _table_misses.add(key)
         if choice is None and online_ok and _online_active and not torch.cuda.is_current_stream_capturing() \
                 and (A.numel() + B.numel() + C.numel()) * C.element_size() <= _online_max_bytes:
             global _online_last

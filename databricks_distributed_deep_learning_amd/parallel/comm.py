@@ -318,17 +318,39 @@ class NativeComm:
 
 
 # ---------------------------------------------------------------------- bucket policy
+class TorchCollectives:
+    """The ``all_reduce(t)`` / ``wait()`` contract of :func:`probe_allreduce` over a plain
+    ``torch.distributed`` group: the auto bucket policy's probe where the native engine is not
+    used (gloo on the CPU, or ``comm="torch"`` on GPUs)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def all_reduce(self, t: torch.Tensor) -> int:
+        dist.all_reduce(t, group=self.group)
+        return 0
+
+    def wait(self) -> None:
+        pass
+
+
 def probe_allreduce(engine, device, sizes_mb: Sequence[float] = (1, 4, 16, 64), iters: int = 5,
-                    dtype: torch.dtype = torch.bfloat16, world: Optional[int] = None) -> List[Dict[str, float]]:
+                    dtype: torch.dtype = torch.bfloat16, world: Optional[int] = None,
+                    agree: bool = True) -> List[Dict[str, float]]:
     """Time all-reduces of each size on ``engine`` (``all_reduce(t)`` + ``wait()``: the native
     engine, or any stand-in with that contract): one warm-up, then the median of ``iters``
     host-timed calls with the device synchronised around each.  Returns per size: MB, ms,
     algorithm bandwidth (GB/s = bytes / t) and bus bandwidth (x 2(n-1)/n, the per-link figure
-    of a ring: comparable across world sizes).  Every rank must call it (collective)."""
+    of a ring: comparable across world sizes).  Every rank must call it (collective).
+
+    ``agree``: each size's time is the MAX over the world's ranks (one scalar all-reduce), so every
+    rank derives the same bucket layout from the probe -- per-rank host timings differ, and ranks
+    whose buckets differ would issue all-reduces of different sizes against each other."""
+    from . import dist as ddist
     n = int(world if world is not None else dist.get_world_size())
     esz = torch.empty((), dtype=dtype).element_size()
     sync = torch.cuda.synchronize if torch.device(device).type == "cuda" else (lambda: None)
-    out = []
+    rows = []
     for mb in sizes_mb:
         t = torch.ones(max(1, int(mb * (1 << 20)) // esz), dtype=dtype, device=device)
         times = []
@@ -340,10 +362,15 @@ def probe_allreduce(engine, device, sizes_mb: Sequence[float] = (1, 4, 16, 64), 
             sync()
             if i:
                 times.append(time.perf_counter() - t0)
-        ms = 1e3 * sorted(times)[len(times) // 2]
-        nbytes = t.numel() * esz
-        alg = nbytes / (ms * 1e-3) / 1e9
-        out.append({"mb": float(mb), "ms": round(ms, 4), "algbw_gbs": round(alg, 2),
+        rows.append((float(mb), 1e3 * sorted(times)[len(times) // 2], t.numel() * esz))
+    ms_all = [r[1] for r in rows]
+    if agree and n > 1 and dist.is_available() and dist.is_initialized():
+        ms_all = ddist.all_reduce_scalars(ms_all, op="max")
+    out = []
+    for (mb, _, nbytes), ms in zip(rows, ms_all):
+        ms = round(ms, 4)
+        alg = nbytes / (max(ms, 1e-6) * 1e-3) / 1e9
+        out.append({"mb": mb, "ms": ms, "algbw_gbs": round(alg, 2),
                     "busbw_gbs": round(alg * 2 * (n - 1) / max(n, 1), 2)})
     return out
 

@@ -110,19 +110,29 @@ class Trainer:
         # (the watchdog runs from the engine's construction on, so a peer lost during the probe
         # aborts the communicator instead of hanging the rank)
         self.rehearsal = False
+        from ..parallel.comm import CommError, NativeComm, TorchCollectives, native_available, probe_allreduce
+
+        def torch_path(comm):
+            # no native engine: the auto bucket policy still probes, over the process group itself
+            # (gloo on the CPU: smaller messages, the same latency-bandwidth fit)
+            if self.world > 1 and (c.comm_probe or c.bucket_mb <= 0):
+                cpu = self.device.type != "cuda"
+                sizes = (0.25, 1, 4) if cpu else (1, 4, 16, 64)
+                return comm, probe_allreduce(TorchCollectives(), self.device, sizes_mb=sizes, iters=3 if cpu else 5,
+                                             dtype=reduce_dtype or self.arena.dtype, world=self.world)
+            return comm, []
         if c.comm not in ("auto", "native") or self.device.type != "cuda":
-            return c.comm, []
+            return torch_path(c.comm)
         if self.world == 1 and not c.dp_rehearsal:
             return c.comm, []
-        from ..parallel.comm import CommError, NativeComm, native_available, probe_allreduce
         if not native_available():
-            return c.comm, []
+            return torch_path(c.comm)
         try:
             eng = NativeComm()
         except CommError:
             if c.comm == "native":
                 raise
-            return "torch", []
+            return torch_path("torch")
         self.rehearsal = self.world == 1
         probe = []
         if self.world > 1 and (c.comm_probe or c.bucket_mb <= 0):

@@ -15,6 +15,9 @@
 #   pmc MODEL             3 PMC passes summarised             -> gpurun_out/pmc_MODEL.md
 #   presets               every BASELINE preset through the train() CLI
 #   rehearse2             2 ranks on this one GPU over gloo through bench.py's own launcher
+#   tuneplans             tune every benchmark / preset GEMM signature with the plan table off
+#                         -> gpurun_out/plans/cache.json (scripts/make_plan_table.py turns it into
+#                         ops/gemm_plans.json)
 #   script FILE [args]    any python script under a 300 s limit (debug / microbenchmarks)
 #
 # MODEL for prof/pmc: resnet50 | bert_base (bench.py) or vit_b16 | bert_large_lamb (train CLI).
@@ -122,6 +125,18 @@ step() {
           || { tail -20 "gpurun_out/preset_$pn.log"; return 1; }
         echo "$pn: $(tail -1 "gpurun_out/preset_$pn.log" | cut -c1-400)"
       done ;;
+    tuneplans)
+      mkdir -p gpurun_out/plans
+      rm -f gpurun_out/plans/cache.json
+      for cmd in "python3 bench.py --steps 3 --warmup 5" "python3 bench.py --model vit_b16 --steps 3 --warmup 5" \
+                 "python3 bench.py --model bert_large --steps 2 --warmup 3" \
+                 "$TRAIN --preset bert_large_lamb --steps 1 --warmup_steps 2 --log_every 0"; do
+        # shellcheck disable=SC2086
+        DDL_GEMM_PLAN_TABLE=0 DDL_GEMM_TUNE_CACHE=gpurun_out/plans/cache.json timeout -k 10 400 $cmd \
+          > gpurun_out/plans/tune.log 2>&1 || { tail -20 gpurun_out/plans/tune.log; return 1; }
+        echo "$cmd: $(tail -1 gpurun_out/plans/tune.log | cut -c1-200)"
+      done
+      python3 -c "import json; print(len(json.load(open('gpurun_out/plans/cache.json'))), 'signatures')" ;;
     rehearse2)
       DDL_BACKEND=gloo timeout -k 10 500 python bench.py --gpus 2 --steps 3 --warmup 1 --batch 64 --bert-batch 32 \
         > gpurun_out/rehearse2.log 2>&1 || { tail -30 gpurun_out/rehearse2.log; return 1; }

@@ -547,3 +547,61 @@ def test_bf16_gradient_reduce_error_world8():
     if out["gloo_bf16"] is not None:
         assert out["gloo_bf16"] < 0.01, out
     print("bf16 vs fp32 reduce error (8 ranks):", out)
+
+
+def _auto_bucket_policy_trainer():
+    """Trainer with bucket_mb = 0 ("auto"): probe -> auto_buckets -> bucket layout, end to end."""
+    import torch.distributed as dist
+    from databricks_distributed_deep_learning_amd.config import get_preset
+    from databricks_distributed_deep_learning_amd.parallel.comm import auto_buckets
+    from databricks_distributed_deep_learning_amd.training.loop import Trainer
+    cfg = get_preset("resnet18_gloo", batch_size=2, image_size=32, steps=1, warmup_steps=0, num_classes=10,
+                     bucket_mb=0.0, log_every=0)
+    tr = Trainer(cfg)
+    s = tr.run()
+    esz = torch.empty((), dtype=tr.ddp.reduce_dtype).element_size()
+    total = tr.arena.numel * esz / 2 ** 20
+    want = auto_buckets(s["comm_probe"], total) if s.get("comm_probe") else None
+    # the layout those sizes give (the reducer's own rule), to compare with the one it built
+    layout = [(b.end - b.start) * esz / 2 ** 20 for b in tr.ddp._build_buckets(want[1], want[0])] if want else None
+    out = {"policy": s["bucket_policy"], "probe": s.get("comm_probe"), "buckets": s["buckets_mb"],
+           "want": want, "layout": layout, "total": total,
+           "world": dist.get_world_size(), "rank": dist.get_rank(), "loss": s["final_loss"]}
+    tr.close()
+    return out
+
+
+def _gather_all(fn):
+    import torch.distributed as dist
+    out = fn()
+    allv = [None] * dist.get_world_size()
+    dist.all_gather_object(allv, out)
+    return allv
+
+
+def _auto_bucket_policy_all_ranks():
+    return _gather_all(_auto_bucket_policy_trainer)
+
+
+def test_auto_bucket_policy_end_to_end_world8():
+    """8 gloo ranks through the Trainer with the default "auto" bucket size:
+    the startup all-reduce probe runs (over the process group: no native engine on the CPU),
+    every rank derives the SAME (first, bucket) sizes from it (the probe's per-size times are
+    the max over ranks -- per-rank timings would otherwise give ranks different bucket layouts,
+    i.e. mismatched all-reduces), and the reducer's buckets follow those sizes."""
+    ranks = Distributor(num_processes=8, use_gpu=False).run(_auto_bucket_policy_all_ranks)
+    assert len(ranks) == 8 and sorted(r["rank"] for r in ranks) == list(range(8))
+    r0 = ranks[0]
+    assert r0["world"] == 8 and r0["policy"]["source"] == "probe", r0["policy"]
+    assert [p["mb"] for p in r0["probe"]] == [0.25, 1.0, 4.0]
+    first, bucket = r0["want"]
+    assert (r0["policy"]["first_bucket_mb"], r0["policy"]["bucket_mb"]) == (first, bucket)
+    for r in ranks[1:]:
+        assert r["probe"] == r0["probe"] and r["policy"] == r0["policy"] and r["buckets"] == r0["buckets"], r
+    b = r0["buckets"]
+    assert abs(sum(b) - r0["total"]) < 0.005 * len(b) + 1e-3, (b, r0["total"])   # (2-decimal MB)
+    # the reducer's buckets are the layout of exactly those sizes (whole tensors per bucket, closed
+    # by the tensor reaching the cap; tensors above a bucket cut into pieces of their own)
+    assert [round(x, 2) for x in b] == [round(x, 2) for x in r0["layout"]], (b, r0["layout"])
+    assert all(x < 2 * bucket + 0.01 for x in b), (b, bucket)
+    assert all(abs(r["loss"] - r0["loss"]) < 1e-6 for r in ranks)

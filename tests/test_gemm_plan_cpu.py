@@ -165,3 +165,48 @@ def test_duo_candidate_contract():
     assert ("duo", 1) in cands
     cands = NG._tune_candidates(NG.MODE_TN, 768, 3072, 16384, 768, 3072, None, None, None, False, None, None)
     assert ("duo", 1) not in cands
+
+
+# ---------------------------------------------------------------- committed plan table
+def _fresh_table(monkeypatch, tmp_path, doc, arch="gfx950", src="abc"):
+    path = tmp_path / "plans.json"
+    path.write_text(__import__("json").dumps(doc))
+    monkeypatch.setattr(NG, "_TABLE_ENV", str(path))
+    monkeypatch.setattr(NG, "_TABLE_PATH", str(path))
+    monkeypatch.setattr(NG, "_table", None)
+    monkeypatch.setattr(NG, "_table_info", dict(NG._table_info))
+    monkeypatch.setattr(NG, "_device_arch", lambda: arch)
+    monkeypatch.setattr(NG._lib, "gemm_src_hash", lambda: src)
+    return NG.load_plan_table()
+
+
+def test_plan_table_loads_for_matching_arch_and_sources(monkeypatch, tmp_path):
+    """The committed table applies only to the GPU architecture and GEMM-kernel build it was tuned
+    on: another source hash or architecture leaves it unused (tuning takes over)."""
+    doc = {"gfx950": {"gemm_src_hash": "abc", "plans": {"0|16384|768|768": ["big192", 1], "2|768|768|16384": ["duo", 4]}}}
+    t = _fresh_table(monkeypatch, tmp_path, doc)
+    assert t == {"0|16384|768|768": ("big192", 1), "2|768|768|16384": ("duo", 4)}
+    assert NG.plan_stats()["status"] == "loaded" and NG.plan_stats()["entries"] == 2
+    assert _fresh_table(monkeypatch, tmp_path, doc, src="other") == {}
+    assert NG.plan_stats()["status"].startswith("stale")
+    assert _fresh_table(monkeypatch, tmp_path, doc, arch="gfx942") == {}
+    assert _fresh_table(monkeypatch, tmp_path, doc, src=None) == {}
+
+
+def test_plan_table_is_in_sync_with_the_tree():
+    """ops/gemm_plans.json's gfx950 entry was tuned against the GEMM kernel sources in this tree
+    (a kernel edit without re-tuning would silently drop the committed plan: the bench's
+    plan_source would read 'tuned').  Every entry names a kernel kind the launcher knows."""
+    import json
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "csrc"))
+    import build as native_build
+    with open(os.path.join(root, "databricks_distributed_deep_learning_amd", "ops", "gemm_plans.json")) as f:
+        doc = json.load(f)
+    ent = doc["gfx950"]
+    assert ent["gemm_src_hash"] == native_build.gemm_src_hash()
+    assert len(ent["plans"]) > 50
+    for k, (kind, s) in ent["plans"].items():
+        assert kind in NG._KINDS and int(s) >= 1, (k, kind, s)
