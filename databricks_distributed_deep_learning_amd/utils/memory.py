@@ -40,10 +40,17 @@ def fit_batch_size(step_fn: Callable[[int], None], device: torch.device, start: 
     per_sample = p0 / b0
     est = int((budget - static) / max(per_sample, 1.0))
     est = max(b0, min(max_batch, est // multiple * multiple))
+    # the candidate must FIT THE BUDGET, not merely run: a probe that squeezed into the last few GB
+    # left nothing for what the probe step does not do (optimizer scratch, the fp32 accumulation
+    # arena, GEMM tuning workspaces at an untuned batch) -- BERT-large LAMB went out of memory in its
+    # first real step that way (round 6).  Over budget: shrink in proportion and probe again.
     while est > b0:
         try:
-            peak_at(est)
-            return est
+            p = peak_at(est)
         except torch.cuda.OutOfMemoryError:
             est = max(b0, int(est * 0.8) // multiple * multiple)
+            continue
+        if static + p <= budget:
+            return est
+        est = max(b0, min(est - multiple, int(est * (budget - static) / p)) // multiple * multiple)
     return b0

@@ -69,3 +69,39 @@ def test_phase_timer_pending_is_bounded():
         assert len(pt._pending) <= 4
     out = pt.summary(reset=True)
     assert pt.steps == 0 and set(out) == {"fwd_ms", "bwd_ms"}
+
+
+def test_fit_batch_size_keeps_the_budget(monkeypatch):
+    """HBM batch sizing (N13) on a simulated 288 GB device whose per-sample memory grows faster
+    than the small-batch probe predicts: the chosen batch's probe peak must fit the budget
+    (1 - headroom of the device), not merely avoid an out-of-memory error -- round 6's BERT-large
+    preset picked a batch that ran at 99 % of HBM and went out of memory in its first real step."""
+    import torch
+    from databricks_distributed_deep_learning_amd.utils.memory import fit_batch_size
+    GB = 1 << 30
+    total, static = 288 * GB, 20 * GB
+    state = {"peak": 0}
+
+    def need(b):                  # superlinear activation memory: the probe at b = 8 under-predicts
+        return int(0.4 * GB * b + 0.0004 * GB * b * b)
+
+    class Props:
+        total_memory = total
+
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: Props())
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda d=None: None)
+    monkeypatch.setattr(torch.cuda, "reset_peak_memory_stats", lambda d=None: state.update(peak=0))
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda d=None: static)
+    monkeypatch.setattr(torch.cuda, "max_memory_allocated", lambda d=None: static + state["peak"])
+    probes = []
+
+    def step(b):
+        probes.append(b)
+        if static + need(b) > total:
+            raise torch.cuda.OutOfMemoryError("simulated")
+        state["peak"] = need(b)
+
+    b = fit_batch_size(step, torch.device("cuda", 0), start=8, headroom=0.15)
+    assert b % 8 == 0 and static + need(b) <= 0.85 * total, (b, probes)
+    assert static + need(b + 8) > 0.85 * total * 0.97, (b, probes)   # and not far below it
