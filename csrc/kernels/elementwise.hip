@@ -1001,3 +1001,191 @@ DDL_API int ddl_softmax_topk(int dtype, const void* logits, long B, int C, int k
                (softmax_topk_k<float><<<B, 256, 0, st>>>((const float*)logits, C, k, probs, top_v, top_i)));
     DDL_RETURN_LAUNCH();
 }
+
+// ======================================================================= step glue
+// Small kernels that replace the ATen launches still left in a training step: the pooler's tanh
+// backward, zero-padded / strided 2-D copies (classifier-head padding, first-token gather and its
+// backward), in-place adds into gradient slots, the gradient-arena zero fill, and the embedding
+// backward's stable id sort.  Each is one launch where ATen took two to six.
+namespace {
+
+// dz = dy * (1 - y^2) (tanh from its output), 8 elements per thread
+template <typename T>
+__global__ __launch_bounds__(256) void tanh_bwd_k(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dz,
+                                                  long n8) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        float g[8], v[8];
+        load8(dy + i * 8, g);
+        load8(y + i * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] *= 1.f - v[e] * v[e];
+        store8(dz + i * 8, g);
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void tanh_bwd_tail_k(const T* __restrict__ dy, const T* __restrict__ y,
+                                                       T* __restrict__ dz, long n0, long n) {
+    const long i = n0 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float v = to_f(y[i]);
+        dz[i] = from_f<T>(to_f(dy[i]) * (1.f - v * v));
+    }
+}
+
+// dst[r][c] = (r < srows && c < scols) ? src[r][c] : 0 for r < drows, c < dcols (element strides ldd / lds):
+// zero padding, slicing and strided gathers in one pass; V = 8 when every row start is 16-byte aligned
+template <typename T, int V>
+__global__ __launch_bounds__(256) void copy2d_k(T* __restrict__ dst, long ldd, long drows, long dcols,
+                                                const T* __restrict__ src, long lds, long srows, long scols) {
+    const long cv = dcols / V, total = drows * cv;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long r = i / cv, c = (i - r * cv) * V;
+        if constexpr (V == 8) {
+            float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (r < srows && c + 8 <= scols) load8(src + r * lds + c, v);
+            else if (r < srows && c < scols)
+                for (int e = 0; e < 8; ++e) v[e] = c + e < scols ? to_f(src[r * lds + c + e]) : 0.f;
+            store8(dst + r * ldd + c, v);
+        } else {
+            dst[r * ldd + c] = (r < srows && c < scols) ? src[r * lds + c] : from_f<T>(0.f);
+        }
+    }
+}
+
+// dst (+)= src, same dtype (a returned gradient folded into its arena slot)
+template <typename T>
+__global__ __launch_bounds__(256) void add_into_k(T* __restrict__ dst, const T* __restrict__ src, long n) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        dst[i] = from_f<T>(to_f(dst[i]) + to_f(src[i]));
+}
+
+// dst[r][c] = a[r][c] + v[c] (the embedding residual: position rows + the token-type row)
+template <typename T>
+__global__ __launch_bounds__(256) void rows_add_row_k(T* __restrict__ dst, const T* __restrict__ a, const T* __restrict__ v,
+                                                      long rows, long cols) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.x * blockDim.x)
+        dst[i] = from_f<T>(to_f(a[i]) + to_f(v[i % cols]));
+}
+
+__global__ __launch_bounds__(256) void zero16_k(uint4* __restrict__ p, long n16) {
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) p[i] = z;
+}
+__global__ void zero_bytes_k(unsigned char* __restrict__ p, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+
+// Stable sort of n <= 32768 token ids in ONE workgroup: key = id * n + position (unique, ordered by
+// (id, position): any sort of these keys is the stable sort of the ids), a bitonic network over the
+// keys in LDS (padded to a power of two with ~0u), then s = key / n, pi = key % n.  One launch
+// instead of rocPRIM's block sort + merge passes + ATen's index fill and int32 cast.
+__global__ __launch_bounds__(1024) void sort_ids_k(const int64_t* __restrict__ ids, int n, int npow2,
+                                                   int* __restrict__ s, int64_t* __restrict__ pi) {
+    extern __shared__ uint32_t keys[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < npow2; i += 1024) keys[i] = i < n ? (uint32_t)ids[i] * (uint32_t)n + (uint32_t)i : ~0u;
+    __syncthreads();
+    const int half = npow2 >> 1;
+    for (int k = 2; k <= npow2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < half; i += 1024) {
+                const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+                const uint32_t a = keys[lo], b = keys[hi];
+                if ((a > b) == ((lo & k) == 0)) {
+                    keys[lo] = b;
+                    keys[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < n; i += 1024) {
+        const uint32_t kk = keys[i];
+        s[i] = (int)(kk / (uint32_t)n);
+        pi[i] = (int64_t)(kk % (uint32_t)n);
+    }
+}
+
+}  // namespace
+
+DDL_API int ddl_tanh_bwd(int dtype, const void* dy, const void* y, void* dz, long n, hipStream_t st) {
+    const long n8 = n / 8, tail = n - n8 * 8;
+    if (n8 > 0)
+        DISPATCH_T(dtype,
+                   (tanh_bwd_k<bf16_t><<<grid_for(n8), 256, 0, st>>>((const bf16_t*)dy, (const bf16_t*)y, (bf16_t*)dz, n8)),
+                   (tanh_bwd_k<float><<<grid_for(n8), 256, 0, st>>>((const float*)dy, (const float*)y, (float*)dz, n8)));
+    if (tail > 0)
+        DISPATCH_T(dtype,
+                   (tanh_bwd_tail_k<bf16_t><<<1, 256, 0, st>>>((const bf16_t*)dy, (const bf16_t*)y, (bf16_t*)dz, n8 * 8, n)),
+                   (tanh_bwd_tail_k<float><<<1, 256, 0, st>>>((const float*)dy, (const float*)y, (float*)dz, n8 * 8, n)));
+    DDL_RETURN_LAUNCH();
+}
+
+// zero-padded / strided 2-D copy (element strides); dst and src must not overlap
+DDL_API int ddl_copy2d(int dtype, void* dst, long ldd, long drows, long dcols, const void* src, long lds, long srows,
+                       long scols, hipStream_t st) {
+    if (drows <= 0 || dcols <= 0) return 0;
+    const int esz = dtype == 1 ? 2 : 4;
+    const bool v8 = dtype == 1 && dcols % 8 == 0 && ldd % 8 == 0 && lds % 8 == 0 &&
+                    ((uintptr_t)dst % 16) == 0 && (scols == 0 || ((uintptr_t)src % 16) == 0);
+    (void)esz;
+    const long work = v8 ? drows * (dcols / 8) : drows * dcols;
+    if (v8)
+        copy2d_k<bf16_t, 8><<<grid_for(work), 256, 0, st>>>((bf16_t*)dst, ldd, drows, dcols, (const bf16_t*)src, lds,
+                                                            srows, scols);
+    else
+        DISPATCH_T(dtype,
+                   (copy2d_k<bf16_t, 1><<<grid_for(work), 256, 0, st>>>((bf16_t*)dst, ldd, drows, dcols,
+                                                                      (const bf16_t*)src, lds, srows, scols)),
+                   (copy2d_k<float, 1><<<grid_for(work), 256, 0, st>>>((float*)dst, ldd, drows, dcols,
+                                                                     (const float*)src, lds, srows, scols)));
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_add_into(int dtype, void* dst, const void* src, long n, hipStream_t st) {
+    if (n <= 0) return 0;
+    DISPATCH_T(dtype, (add_into_k<bf16_t><<<grid_for(n), 256, 0, st>>>((bf16_t*)dst, (const bf16_t*)src, n)),
+               (add_into_k<float><<<grid_for(n), 256, 0, st>>>((float*)dst, (const float*)src, n)));
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_rows_add_row(int dtype, void* dst, const void* a, const void* v, long rows, long cols, hipStream_t st) {
+    if (rows * cols <= 0) return 0;
+    DISPATCH_T(dtype,
+               (rows_add_row_k<bf16_t><<<grid_for(rows * cols), 256, 0, st>>>((bf16_t*)dst, (const bf16_t*)a,
+                                                                            (const bf16_t*)v, rows, cols)),
+               (rows_add_row_k<float><<<grid_for(rows * cols), 256, 0, st>>>((float*)dst, (const float*)a,
+                                                                           (const float*)v, rows, cols)));
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_zero(void* p, long nbytes, hipStream_t st) {
+    if (nbytes <= 0) return 0;
+    unsigned char* b = (unsigned char*)p;
+    long head = (long)((16 - ((uintptr_t)b & 15)) & 15);
+    if (head > nbytes) head = nbytes;
+    if (head) zero_bytes_k<<<1, 64, 0, st>>>(b, head);
+    const long n16 = (nbytes - head) / 16;
+    if (n16 > 0) zero16_k<<<grid_for(n16), 256, 0, st>>>((uint4*)(b + head), n16);
+    const long tail = nbytes - head - n16 * 16;
+    if (tail > 0) zero_bytes_k<<<1, 64, 0, st>>>(b + head + n16 * 16, tail);
+    DDL_RETURN_LAUNCH();
+}
+
+// 1 when ddl_sort_ids can sort n ids below vocab (else the caller sorts another way)
+DDL_API int ddl_sort_ids_ok(long n, long vocab) {
+    return n > 0 && n <= 32768 && (unsigned long long)vocab * (unsigned long long)n < (1ull << 32) ? 1 : 0;
+}
+
+DDL_API int ddl_sort_ids(const int64_t* ids, long n, int* s, int64_t* pi, hipStream_t st) {
+    if (n <= 0 || n > 32768) return -1;
+    int npow2 = 1;
+    while (npow2 < n) npow2 <<= 1;
+    if (npow2 < 2) npow2 = 2;
+    static const bool big_lds = hipFuncSetAttribute((const void*)sort_ids_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    32768 * 4) == hipSuccess;
+    if (npow2 > 16384 && !big_lds) return -1;
+    sort_ids_k<<<1, 1024, (size_t)npow2 * 4, st>>>(ids, (int)n, npow2, s, pi);
+    DDL_RETURN_LAUNCH();
+}

@@ -65,12 +65,13 @@ class BertEmbeddings(nn.Module):
     def forward(self, input_ids, token_type_ids=None):
         B, S = input_ids.shape
         we = self.word_embeddings(input_ids)
-        pe = self.position_embeddings.weight[:S].unsqueeze(0)
         if token_type_ids is None:
-            te = self.token_type_embeddings.weight[0].view(1, 1, -1)
+            # position rows + token type 0 in one native pass; its backward writes both parameters'
+            # gradient slots directly (ops/glue.py)
+            r = ops.embedding_residual(self.position_embeddings.weight, self.token_type_embeddings.weight, S)
         else:
-            te = self.token_type_embeddings(token_type_ids)
-        h = self.LayerNorm(we, residual=pe + te)
+            r = self.position_embeddings.weight[:S].unsqueeze(0) + self.token_type_embeddings(token_type_ids)
+        h = self.LayerNorm(we, residual=r)
         return self.dropout(h)
 
 
@@ -123,7 +124,7 @@ class BertModel(nn.Module):
         h = self.embeddings(input_ids, token_type_ids)
         for layer in self.layers:
             h = layer(h, mask_bias)
-        pooled = self.pooler(h[:, 0].contiguous())
+        pooled = self.pooler(ops.first_token(h))
         return h, pooled
 
 

@@ -143,6 +143,15 @@ _SIGS = {
     "ddl_conv_w_dgrad_batch": [P, P, I, P],
     "ddl_gelu_bwd_colsum": [I, P, P, P, L, I, P, P, I, I, P],
     "ddl_acc_f32": [I, P, P, L, P],
+    # step glue (elementwise.hip): tanh backward, zero-padded 2-D copies, adds into gradient slots,
+    # the gradient-arena zero fill, the embedding backward's id sort
+    "ddl_tanh_bwd": [I, P, P, P, L, P],
+    "ddl_copy2d": [I, P, L, L, L, P, L, L, L, P],
+    "ddl_add_into": [I, P, P, L, P],
+    "ddl_zero": [P, L, P],
+    "ddl_rows_add_row": [I, P, P, P, L, L, P],
+    "ddl_sort_ids_ok": [L, L],
+    "ddl_sort_ids": [P, L, P, P, P],
     "ddl_drain_acc": [I, P, P, L, P],
     "ddl_softmax_topk": [I, P, L, I, I, P, P, P, P],
     "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],

@@ -1,6 +1,8 @@
 """Autograd bindings for GELU / dropout (csrc/kernels/elementwise.hip)."""
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from ._lib import call, dcode, p
@@ -69,3 +71,35 @@ def colsum(x2d: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> to
     part = torch.empty(nblk * C, dtype=torch.float32, device=x2d.device)
     call("ddl_colsum", dcode(x2d), p(x2d), rows, C, p(part), p(out), dcode(out), int(accumulate))
     return out
+
+
+# ------------------------------------------------------------------ step glue (native, no ATen launches)
+def tanh_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """dz = dy * (1 - y^2) from tanh's output."""
+    dy, y = dy.contiguous(), y.contiguous()
+    dz = torch.empty_like(dy)
+    call("ddl_tanh_bwd", dcode(dy), p(dy), p(y), p(dz), dy.numel())
+    return dz
+
+
+def copy2d(dst: torch.Tensor, src: Optional[torch.Tensor], ldd: int, drows: int, dcols: int, lds: int = 0,
+           srows: int = 0, scols: int = 0) -> torch.Tensor:
+    """dst[r, c] = src[r, c] inside src's (srows x scols) window, 0 elsewhere, for r < drows, c < dcols
+    (element strides ldd / lds): zero padding, slicing and strided row gathers in one launch."""
+    assert src is None or src.dtype == dst.dtype
+    call("ddl_copy2d", dcode(dst), p(dst), ldd, drows, dcols, p(src), lds, srows if src is not None else 0,
+         scols if src is not None else 0)
+    return dst
+
+
+def add_into(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """dst += src in place (same dtype, contiguous)."""
+    assert dst.dtype == src.dtype and dst.numel() == src.numel() and dst.is_contiguous() and src.is_contiguous()
+    call("ddl_add_into", dcode(dst), p(dst), p(src), dst.numel())
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """Native zero fill of a contiguous tensor."""
+    assert t.is_contiguous()
+    call("ddl_zero", p(t), t.numel() * t.element_size())
+    return t

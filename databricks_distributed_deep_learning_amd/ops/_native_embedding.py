@@ -10,6 +10,7 @@ import os
 
 import torch
 
+from . import _lib
 from ._lib import call, dcode, grad_ready, grad_sink, p
 
 
@@ -39,8 +40,14 @@ class _Embedding(torch.autograd.Function):
         if _SORTED and n > 0:
             # untouched rows: the sink keeps its value (accumulate), a fresh gradient starts at zero
             dw = sink if sink is not None else torch.zeros(V, D, dtype=ctx.wdtype, device=dy.device)
-            # int32 keys (V < 2^31): the radix sort makes half the passes of an int64 one
-            s, pi = torch.sort(ids.view(-1).to(torch.int32), stable=True)
+            if _lib.fn("ddl_sort_ids_ok")(n, V):
+                # one native launch: a bitonic sort of (id, position) keys in one workgroup's LDS
+                s = torch.empty(n, dtype=torch.int32, device=dy.device)
+                pi = torch.empty(n, dtype=torch.int64, device=dy.device)
+                call("ddl_sort_ids", p(ids), n, p(s), p(pi))
+            else:
+                # int32 keys (V < 2^31): the radix sort makes half the passes of an int64 one
+                s, pi = torch.sort(ids.view(-1).to(torch.int32), stable=True)
             part = torch.empty(2 * ((n + 15) // 16) * D, dtype=torch.float32, device=dy.device)
             call("ddl_embedding_bwd_sorted", dcode(dy), p(s), p(pi), p(dy), p(dw), p(part), n, D,
                  int(sink is not None))

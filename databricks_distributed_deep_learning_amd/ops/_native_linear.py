@@ -40,7 +40,9 @@ class _LinearPadN(torch.autograd.Function):
     """y = x W^T (+ b) (tanh / relu) for N % 8 != 0 on the native GEMMs: W, b and dy are
     zero-padded to Np = roundup(N, 8) rows / columns (a few KB for a classifier head), so the
     forward NT, the dgrad NN (reduction over Np) and the weight-gradient TN are the same
-    MFMA kernels as every other Linear -- no vendor GEMM runs for the head."""
+    MFMA kernels as every other Linear -- no vendor GEMM runs for the head.  The padded W / b are
+    cached per parameter version (rebuilt once per optimizer step), every pad / slice is one native
+    ``ddl_copy2d`` launch, and the gradients go straight into the arena slots."""
 
     @staticmethod
     def forward(ctx, x, w, b, act):
@@ -50,17 +52,13 @@ class _LinearPadN(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         M = x2.shape[0]
-        wp = torch.zeros(Np, K, dtype=w.dtype, device=w.device)
-        wp[:N] = w
-        bp = None
-        if b is not None:
-            bp = torch.zeros(Np, dtype=b.dtype, device=b.device)
-            bp[:N] = b
+        wp, bp = _padded(w, b, Np)
         y = torch.empty(M, Np, dtype=x.dtype, device=x.device)
         gemm(MODE_NT, x2, K, wp, K, y, Np, M, Np, K, bias=bp, act=act if act in ("tanh", "relu") else None)
-        out = y[:, :N].contiguous()
+        out = E.copy2d(torch.empty(M, N, dtype=x.dtype, device=x.device), y, N, M, N, Np, M, N)
         ctx.save_for_backward(x2, wp, out if act in ("tanh", "relu") else None)
         ctx.act, ctx.has_bias, ctx.xshape, ctx.N = act, b is not None, x.shape, N
+        ctx.w_param, ctx.b_param = w, b
         return out.view(*x.shape[:-1], N)
 
     @staticmethod
@@ -70,11 +68,11 @@ class _LinearPadN(torch.autograd.Function):
         N, Np = ctx.N, wp.shape[0]
         dy2 = dy.reshape(M, N)
         if ctx.act == "tanh":
-            dy2 = (dy2.float() * (1 - y.float() ** 2)).to(dy2.dtype)
+            dy2 = E.tanh_bwd(dy2, y)
         elif ctx.act == "relu":
             dy2 = dy2 * (y > 0)
-        dyp = torch.zeros(M, Np, dtype=dy2.dtype, device=dy2.device)
-        dyp[:, :N] = dy2
+        dy2 = dy2.contiguous()
+        dyp = E.copy2d(torch.empty(M, Np, dtype=dy2.dtype, device=dy2.device), dy2, Np, M, Np, N, M, N)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=x2.dtype, device=x2.device)
@@ -83,12 +81,45 @@ class _LinearPadN(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dwp = torch.empty(Np, K, dtype=wp.dtype, device=wp.device)
             gemm(MODE_TN, dyp, Np, x2, K, dwp, K, Np, K, M)
-            dw = dwp[:N]
+            sink = grad_sink(ctx.w_param)
+            if sink is not None and sink.dtype == dwp.dtype:
+                E.add_into(sink.view(-1), dwp[:N].reshape(-1))     # rows 0..N-1: contiguous
+                grad_ready(ctx.w_param)
+            else:
+                dw = dwp[:N]
         if ctx.has_bias and ctx.needs_input_grad[2]:
             dbp = torch.empty(Np, dtype=wp.dtype, device=wp.device)
             E.colsum(dyp, dbp)
-            db = dbp[:N]
+            sink = grad_sink(ctx.b_param)
+            if sink is not None and sink.dtype == dbp.dtype:
+                E.add_into(sink.view(-1), dbp[:N])
+                grad_ready(ctx.b_param)
+            else:
+                db = dbp[:N]
         return dx, dw, db, None
+
+
+def _padded(w: torch.Tensor, b: Optional[torch.Tensor], Np: int):
+    """W zero-padded to Np rows (and b to Np), cached on the parameter until its values change (the
+    same version key as the W^T cache below)."""
+    ref = getattr(w, "_ddl_arena", None)
+    arena = ref() if ref is not None else None
+    key = (w.data_ptr(), w._version, Np, arena.generation if arena is not None else -1,
+           None if b is None else (b.data_ptr(), b._version))
+    c = getattr(w, "_ddl_padn", None)
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    N, K = w.shape
+    wc = w.contiguous()
+    wp = E.copy2d(torch.empty(Np, K, dtype=w.dtype, device=w.device), wc, K, Np, K, K, N, K)
+    bp = None
+    if b is not None:
+        bp = E.copy2d(torch.empty(Np, dtype=b.dtype, device=b.device), b.contiguous(), Np, 1, Np, N, 1, N)
+    try:
+        w._ddl_padn = (key, wp, bp)
+    except (AttributeError, RuntimeError):
+        pass
+    return wp, bp
 
 
 # dgrad as an NT GEMM against a cached W^T (DDL_DGRAD_NT=1) or as NN with W read through
@@ -205,7 +236,7 @@ class _Linear(torch.autograd.Function):
             else:
                 call("ddl_gelu_bwd", dcode(dy2), p(dy2), p(saved), p(dz), dz.numel())
         elif ctx.act == "tanh":
-            dz = (dy2.float() * (1 - saved.float() ** 2)).to(dy2.dtype)
+            dz = E.tanh_bwd(dy2, saved)
         elif ctx.act == "relu":
             dz = dy2 * (saved > 0)
         else:

@@ -444,7 +444,12 @@ class _LayerNorm(torch.autograd.Function):
                     ctx.bridge.put(dres)       # summed into the consuming Linear's dgrad epilogue
                     dres = None
             else:
-                dres = g.view(-1, ctx.res_rows, H).float().sum(0).to(dx.dtype).view(ctx.res_shape)
+                # broadcast residual ([1, S, H] against [B, S, H]): its gradient is the sum over the
+                # batch -- one native column-sum launch over [B, S * H] (fp32 partials, bf16 out)
+                from . import _native_elementwise as E
+                dres = torch.empty(ctx.res_rows * H, dtype=dx.dtype, device=dx.device)
+                E.colsum(g.reshape(-1, ctx.res_rows * H), dres)
+                dres = dres.view(ctx.res_shape)
         return dx, dg, db, None, dres, None, None, None
 
 

@@ -100,7 +100,12 @@ class ParamArena:
                 e.param.grad = view
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        from ..ops import _lib
+        if self.grad.is_cuda and _lib.mode() != "off" and _lib.available():
+            from ..ops import _native_elementwise as E
+            E.zero_(self.grad)          # the framework's own fill kernel (no ATen launch)
+        else:
+            self.grad.zero_()
 
     def param_views(self, flat: torch.Tensor) -> List[torch.Tensor]:
         return [flat[e.offset:e.offset + e.numel].view(e.shape) for e in self.entries]

@@ -61,6 +61,7 @@ class FlatOptimizer:
         self.weight_decay = weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
+        self._scale_cache = {}
         self.shard = None
         # ranges: (arena lo, arena hi, local offset); groups: (start, end) gathered per rank chunk
         self.ranges = [(0, arena.numel, 0)]
@@ -161,7 +162,11 @@ class FlatOptimizer:
             self.last_grad_norm = norm
             clip = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0)
             return clip * grad_scale
-        return torch.full((), grad_scale, dtype=torch.float32, device=grad.device)
+        key = (float(grad_scale), grad.device)
+        t = self._scale_cache.get(key)
+        if t is None:                      # one device scalar per (scale, device): no fill per step
+            t = self._scale_cache[key] = torch.full((), grad_scale, dtype=torch.float32, device=grad.device)
+        return t
 
     # ------------------------------------------------------------------ range steps
     # The data-parallel reducer can hand the optimizer one bucket (a contiguous range of

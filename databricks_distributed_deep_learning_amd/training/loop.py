@@ -194,7 +194,7 @@ class Trainer:
                     loss = self.loss_fn(batch)
                 ph.mark("fwd")
                 with profiling.range("bwd"):
-                    loss.backward()
+                    loss.backward(self._seed_grad(loss))
                 ph.mark("bwd")
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
         if self.eager_optimizer:
@@ -221,7 +221,15 @@ class Trainer:
             ph.mark("opt")
         ph.end_step()
         self.step += 1
-        return loss_sum / c.grad_accum
+        return loss_sum / c.grad_accum if c.grad_accum > 1 else loss_sum
+
+    def _seed_grad(self, loss: torch.Tensor) -> torch.Tensor:
+        """d(loss)/d(loss) = 1, one cached device scalar (``backward()`` would fill a new one per step)."""
+        key = (loss.dtype, loss.device)
+        g = self.__dict__.setdefault("_seed_grads", {}).get(key)
+        if g is None:
+            g = self._seed_grads[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+        return g
 
     def agree_kernel_plans(self, max_rounds: int = 3) -> None:
         """Data-parallel ranks run identical GEMM kernel plans (ops/_native_gemm.py

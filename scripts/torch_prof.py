@@ -27,3 +27,18 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stac
     torch.cuda.synchronize()
 print(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=40, max_name_column_width=60,
                                                    max_src_column_width=200))
+
+# where each ATen op that launched device work comes from (first frames inside this package)
+from collections import defaultdict  # noqa: E402
+
+agg = defaultdict(lambda: [0, 0.0])
+for ev in prof.events():
+    if not ev.name.startswith("aten::") or ev.device_time_total <= 0:
+        continue
+    frames = [f for f in (ev.stack or []) if "databricks_distributed" in f][:3]
+    key = (ev.name, " <- ".join(f.split("databricks_distributed_deep_learning_amd/")[-1] for f in frames))
+    agg[key][0] += 1
+    agg[key][1] += ev.device_time_total
+print("\n### ATen ops with device time, by call site (2 steps)")
+for (name, where), (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+    print(f"{us:9.1f} us {n:4d}x {name:28s} {where}")
