@@ -469,3 +469,63 @@ DDL_API int ddl_stem_wgrad(const void* xs, const void* dy, void* dw, int N, int 
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -2 - (int)e;
 }
+
+// ------------------------------------------------------------------ space-to-depth transforms
+// The stem's stride-2 conv runs as a stride-1 conv of the image's 2x2 space-to-depth transform
+// (ops/_native_conv.py _StemConvS2D).  These build the transformed input / weight in ONE pass each
+// (ATen took a pad + a permuted copy for each: four launches and two full-size intermediates).
+namespace {
+// xs[n][i][j][(dy * 2 + dx) * 4 + c] = x[n][2i + dy - pad][2j + dx - pad][c] (0 outside, c >= C);
+// one thread per output pixel: 4 input pixels of C <= 4 channels -> 32 bytes, two 16-byte stores
+__global__ __launch_bounds__(256) void s2d_input_k(const bf16_t* __restrict__ x, int N, int H, int W, int C, int pad,
+                                                   bf16_t* __restrict__ xs, int Hs, int Ws) {
+    const long total = (long)N * Hs * Ws;
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        const int j = (int)(t % Ws);
+        const long r = t / Ws;
+        const int i = (int)(r % Hs), n = (int)(r / Hs);
+        uint16_t v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int h = 2 * i + (q >> 1) - pad, w = 2 * j + (q & 1) - pad;
+            const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+            const bf16_t* src = x + (((long)n * H + (in ? h : 0)) * W + (in ? w : 0)) * C;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[q * 4 + c] = (in && c < C) ? src[c] : (uint16_t)0;
+        }
+        uint4* dst = reinterpret_cast<uint4*>(xs + t * 16);
+        dst[0] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
+        dst[1] = make_uint4(v[8] | (v[9] << 16), v[10] | (v[11] << 16), v[12] | (v[13] << 16), v[14] | (v[15] << 16));
+    }
+}
+
+// ws[k][r2][s2][(dy * 2 + dx) * 4 + c] = w[k][2 r2 + dy][2 s2 + dx][c] (0 past R / S / C)
+__global__ __launch_bounds__(256) void s2d_weight_k(const bf16_t* __restrict__ w, int K, int R, int S, int C,
+                                                    bf16_t* __restrict__ ws, int R2, int S2) {
+    const long total = (long)K * R2 * S2 * 16;
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        const int ch = (int)(t & 15), c = ch & 3, q = ch >> 2;
+        const long r = t >> 4;
+        const int s2 = (int)(r % S2), r2 = (int)((r / S2) % R2), k = (int)(r / ((long)S2 * R2));
+        const int rr = 2 * r2 + (q >> 1), ss = 2 * s2 + (q & 1);
+        ws[t] = (rr < R && ss < S && c < C) ? w[(((long)k * R + rr) * S + ss) * C + c] : (bf16_t)0;
+    }
+}
+}  // namespace
+
+DDL_API int ddl_s2d_input(const void* x, int N, int H, int W, int C, int pad, void* xs, int Hs, int Ws,
+                          hipStream_t st) {
+    if (C > 4 || C < 1 || 2 * Hs < H + 2 * pad || 2 * Ws < W + 2 * pad) return -1;
+    const long total = (long)N * Hs * Ws;
+    const int grid = (int)std::min<long>((total + 255) / 256, 8192);
+    s2d_input_k<<<grid, 256, 0, st>>>((const bf16_t*)x, N, H, W, C, pad, (bf16_t*)xs, Hs, Ws);
+    DDL_RETURN_LAUNCH();
+}
+
+DDL_API int ddl_s2d_weight(const void* w, int K, int R, int S, int C, void* ws, int R2, int S2, hipStream_t st) {
+    if (C > 4 || C < 1 || 2 * R2 < R || 2 * S2 < S) return -1;
+    const long total = (long)K * R2 * S2 * 16;
+    s2d_weight_k<<<(int)std::min<long>((total + 255) / 256, 4096), 256, 0, st>>>((const bf16_t*)w, K, R, S, C,
+                                                                                 (bf16_t*)ws, R2, S2);
+    DDL_RETURN_LAUNCH();
+}

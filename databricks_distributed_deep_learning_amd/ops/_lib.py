@@ -159,6 +159,8 @@ _SIGS = {
     "ddl_conv3x3_wgrad": [P, P, P, I, I, I, I, I, P, L, I, I, I, P],
     "ddl_stem_wgrad": [P, P, P, I, I, I, I, I, I, I, P, L, I, I, I, P],
     "ddl_stem_fwd": [P, P, P, I, I, I, I, P, I, P],
+    "ddl_s2d_input": [P, I, I, I, I, I, P, I, I, P],
+    "ddl_s2d_weight": [P, I, I, I, I, P, I, I, P],
     "ddl_skinny_gemm": [P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_stream_gemm": [P, P, P, L, I, I, P, P, P, P, P, P, I, P],
     "ddl_stream_wgrad_ws": [I, I],

@@ -532,6 +532,11 @@ def _s2d_input(x, pad):
     N, H, W_, C = x.shape
     Hp, Wp = H + 2 * pad, W_ + 2 * pad
     Hp2, Wp2 = Hp + Hp % 2, Wp + Wp % 2
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous():
+        # one native pass (csrc/kernels/stem_conv.hip ddl_s2d_input) instead of a pad + a permuted copy
+        xs = torch.empty(N, Hp2 // 2, Wp2 // 2, 16, dtype=x.dtype, device=x.device)
+        _lib.call("ddl_s2d_input", x.data_ptr(), N, H, W_, C, pad, xs.data_ptr(), Hp2 // 2, Wp2 // 2)
+        return xs
     xp = F.pad(x, (0, 4 - C, pad, pad + Wp2 - Wp, pad, pad + Hp2 - Hp))
     return xp.view(N, Hp2 // 2, 2, Wp2 // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, Hp2 // 2, Wp2 // 2, 16)
 
@@ -541,6 +546,10 @@ def _s2d_weight(w):
     the space-to-depth input (taps past R / S are zero)."""
     K, R, S, C = w.shape
     R2, S2 = (R + 1) // 2, (S + 1) // 2
+    if w.is_cuda and w.dtype == torch.bfloat16 and w.is_contiguous():
+        ws = torch.empty(K, R2, S2, 16, dtype=w.dtype, device=w.device)
+        _lib.call("ddl_s2d_weight", w.data_ptr(), K, R, S, C, ws.data_ptr(), R2, S2)
+        return ws
     wp = F.pad(w, (0, 4 - C, 0, 2 * S2 - S, 0, 2 * R2 - R))
     return wp.view(K, R2, 2, S2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(K, R2, S2, 16)
 

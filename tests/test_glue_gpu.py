@@ -131,3 +131,16 @@ def test_classifier_head_padded_linear_matches_reference():
         torch.testing.assert_close(b.grad.float(), dy.float().sum(0), rtol=2e-2, atol=0.1)
         with torch.no_grad():
             w.mul_(-1.5)                      # version bump: the padded copy must be rebuilt
+
+
+@pytest.mark.parametrize("H,W,C,pad", [(224, 224, 3, 3), (31, 29, 3, 3), (16, 16, 4, 1), (15, 17, 1, 2)])
+def test_stem_space_to_depth_transforms_native(H, W, C, pad):
+    """ddl_s2d_input / ddl_s2d_weight (one native pass each) == the pad + permute reference (the same
+    functions on CPU tensors), odd extents included."""
+    dev = gpu_device()
+    from databricks_distributed_deep_learning_amd.ops import _native_conv as NC
+    torch.manual_seed(H + W)
+    x = torch.randn(2, H, W, C).bfloat16()
+    w = torch.randn(64, 7, 7, C).bfloat16()
+    assert torch.equal(NC._s2d_input(x.to(dev), pad).cpu(), NC._s2d_input(x, pad))
+    assert torch.equal(NC._s2d_weight(w.to(dev)).cpu(), NC._s2d_weight(w))
