@@ -773,10 +773,20 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
         *reinterpret_cast<float4*>(&s_acc[2][w][256 * k + 4 * lane]) = make_float4(ds[k][0], ds[k][1], ds[k][2], ds[k][3]);
     }
     __syncthreads();
+    // column sums over the 4 wave rows: 4 consecutive columns per thread, ds_read_b128 (16 lanes x
+    // 16 B = one pass over all 64 banks: conflict free) and 16-byte global stores.  The scalar
+    // form (one column per thread, the four wave rows paired into ds_read2_b32) was 50 % bank-
+    // conflict cycles in the PMC pass (profiles/pmc_bert.md, round 5).
     const int nv = dxsum ? 3 : 2;
-    for (int c = threadIdx.x; c < H; c += 256) {
-        for (int v = 0; v < nv; ++v)
-            part[(long)blockIdx.x * nv * H + v * H + c] = s_acc[v][0][c] + s_acc[v][1][c] + s_acc[v][2][c] + s_acc[v][3][c];
+    for (int c = 4 * threadIdx.x; c < H; c += 1024) {
+        for (int v = 0; v < nv; ++v) {
+            const float4 a = *reinterpret_cast<const float4*>(&s_acc[v][0][c]);
+            const float4 b = *reinterpret_cast<const float4*>(&s_acc[v][1][c]);
+            const float4 e = *reinterpret_cast<const float4*>(&s_acc[v][2][c]);
+            const float4 f = *reinterpret_cast<const float4*>(&s_acc[v][3][c]);
+            *reinterpret_cast<float4*>(part + (long)blockIdx.x * nv * H + v * H + c) =
+                make_float4(a.x + b.x + e.x + f.x, a.y + b.y + e.y + f.y, a.z + b.z + e.z + f.z, a.w + b.w + e.w + f.w);
+        }
     }
 }
 

@@ -102,8 +102,10 @@ step() {
       rm -rf "gpurun_out/prof_$m"
       head -14 "gpurun_out/kernels_$m.md" ;;
     pmc)
+      # 3 steady-state steps after 2 warm-up steps; the summary counts only dispatches after the
+      # warm-up's last optimizer kernel (pmc_summary.py --after)
       local m=$1 cmd
-      cmd=$(run_model "$m" 2 1) || return 1
+      cmd=$(run_model "$m" 3 2) || return 1
       rm -rf "gpurun_out/pmc_$m"
       # tune once into a cache first: the counted runs load the GEMM kernel choices instead of
       # timing every candidate (whose dispatches would otherwise fill the table)
@@ -112,8 +114,8 @@ step() {
       timeout -k 10 300 $cmd > "gpurun_out/pmc_${m}_tune.log" 2>&1 || { tail -20 "gpurun_out/pmc_${m}_tune.log"; return 1; }
       bash scripts/pmc_profile.sh "gpurun_out/pmc_$m" -- $cmd || return 1
       unset DDL_GEMM_TUNE_CACHE
-      python3 scripts/pmc_summary.py "gpurun_out/pmc_$m" --top 30 --title "$m training step (1 warm-up + 2 steps)" \
-        > "gpurun_out/pmc_$m.md"
+      python3 scripts/pmc_summary.py "gpurun_out/pmc_$m" --top 30 --after "$(opt_kernel "$m"):2" \
+        --title "$m training step, steady state (3 steps counted after 2 warm-up steps)" > "gpurun_out/pmc_$m.md"
       rm -rf "gpurun_out/pmc_$m"
       head -14 "gpurun_out/pmc_$m.md" ;;
     presets)

@@ -33,14 +33,38 @@ def short(name: str) -> str:
     return name[:80]
 
 
-def load(d: str):
+def steady_ids(rows, after: str):
+    """Dispatch ids past the N-th dispatch of the kernel named in ``after`` ("name:N", e.g. the
+    optimizer kernel that ends each warm-up step): the warm-up steps' dispatches are dropped."""
+    if not after:
+        return None
+    name, _, n = after.rpartition(":")
+    order = {}
+    for row in rows:
+        did = int(row.get("Dispatch_Id") or 0)
+        order.setdefault(did, short(row.get("Kernel_Name", "?")))
+    seen = 0
+    for did in sorted(order):
+        if name in order[did]:
+            seen += 1
+            if seen == int(n):
+                return {d for d in order if d > did}
+    return set()
+
+
+def load(d: str, after: str = ""):
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = collections.defaultdict(lambda: collections.defaultdict(float))   # per pass file
     calls = collections.defaultdict(set)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         seen = set()
         with open(path) as f:
-            for row in csv.DictReader(f):
+            rows = list(csv.DictReader(f))
+        keep = steady_ids(rows, after)
+        if True:
+            for row in rows:
+                if keep is not None and int(row.get("Dispatch_Id") or 0) not in keep:
+                    continue
                 k = short(row.get("Kernel_Name", "?"))
                 vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
                 did = (path, row.get("Dispatch_Id"))
@@ -57,8 +81,10 @@ def main():
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--match", default="")
     ap.add_argument("--title", default="")
+    ap.add_argument("--after", default="", help="name:N -- count only dispatches after the N-th dispatch of "
+                                                "kernel `name` (drop the warm-up steps)")
     a = ap.parse_args()
-    vals, dur, calls = load(a.dir)
+    vals, dur, calls = load(a.dir, a.after)
     names = [k for k in vals if a.match in k]
     tot_t = {k: max(dur[k].values()) if dur[k] else 0.0 for k in names}
     names.sort(key=lambda k: -tot_t[k])
