@@ -414,7 +414,16 @@ def _dgrad(dy, w, x_shape, stride, pad, residual=None, bnb=None, param=None):
         key = (tuple(dy.shape), tuple(w.shape), stride, pad)
         choice = _MULTI_CHOICE.get(key)
         if choice is None:
-            choice = _pick_dgrad_path(key, serial, multi, dx)
+            # part of the reproducible kernel plan: the committed table (ops/gemm_plans.json) holds it
+            # under "dgrad_path|..."; only a miss is timed here (and recorded for the next table)
+            from . import _native_gemm as NG
+            skey = "dgrad_path|" + "|".join(str(v) for v in key)
+            planned = NG.lookup_choice(skey)
+            if planned is not None and planned[0] in ("serial", "multi", "multi_narrow"):
+                choice = _MULTI_CHOICE[key] = planned[0]
+            else:
+                choice = _pick_dgrad_path(key, serial, multi, dx)
+                NG.record_choice(skey, (choice, 1))
         if choice == "serial":
             serial(dx)
         else:

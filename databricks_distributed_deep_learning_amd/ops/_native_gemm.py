@@ -471,6 +471,24 @@ def plan_usage():
         _used = prev
 
 
+def lookup_choice(key: str):
+    """A non-GEMM kernel choice (e.g. the strided-conv dgrad path) from this process's tuning / the tune
+    cache, else from the committed plan table; None = not planned (the caller tunes and records it)."""
+    if _used is not None:
+        _used.add(key)
+    v = _tuned.get(key)
+    if v is None:
+        v = load_plan_table().get(key)
+        (_table_hits if v is not None else _table_misses).add(key)
+    return v
+
+
+def record_choice(key: str, value) -> None:
+    """Remember a choice tuned in this process (and in DDL_GEMM_TUNE_CACHE, so tuning runs feed the table)."""
+    _tuned[key] = tuple(value)
+    _save_cache()
+
+
 def current_plan(keys) -> dict:
     """(kernel, splits) of each signature in ``keys`` as this process runs it."""
     tab = load_plan_table()

@@ -32,6 +32,7 @@ def main() -> int:
     ap.add_argument("--arch", default="gfx950")
     ap.add_argument("--replace", action="store_true", help="drop the architecture's old entries first")
     ap.add_argument("--table", default=TABLE)
+    ap.add_argument("--only-new", action="store_true", help="add signatures the table lacks; keep existing entries")
     a = ap.parse_args()
     import build as native_build     # csrc/build.py: the same hash the library embeds
     src = native_build.gemm_src_hash()
@@ -51,6 +52,8 @@ def main() -> int:
     for path in a.caches:
         with open(path) as f:
             for k, v in json.load(f).items():
+                if a.only_new and k in plans:
+                    continue
                 plans[k] = [str(v[0]), int(v[1])]
     doc[a.arch] = {"gemm_src_hash": src, "plans": dict(sorted(plans.items()))}
     with open(a.table + ".tmp", "w") as f:      # one line per signature (reviewable diffs)
