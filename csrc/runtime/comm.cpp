@@ -79,6 +79,7 @@ struct Rccl {
     decltype(&ncclGroupEnd) groupEnd = nullptr;
     decltype(&ncclGetErrorString) errorString = nullptr;
     decltype(&ncclCommGetAsyncError) getAsyncError = nullptr;   // optional
+    decltype(&ncclCommFinalize) commFinalize = nullptr;         // optional (non-blocking teardown)
 };
 
 Rccl g_rccl;
@@ -114,7 +115,9 @@ bool load_rccl(const char* path) {
            (g_rccl.getAsyncError = reinterpret_cast<decltype(&ncclCommGetAsyncError)>(
                 dlsym(g_rccl.so, "ncclCommGetAsyncError")), true) &&
            (g_rccl.commInitRankConfig = reinterpret_cast<decltype(&ncclCommInitRankConfig)>(
-                dlsym(g_rccl.so, "ncclCommInitRankConfig")), true);
+                dlsym(g_rccl.so, "ncclCommInitRankConfig")), true) &&
+           (g_rccl.commFinalize = reinterpret_cast<decltype(&ncclCommFinalize)>(
+                dlsym(g_rccl.so, "ncclCommFinalize")), true);
 }
 
 bool ok(ncclResult_t r, const char* what) {
@@ -296,7 +299,7 @@ DDL_API void* ddl_comm_create(const char* rccl_path, const char* id_bytes, int w
     std::memcpy(id.internal, id_bytes, NCCL_UNIQUE_ID_BYTES);
     ncclComm_t c = nullptr;
     const char* nb = getenv("DDL_COMM_NONBLOCKING");
-    e->nonblocking = g_rccl.commInitRankConfig && g_rccl.getAsyncError && !(nb && nb[0] == '0');
+    e->nonblocking = g_rccl.commInitRankConfig && g_rccl.getAsyncError && g_rccl.commFinalize && !(nb && nb[0] == '0');
     bool good;
     if (e->nonblocking) {
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -607,10 +610,16 @@ DDL_API void ddl_comm_destroy(void* h, int abort) {
         if (c) {
             while (e->inflight.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
             hipStreamSynchronize(e->stream);
-            ncclResult_t r = g_rccl.commDestroy(c);
-            // non-blocking: the destroy may finish asynchronously (c stays valid until it reports)
-            while (e->nonblocking && r == ncclInProgress && g_rccl.getAsyncError(c, &r) == ncclSuccess)
-                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            if (e->nonblocking) {
+                // non-blocking teardown: finalize (flushes outstanding work; may answer ncclInProgress,
+                // polled while the communicator is still alive), THEN destroy, after which c is gone
+                ncclResult_t r = g_rccl.commFinalize(c);
+                while (r == ncclInProgress) {
+                    std::this_thread::sleep_for(std::chrono::microseconds(200));
+                    if (g_rccl.getAsyncError(c, &r) != ncclSuccess) break;
+                }
+            }
+            g_rccl.commDestroy(c);
         }
     }
     for (int i = 0; i < RING; ++i) {
