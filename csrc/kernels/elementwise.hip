@@ -1077,33 +1077,82 @@ __global__ void zero_bytes_k(unsigned char* __restrict__ p, long n) {
 }
 
 // Stable sort of n <= 32768 token ids in ONE workgroup: key = id * n + position (unique, ordered by
-// (id, position): any sort of these keys is the stable sort of the ids), a bitonic network over the
-// keys in LDS (padded to a power of two with ~0u), then s = key / n, pi = key % n.  One launch
-// instead of rocPRIM's block sort + merge passes + ATen's index fill and int32 cast.
-__global__ __launch_bounds__(1024) void sort_ids_k(const int64_t* __restrict__ ids, int n, int npow2,
-                                                   int* __restrict__ s, int64_t* __restrict__ pi) {
+// (id, position): any sort of these keys is the stable sort of the ids), a bitonic network over
+// N = 1024 R keys (padded with ~0u), then s = key / n, pi = key % n.  One launch instead of rocPRIM's
+// block sort + merge passes + ATen's index fill and int32 cast.
+// Thread t holds keys t R .. t R + R - 1 in registers, so a compare-exchange at distance j runs
+//   j < R:        inside the thread (register pairs, no communication);
+//   R <= j < 64R: against lane t ^ (j / R) of the same wave (__shfl_xor, no barrier);
+//   j >= 64R:     through LDS (one store + one barrier + one partner read + one barrier), the image
+//                 XOR-swizzled by 32-key block so the R-strided stores and partner reads of a wave
+//                 hit 32 distinct banks.
+// The first version ran every one of the log2(N) (log2(N) + 1) / 2 stages through LDS with a
+// barrier each (105 stages at N = 16384): 125 us per BERT-base step (profiles/kernels_bert.md).
+__device__ __forceinline__ int sort_swz(int e) { return e ^ ((e >> 5) & 31); }
+
+template <int R, int J>
+__device__ __forceinline__ void sort_reg_stage(uint32_t (&v)[R], int tid, int k) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r & J) continue;
+        const bool asc = ((tid * R + r) & k) == 0;
+        const uint32_t a = v[r], b = v[r | J];
+        v[r] = asc ? min(a, b) : max(a, b);
+        v[r | J] = asc ? max(a, b) : min(a, b);
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void sort_ids_k(const int64_t* __restrict__ ids, int n, int* __restrict__ s,
+                                                   int64_t* __restrict__ pi) {
     extern __shared__ uint32_t keys[];
+    constexpr int N = 1024 * R;
     const int tid = threadIdx.x;
-    for (int i = tid; i < npow2; i += 1024) keys[i] = i < n ? (uint32_t)ids[i] * (uint32_t)n + (uint32_t)i : ~0u;
-    __syncthreads();
-    const int half = npow2 >> 1;
-    for (int k = 2; k <= npow2; k <<= 1) {
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = tid * R + r;
+        v[r] = e < n ? (uint32_t)ids[e] * (uint32_t)n + (uint32_t)e : ~0u;
+    }
+    for (int k = 2; k <= N; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < half; i += 1024) {
-                const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
-                const uint32_t a = keys[lo], b = keys[hi];
-                if ((a > b) == ((lo & k) == 0)) {
-                    keys[lo] = b;
-                    keys[hi] = a;
+            if (j >= 64 * R) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) keys[sort_swz(tid * R + r)] = v[r];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int e = tid * R + r;
+                    const uint32_t b = keys[sort_swz(e ^ j)];
+                    const bool asc = (e & k) == 0, lower = (e & j) == 0;
+                    v[r] = lower == asc ? min(v[r], b) : max(v[r], b);
                 }
+                __syncthreads();
+            } else if (j >= R) {
+                const int tj = j / R;
+                const bool lower = (tid & tj) == 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t b = (uint32_t)__shfl_xor((int)v[r], tj, 64);
+                    const bool asc = ((tid * R + r) & k) == 0;
+                    v[r] = lower == asc ? min(v[r], b) : max(v[r], b);
+                }
+            } else {
+                if constexpr (R > 16) { if (j == 16) sort_reg_stage<R, 16 % R>(v, tid, k); }
+                if constexpr (R > 8) { if (j == 8) sort_reg_stage<R, 8 % R>(v, tid, k); }
+                if constexpr (R > 4) { if (j == 4) sort_reg_stage<R, 4 % R>(v, tid, k); }
+                if constexpr (R > 2) { if (j == 2) sort_reg_stage<R, 2 % R>(v, tid, k); }
+                if constexpr (R > 1) { if (j == 1) sort_reg_stage<R, 1>(v, tid, k); }
             }
-            __syncthreads();
         }
     }
-    for (int i = tid; i < n; i += 1024) {
-        const uint32_t kk = keys[i];
-        s[i] = (int)(kk / (uint32_t)n);
-        pi[i] = (int64_t)(kk % (uint32_t)n);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = tid * R + r;
+        if (e < n) {
+            s[e] = (int)(v[r] / (uint32_t)n);
+            pi[e] = (int64_t)(v[r] % (uint32_t)n);
+        }
     }
 }
 
@@ -1178,14 +1227,22 @@ DDL_API int ddl_sort_ids_ok(long n, long vocab) {
     return n > 0 && n <= 32768 && (unsigned long long)vocab * (unsigned long long)n < (1ull << 32) ? 1 : 0;
 }
 
+template <int R>
+static int sort_ids_launch(const int64_t* ids, long n, int* s, int64_t* pi, hipStream_t st) {
+    static const bool big_lds = R <= 8 || hipFuncSetAttribute((const void*)sort_ids_k<R>,
+                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                              1024 * R * 4) == hipSuccess;
+    if (!big_lds) return -1;
+    sort_ids_k<R><<<1, 1024, (size_t)1024 * R * 4, st>>>(ids, (int)n, s, pi);
+    DDL_RETURN_LAUNCH();
+}
+
 DDL_API int ddl_sort_ids(const int64_t* ids, long n, int* s, int64_t* pi, hipStream_t st) {
     if (n <= 0 || n > 32768) return -1;
-    int npow2 = 1;
-    while (npow2 < n) npow2 <<= 1;
-    if (npow2 < 2) npow2 = 2;
-    static const bool big_lds = hipFuncSetAttribute((const void*)sort_ids_k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    32768 * 4) == hipSuccess;
-    if (npow2 > 16384 && !big_lds) return -1;
-    sort_ids_k<<<1, 1024, (size_t)npow2 * 4, st>>>(ids, (int)n, npow2, s, pi);
-    DDL_RETURN_LAUNCH();
+    if (n <= 1024) return sort_ids_launch<1>(ids, n, s, pi, st);
+    if (n <= 2048) return sort_ids_launch<2>(ids, n, s, pi, st);
+    if (n <= 4096) return sort_ids_launch<4>(ids, n, s, pi, st);
+    if (n <= 8192) return sort_ids_launch<8>(ids, n, s, pi, st);
+    if (n <= 16384) return sort_ids_launch<16>(ids, n, s, pi, st);
+    return sort_ids_launch<32>(ids, n, s, pi, st);
 }

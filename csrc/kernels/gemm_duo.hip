@@ -342,11 +342,16 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
                 rb[i][j] = __builtin_amdgcn_raw_buffer_load_b64(
                     prs, (int)(((long)(mw + i * 16 + r16) * p.ldc + nw + j * 16 + g4) * 2), 0, 0);
     }
-    // tile image: row r (0..255), 16-byte chunk c (0..15) at r * 256 + ((c ^ (r & 15)) << 4)
+    // tile image: row r (0..255) of 256 B, its 8-byte unit u (0..31) at r * 256 + ((u ^ (r & 15)) << 3).
+    // An 8-byte swizzle, not a 16-byte one: a ds_write_b64 lane group is 16 lanes = 16 rows of ONE
+    // 8-byte unit, banked over 128 B, so the 16 rows must land on 16 distinct 8-byte slots (the 16-byte
+    // chunk swizzle gave 8: a 2-way conflict on every epilogue store, the 14-16 % LDS conflict rate of
+    // the short-K NT kernels in profiles/pmc_bert.md / pmc_r50.md).  A 16-byte chunk c of row r then
+    // sits whole at chunk c ^ ((r >> 1) & 7), its halves swapped when r is odd (store_image swaps back).
     const int wr0 = wm * 128 + r16;                    // this lane's image row for i = 0
     auto img_off = [&](int i, int j) {
-        const int c = wn * 8 + j * 2 + (l >> 5);
-        return (wr0 + i * 16) * 256 + ((c ^ r16) << 4) + ((l >> 4) & 1) * 8;
+        const int u = (wn * 8 + j * 2 + (l >> 5)) * 2 + ((l >> 4) & 1);
+        return (wr0 + i * 16) * 256 + ((u ^ r16) << 3);
     };
     // every wave's last fragment reads of the ring are done (each waited lgkmcnt before its MFMAs)
     BARRIER();
@@ -455,10 +460,12 @@ __global__ __launch_bounds__(NTH, 2) void gemm_duo_k(DuoParams p) {
         BARRIER();
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)bytes, 0x00020000);
         const int c = l & 15;
+        const bool odd = (l >> 4) & 1;                 // r & 1 for every it
 #pragma unroll
         for (int it = 0; it < 16; ++it) {
             const int r = w * 64 + it * 4 + (l >> 4);
-            u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+            u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * 256 + ((c ^ ((r >> 1) & 7)) << 4));
+            if (odd) v = u32x4{v[2], v[3], v[0], v[1]};
             const int off = (int)(((long)(m0 + r) * ld + n0 + c * 8) * 2);
             if (acc_c) {   // C += result (weight gradients into their arena slot), summed in fp32
                 const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);

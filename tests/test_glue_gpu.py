@@ -8,7 +8,7 @@ from conftest import gpu_device
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [1, 7, 4096, 16384, 16385, 32768])
+@pytest.mark.parametrize("n", [1, 7, 1000, 2048, 4096, 8192, 16384, 16385, 32768])
 def test_sort_ids_is_the_stable_sort(n):
     """The one-workgroup bitonic sort of (id, position) keys == torch's stable sort (ids and the
     permutation), with long runs of one id (padding) and two-valued ids (token types)."""
