@@ -1076,18 +1076,23 @@ __global__ void zero_bytes_k(unsigned char* __restrict__ p, long n) {
     if (i < n) p[i] = 0;
 }
 
-// Stable sort of n <= 32768 token ids in ONE workgroup: key = id * n + position (unique, ordered by
-// (id, position): any sort of these keys is the stable sort of the ids), a bitonic network over
-// N = 1024 R keys (padded with ~0u), then s = key / n, pi = key % n.  One launch instead of rocPRIM's
+// Stable sort of n <= 32768 token ids: key = id * n + position (unique, ordered by (id, position): any
+// sort of these keys is the stable sort of the ids), then s = key / n, pi = key % n.  Replaces rocPRIM's
 // block sort + merge passes + ATen's index fill and int32 cast.
-// Thread t holds keys t R .. t R + R - 1 in registers, so a compare-exchange at distance j runs
-//   j < R:        inside the thread (register pairs, no communication);
-//   R <= j < 64R: against lane t ^ (j / R) of the same wave (__shfl_xor, no barrier);
-//   j >= 64R:     through LDS (one store + one barrier + one partner read + one barrier), the image
-//                 XOR-swizzled by 32-key block so the R-strided stores and partner reads of a wave
-//                 hit 32 distinct banks.
-// The first version ran every one of the log2(N) (log2(N) + 1) / 2 stages through LDS with a
-// barrier each (105 stages at N = 16384): 125 us per BERT-base step (profiles/kernels_bert.md).
+//   1. sort_chunk_k: one workgroup per 2048-key chunk (one chunk: the whole job, results written
+//      directly), a bitonic network with thread t holding keys t R .. t R + R - 1 in registers, so a
+//      compare-exchange at distance j runs
+//        j < R:        inside the thread (register pairs);
+//        R <= j < 64R: against lane t ^ (j / R) of the same wave (__shfl_xor, no barrier);
+//        j >= 64R:     through LDS (store, barrier, partner read, barrier), the image XOR-swizzled by
+//                      32-key block so R-strided stores and partner reads hit 32 distinct banks;
+//   2. sort_merge_k: one workgroup merges the sorted chunks in LDS (log2(chunks) merge-path levels:
+//      each thread binary-searches its diagonal, then merges E = N / 1024 keys into registers).
+// A bitonic network is VALU-bound on ONE CU (~9,400 instructions per wave at N = 16384 in registers;
+// 81 us), and the first version -- every one of its 105 stages through LDS with a barrier -- took
+// 125 us per BERT-base step (profiles/kernels_bert.md); chunks spread the network over 8-16 CUs and
+// the merge levels cost ~log2(N) + E steps per thread.
+constexpr int SORT_CHUNK = 2048;
 __device__ __forceinline__ int sort_swz(int e) { return e ^ ((e >> 5) & 31); }
 
 template <int R, int J>
@@ -1102,18 +1107,25 @@ __device__ __forceinline__ void sort_reg_stage(uint32_t (&v)[R], int tid, int k)
     }
 }
 
+// tmp == null: the one chunk is the whole job (s / pi written); else the sorted keys of chunk
+// blockIdx.x go to tmp[blockIdx.x * 1024 R ..]
 template <int R>
-__global__ __launch_bounds__(1024) void sort_ids_k(const int64_t* __restrict__ ids, int n, int* __restrict__ s,
-                                                   int64_t* __restrict__ pi) {
+__global__ __launch_bounds__(1024) void sort_chunk_k(const int64_t* __restrict__ ids, int n, int* __restrict__ s,
+                                                     int64_t* __restrict__ pi, uint32_t* __restrict__ tmp) {
     extern __shared__ uint32_t keys[];
     constexpr int N = 1024 * R;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, base = blockIdx.x * N;
+    // keys in and results out through the LDS image, so the global loads and stores are coalesced
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int e = base + q * 1024 + tid;
+        keys[sort_swz(q * 1024 + tid)] = e < n ? (uint32_t)ids[e] * (uint32_t)n + (uint32_t)e : ~0u;
+    }
+    __syncthreads();
     uint32_t v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = tid * R + r;
-        v[r] = e < n ? (uint32_t)ids[e] * (uint32_t)n + (uint32_t)e : ~0u;
-    }
+    for (int r = 0; r < R; ++r) v[r] = keys[sort_swz(tid * R + r)];
+    __syncthreads();
     for (int k = 2; k <= N; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             if (j >= 64 * R) {
@@ -1138,20 +1150,75 @@ __global__ __launch_bounds__(1024) void sort_ids_k(const int64_t* __restrict__ i
                     v[r] = lower == asc ? min(v[r], b) : max(v[r], b);
                 }
             } else {
-                if constexpr (R > 16) { if (j == 16) sort_reg_stage<R, 16 % R>(v, tid, k); }
-                if constexpr (R > 8) { if (j == 8) sort_reg_stage<R, 8 % R>(v, tid, k); }
-                if constexpr (R > 4) { if (j == 4) sort_reg_stage<R, 4 % R>(v, tid, k); }
-                if constexpr (R > 2) { if (j == 2) sort_reg_stage<R, 2 % R>(v, tid, k); }
                 if constexpr (R > 1) { if (j == 1) sort_reg_stage<R, 1>(v, tid, k); }
             }
         }
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int e = tid * R + r;
+    for (int r = 0; r < R; ++r) keys[sort_swz(tid * R + r)] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int e = q * 1024 + tid;
+        const uint32_t kk = keys[sort_swz(e)];
+        if (tmp) {
+            tmp[base + e] = kk;
+        } else if (e < n) {
+            s[e] = (int)(kk / (uint32_t)n);
+            pi[e] = (int64_t)(kk % (uint32_t)n);
+        }
+    }
+}
+
+// merge nc sorted chunks of SORT_CHUNK keys (tmp) into the sorted whole: N = 1024 E keys in LDS
+// (chunks past nc read as ~0u), merge-path levels of run length L = SORT_CHUNK .. N / 2.  tmp may
+// alias pi: every key is read into LDS before the first output is written.
+template <int E>
+__global__ __launch_bounds__(1024) void sort_merge_k(const uint32_t* __restrict__ tmp, int nc, int n,
+                                                     int* __restrict__ s, int64_t* __restrict__ pi) {
+    extern __shared__ uint32_t keys[];
+    constexpr int N = 1024 * E;
+    const int tid = threadIdx.x;
+    const int nk = nc * SORT_CHUNK;
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+        const int e = q * 1024 + tid;
+        keys[sort_swz(e)] = e < nk ? tmp[e] : ~0u;
+    }
+    __syncthreads();
+    const int o0 = tid * E;
+    for (int L = SORT_CHUNK; L < N; L <<= 1) {
+        const int blk = o0 & ~(2 * L - 1), d = o0 - blk;
+        const int A = blk, B = blk + L;
+        // diagonal d: i keys of run A and d - i of run B come first
+        int lo = max(0, d - L), hi = min(d, L);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (keys[sort_swz(A + mid)] < keys[sort_swz(B + d - 1 - mid)]) lo = mid + 1;
+            else hi = mid;
+        }
+        int i = lo, j = d - lo;
+        uint32_t out[E];
+        uint32_t a = i < L ? keys[sort_swz(A + i)] : ~0u, b = j < L ? keys[sort_swz(B + j)] : ~0u;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const bool takeA = j >= L || (i < L && a <= b);
+            out[e] = takeA ? a : b;
+            if (takeA) { ++i; a = i < L ? keys[sort_swz(A + i)] : ~0u; }
+            else { ++j; b = j < L ? keys[sort_swz(B + j)] : ~0u; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) keys[sort_swz(o0 + e)] = out[e];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+        const int e = q * 1024 + tid;
         if (e < n) {
-            s[e] = (int)(v[r] / (uint32_t)n);
-            pi[e] = (int64_t)(v[r] % (uint32_t)n);
+            const uint32_t kk = keys[sort_swz(e)];
+            s[e] = (int)(kk / (uint32_t)n);
+            pi[e] = (int64_t)(kk % (uint32_t)n);
         }
     }
 }
@@ -1227,22 +1294,34 @@ DDL_API int ddl_sort_ids_ok(long n, long vocab) {
     return n > 0 && n <= 32768 && (unsigned long long)vocab * (unsigned long long)n < (1ull << 32) ? 1 : 0;
 }
 
-template <int R>
-static int sort_ids_launch(const int64_t* ids, long n, int* s, int64_t* pi, hipStream_t st) {
-    static const bool big_lds = R <= 8 || hipFuncSetAttribute((const void*)sort_ids_k<R>,
-                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                              1024 * R * 4) == hipSuccess;
-    if (!big_lds) return -1;
-    sort_ids_k<R><<<1, 1024, (size_t)1024 * R * 4, st>>>(ids, (int)n, s, pi);
+static bool sort_lds_ok(const void* k, int bytes) {
+    return bytes <= 65536 || hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess;
+}
+
+template <int E>
+static int sort_merge_launch(const int64_t* ids, long n, int* s, int64_t* pi, hipStream_t st) {
+    static const bool ok = sort_lds_ok((const void*)sort_merge_k<E>, 1024 * E * 4);
+    if (!ok) return -1;
+    const int nc = (int)((n + SORT_CHUNK - 1) / SORT_CHUNK);
+    // the sorted chunks (nc x 2048 keys, <= 8 n bytes for nc >= 2) live in pi's storage until merged
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(pi);
+    sort_chunk_k<SORT_CHUNK / 1024><<<nc, 1024, SORT_CHUNK * 4, st>>>(ids, (int)n, s, pi, tmp);
+    sort_merge_k<E><<<1, 1024, (size_t)1024 * E * 4, st>>>(tmp, nc, (int)n, s, pi);
     DDL_RETURN_LAUNCH();
 }
 
 DDL_API int ddl_sort_ids(const int64_t* ids, long n, int* s, int64_t* pi, hipStream_t st) {
     if (n <= 0 || n > 32768) return -1;
-    if (n <= 1024) return sort_ids_launch<1>(ids, n, s, pi, st);
-    if (n <= 2048) return sort_ids_launch<2>(ids, n, s, pi, st);
-    if (n <= 4096) return sort_ids_launch<4>(ids, n, s, pi, st);
-    if (n <= 8192) return sort_ids_launch<8>(ids, n, s, pi, st);
-    if (n <= 16384) return sort_ids_launch<16>(ids, n, s, pi, st);
-    return sort_ids_launch<32>(ids, n, s, pi, st);
+    if (n <= 1024) {
+        sort_chunk_k<1><<<1, 1024, 1024 * 4, st>>>(ids, (int)n, s, pi, nullptr);
+        DDL_RETURN_LAUNCH();
+    }
+    if (n <= 2048) {
+        sort_chunk_k<2><<<1, 1024, 2048 * 4, st>>>(ids, (int)n, s, pi, nullptr);
+        DDL_RETURN_LAUNCH();
+    }
+    if (n <= 4096) return sort_merge_launch<4>(ids, n, s, pi, st);
+    if (n <= 8192) return sort_merge_launch<8>(ids, n, s, pi, st);
+    if (n <= 16384) return sort_merge_launch<16>(ids, n, s, pi, st);
+    return sort_merge_launch<32>(ids, n, s, pi, st);
 }
