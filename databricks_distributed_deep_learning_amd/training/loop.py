@@ -16,6 +16,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import sys
 import time
 from typing import Any, Callable, Dict, Optional
 
@@ -90,8 +91,13 @@ class Trainer:
         self.eager_optimizer = (cfg.overlap_optimizer and cfg.eager_optimizer and self.opt.supports_ranges()
                                 and os.environ.get("DDL_EAGER_OPTIMIZER", "1") != "0"
                                 and self.ddp.reduce_dtype == self.arena.dtype and self.arena.grad.is_cuda)
+        self.auto_batch = None
         if cfg.batch_size <= 0:
             cfg.batch_size = self._auto_batch()
+            from ..utils.memory import last_fit
+            self.auto_batch = dict(last_fit)
+            if ddist.is_main():
+                print(f"[auto-batch] per-rank batch {cfg.batch_size}: {self.auto_batch}", file=sys.stderr, flush=True)
         self.loader = self._make_loader()
         self.step = 0
         self.logger = JsonlLogger(cfg.log_file, enabled=ddist.is_main())
@@ -197,6 +203,11 @@ class Trainer:
                     loss.backward(self._seed_grad(loss))
                 ph.mark("bwd")
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+            # drop this micro-step's graph now: the native autograd Functions keep operands on ctx
+            # attributes, which live as long as the graph does -- held through the NEXT micro-step's
+            # forward they cost BERT-large (batch 128 x seq 512) 11.4 GB over the fitter's one-micro-step
+            # probe, and the fitted batch went out of memory (scripts/debug/autobatch_mem.py --compare)
+            del loss
         if self.eager_optimizer:
             with profiling.range("comm_wait+opt"):
                 self.ddp.finish()               # joins the side stream (or runs the remaining updates)
@@ -350,6 +361,8 @@ class Trainer:
             "comm": self.ddp.comm, "phases_ms": {k: round(v, 3) for k, v in phases.items()},
             "bucket_policy": self.bucket_policy,
         }
+        if self.auto_batch:
+            summary["auto_batch"] = self.auto_batch
         if self.comm_probe:
             summary["comm_probe"] = self.comm_probe
         if self.rehearsal:

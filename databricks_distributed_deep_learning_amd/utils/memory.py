@@ -7,9 +7,12 @@ sized for one MI355X's 288 GB.
 """
 from __future__ import annotations
 
-from typing import Callable
+from typing import Any, Callable, Dict
 
 import torch
+
+# the last fit's decisions (reported in the training summary as ``auto_batch``)
+last_fit: Dict[str, Any] = {}
 
 
 def fit_batch_size(step_fn: Callable[[int], None], device: torch.device, start: int = 8,
@@ -25,8 +28,12 @@ def fit_batch_size(step_fn: Callable[[int], None], device: torch.device, start: 
         base = torch.cuda.memory_allocated(device)
         step_fn(b)
         torch.cuda.synchronize(device)
-        return torch.cuda.max_memory_allocated(device) - base
+        peak = torch.cuda.max_memory_allocated(device) - base
+        last_fit["probes"].append([b, round(peak / 2**30, 2)])
+        return peak
 
+    last_fit.clear()
+    last_fit.update(budget_gb=round(budget / 2**30, 2), probes=[])
     b0 = start
     while True:
         try:
@@ -38,6 +45,7 @@ def fit_batch_size(step_fn: Callable[[int], None], device: torch.device, start: 
                 raise
     static = torch.cuda.memory_allocated(device)
     per_sample = p0 / b0
+    last_fit.update(static_gb=round(static / 2**30, 2), gb_per_sample=round(per_sample / 2**30, 4))
     est = int((budget - static) / max(per_sample, 1.0))
     est = max(b0, min(max_batch, est // multiple * multiple))
     # the candidate must FIT THE BUDGET, not merely run: a probe that squeezed into the last few GB
@@ -49,8 +57,11 @@ def fit_batch_size(step_fn: Callable[[int], None], device: torch.device, start: 
             p = peak_at(est)
         except torch.cuda.OutOfMemoryError:
             est = max(b0, int(est * 0.8) // multiple * multiple)
+            last_fit["probes"].append([est, "oom"])
             continue
         if static + p <= budget:
+            last_fit["batch"] = est
             return est
         est = max(b0, min(est - multiple, int(est * (budget - static) / p)) // multiple * multiple)
+    last_fit["batch"] = b0
     return b0
