@@ -10,8 +10,9 @@ plus a summary with the weak-scaling efficiency of each N against N=1:
 
     efficiency(N) = value(N) / (N * value(1))     (per-GPU batch fixed: weak scaling)
 
-Each run is a fresh set of processes, so every N pays its own GEMM tuning in its
-warm-up steps and nothing from a previous N is cached.  ``--backend gloo`` with
+Each run is a fresh set of processes: every N loads the committed GEMM plan table
+(ops/gemm_plans.json; tuning only for a signature the table misses) and nothing from a
+previous N is cached.  ``--backend gloo`` with
 ``--max-visible`` rehearses the sweep on the CPU
 (tests/test_launch_cpu.py::test_bench_self_launch_and_scaling_sweep).
 """
