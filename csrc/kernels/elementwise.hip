@@ -307,12 +307,25 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_k(const T* __restrict__ x
 // Row forms of the two kernels above and below for the ResNet stem: one block per output (input) row,
 // 32-bit index math.  The flat forms decompose a 64-bit element index per thread with 64-bit div /
 // mod (software sequences) and ran at ~2.3-2.5 TB/s on the 411 MB stem activation.
+// Workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b & 7), each with its own L2.
+// This bijection of [0, n) gives XCD x a CONTIGUOUS range of logical block ids, so neighbouring blocks
+// that share input rows (pooling windows) share them in one L2 instead of fetching them twice.
+__device__ __forceinline__ int xcd_contiguous(int bid, int n) {
+    const int xcd = bid & 7, qn = n >> 3, rn = n & 7;
+    return (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (bid >> 3);
+}
+
+// Rows in XCD-contiguous order (xcd_contiguous): output rows p and p + 1 share input row 2p + 1, and
+// round-robin placement put them on different XCDs, i.e. two L2s fetching it (stem shape, batch 256:
+// forward 234 -> 225 us, backward 206 -> 193 us; blocks sized to one pass per row, 448 / 896 threads,
+// were slower: 237 / 265 us -- profiles/pool_ab_r06.log).
 template <typename T>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_rows_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                               const float* __restrict__ shift, T* __restrict__ y,
                                                               uint8_t* __restrict__ idx, uint8_t* __restrict__ mask,
                                                               int H, int W, int C, int P, int Q) {
-    const int c8 = C / 8, n = blockIdx.x / P, p = blockIdx.x - n * P;
+    const int row = xcd_contiguous(blockIdx.x, gridDim.x);
+    const int c8 = C / 8, n = row / P, p = row - n * P;
     const long img = (long)n * H * W * C;
     for (int t = threadIdx.x; t < Q * c8; t += 256) {
         const int q = t / c8, cg = t - q * c8;
@@ -356,7 +369,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bwd_rows_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                           T* __restrict__ dx, int H, int W, int C, int P, int Q, int K,
                                                           int S, int pad) {
-    const int c8 = C / 8, n = blockIdx.x / H, h = blockIdx.x - n * H;
+    const int row = xcd_contiguous(blockIdx.x, gridDim.x);   // input rows 2p, 2p + 1 read pooled row p
+    const int c8 = C / 8, n = row / H, h = row - n * H;
     const int p_lo = max(0, (h + pad - K + S) / S), p_hi = min(P - 1, (h + pad) / S);
     for (int t = threadIdx.x; t < W * c8; t += 256) {
         const int w = t / c8, cg = t - w * c8;
@@ -792,10 +806,10 @@ DDL_API int ddl_bn_relu_maxpool(int dtype, const void* x, const float* scale, co
     const long tot = (long)N * P * Q * (C / 8);
     if ((long)N * P < (1L << 31) && rows_form_enabled()) {
         DISPATCH_T(dtype,
-                   (bn_relu_maxpool_rows_k<bf16_t><<<N * P, 256, 0, st>>>((const bf16_t*)x, scale, shift, (bf16_t*)y,
-                                                                          idx, mask, H, W, C, P, Q)),
-                   (bn_relu_maxpool_rows_k<float><<<N * P, 256, 0, st>>>((const float*)x, scale, shift, (float*)y, idx,
-                                                                         mask, H, W, C, P, Q)));
+                   (bn_relu_maxpool_rows_k<bf16_t><<<N * P, 256, 0, st>>>(
+                       (const bf16_t*)x, scale, shift, (bf16_t*)y, idx, mask, H, W, C, P, Q)),
+                   (bn_relu_maxpool_rows_k<float><<<N * P, 256, 0, st>>>(
+                       (const float*)x, scale, shift, (float*)y, idx, mask, H, W, C, P, Q)));
         DDL_RETURN_LAUNCH();
     }
     DISPATCH_T(dtype,
@@ -811,10 +825,10 @@ DDL_API int ddl_maxpool_bwd(int dtype, const void* dy, const uint8_t* idx, void*
     const long tot = (long)N * H * W * (C / 8);
     if ((long)N * H < (1L << 31) && rows_form_enabled()) {
         DISPATCH_T(dtype,
-                   (maxpool_bwd_rows_k<bf16_t><<<N * H, 256, 0, st>>>((const bf16_t*)dy, idx, (bf16_t*)dx, H, W, C, P, Q,
-                                                                      K, S, pad)),
-                   (maxpool_bwd_rows_k<float><<<N * H, 256, 0, st>>>((const float*)dy, idx, (float*)dx, H, W, C, P, Q, K,
-                                                                     S, pad)));
+                   (maxpool_bwd_rows_k<bf16_t><<<N * H, 256, 0, st>>>(
+                       (const bf16_t*)dy, idx, (bf16_t*)dx, H, W, C, P, Q, K, S, pad)),
+                   (maxpool_bwd_rows_k<float><<<N * H, 256, 0, st>>>(
+                       (const float*)dy, idx, (float*)dx, H, W, C, P, Q, K, S, pad)));
         DDL_RETURN_LAUNCH();
     }
     DISPATCH_T(dtype,
