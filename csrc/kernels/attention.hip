@@ -61,8 +61,14 @@ __device__ __forceinline__ int swz_tr(int r, int c) { return c ^ (2 * ((r >> 1) 
 // x one chunk per half-wave pass) and read transposed (8 rows x 2 chunks per pass).  swz_tr repeats
 // its pattern every 8 rows, so rows r and r + 8 of a write pass collided (2-way: the 16.7 % LDS
 // bank conflicts of attn_bwd_fused_k); bit 3 of the row in the chunk's low bit separates them and
-// keeps the transposed reads conflict free.
+// keeps the transposed reads conflict free.  A ds_write_b64 lane group is 16 lanes banked over 128 B
+// (one row), so rows r and r ^ 1 -- same chunk -- still shared 8-byte slots: odd rows also swap the
+// two 8-byte halves of every chunk (ds_half; frag_tr<., true> reads them back), which makes the 16
+// pieces of a write pass 16 distinct slots and leaves every transposed read pass's slot set as it was.
 __device__ __forceinline__ int swz_ds(int r, int c) { return c ^ ((2 * ((r >> 1) & 3)) | ((r >> 3) & 1)); }
+
+// byte offset of the 8-byte half `h` (0 / 1) of a chunk in row r of a dS^T image
+__device__ __forceinline__ int ds_half(int r, int h) { return ((h ^ r) & 1) * 8; }
 
 template <bool TR, bool DS = false>
 __device__ __forceinline__ int lds_off(int r, int c) {
@@ -86,8 +92,10 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* lds, int kb, int cbase) {
     const int g = l >> 4, q = (l >> 2) & 3, p = l & 3;
     const int col = cbase + 4 * p;
     const int ra = kb + 4 * g + q, rb = ra + 16;
-    const char* pa = lds + lds_off<TR, DS>(ra, col >> 3) + (p & 1) * 8;
-    const char* pb = lds + lds_off<TR, DS>(rb, col >> 3) + (p & 1) * 8;
+    // dS^T images also swap the 8-byte halves of odd rows (swz_ds below); rb = ra + 16 has ra's parity
+    const int half = DS ? ((p ^ ra) & 1) : (p & 1);
+    const char* pa = lds + lds_off<TR, DS>(ra, col >> 3) + half * 8;
+    const char* pb = lds + lds_off<TR, DS>(rb, col >> 3) + half * 8;
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pa);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)pb);
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -390,7 +398,10 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
     // 23 % conflicted tr reads; a second, transposed copy of each tile doubled the staging)
     __shared__ __attribute__((aligned(16))) char smem[2 * TQ * ROWB];
     __shared__ float s_lse[TQ], s_delta[TQ];
-    __shared__ __attribute__((aligned(16))) uint32_t s_dm[4 * TQ];      // this tile's keep words [g][q]
+    // this tile's keep words [g][q], rows TQ + 8 words apart (at TQ words = 256 B, the 4 rows a lane
+    // group's 16-byte reads hit at one q shared banks: 2-way)
+    constexpr int DMT = TQ + 8;
+    __shared__ __attribute__((aligned(16))) uint32_t s_dm[4 * DMT];
     const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -417,7 +428,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
     static_assert(TROWS_B <= 128 && 128 % TROWS_B == 0, "a workgroup's keys in one 128-key keep word");
     const int kq = kok ? myk : 0;
     const int kw_blk = (blockIdx.x * TROWS_B) >> 7;
-    const uint32_t* dmw = s_dm + ((kq >> 2) & 3) * TQ;
+    const uint32_t* dmw = s_dm + ((kq >> 2) & 3) * DMT;
     const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
     f32x4 dv[4], dk[4];
 #pragma unroll
@@ -446,7 +457,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
         __syncthreads();             // previous tile fully consumed
         a.store<true>(sQ);
         c.store<true>(sO);
-        if (p_drop > 0.f && threadIdx.x < 4 * TQ) s_dm[threadIdx.x] = wd;
+        if (p_drop > 0.f && threadIdx.x < 4 * TQ) s_dm[(threadIdx.x >> 6) * DMT + (threadIdx.x & (TQ - 1))] = wd;
         if (threadIdx.x < TQ) {
             s_lse[threadIdx.x] = nlse;
             s_delta[threadIdx.x] = ndel;
@@ -854,7 +865,10 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
     __shared__ __attribute__((aligned(16))) float s_lse[FS];
     __shared__ __attribute__((aligned(16))) float s_delta[FS];
     __shared__ float s_mask[FS];
-    __shared__ __attribute__((aligned(16))) uint32_t s_dm[DROP ? 4 * FS : 4];   // keep-bit words [g][q]
+    // keep-bit words [g][q], rows DMS words apart: a lane group's 16-byte reads hit 4 rows at one q,
+    // and at FS words (2 x 256 B) apart those rows shared banks (2-way)
+    constexpr int DMS = FS + 8;
+    __shared__ __attribute__((aligned(16))) uint32_t s_dm[DROP ? 4 * DMS : 4];
     const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
     const long rs = 3L * H * D;
@@ -908,7 +922,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
     }
     if (DROP) {   // the forward's dropout keep bits of this (b, h): word (g, q), one per thread
         const int gq = tid >> 7, q = tid & (FS - 1);
-        s_dm[tid] = q < S ? dmask[dmask_word(bh, S, 0, gq, q)] : 0u;
+        s_dm[gq * DMS + q] = q < S ? dmask[dmask_word(bh, S, 0, gq, q)] : 0u;
     }
     __syncthreads();
 
@@ -929,7 +943,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
         const float mb2 = s_mask[kok ? myk : 0];
         // my key's dropout keep bits: LDS words (gk, q), bit kbit
         const int kq = kok ? myk : 0;
-        const uint32_t* dmw = s_dm + (DROP ? ((kq >> 2) & 3) * FS : 0);
+        const uint32_t* dmw = s_dm + (DROP ? ((kq >> 2) & 3) * DMS : 0);
         const int kbit = (kq >> 4) * 4 + (kq & 3);
         f32x4 dv[4], dk[4];
 #pragma unroll
@@ -1021,7 +1035,7 @@ __global__ __launch_bounds__(512, 4) void attn_bwd_fused_k(const bf16_t* __restr
             const int q0 = 16 * c + 4 * g;             // block c = (qc, j) = (c / 2, c % 2)
             char* img = q0 < 64 ? sT0 : sT1;
             const int qq = q0 & 63;
-            *reinterpret_cast<uint2*>(img + lds_off<true, true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[c];
+            *reinterpret_cast<uint2*>(img + lds_off<true, true>(myk, qq >> 3) + ds_half(myk, (qq >> 2) & 1)) = dsk[c];
         }
     }
     __syncthreads();
@@ -1251,7 +1265,8 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
     constexpr int OFF_DEL = OFF_LSE + FM * 4;
     constexpr int OFF_MSK = OFF_DEL + FM * 4;
     constexpr int OFF_DM = OFF_MSK + FM * 4;
-    __shared__ __attribute__((aligned(16))) char smem[OFF_DM + (DROP ? 2 * 4 * FM * 4 : 16)];
+    constexpr int DMM = FM + 8;     // keep-word row stride (see attn_bwd_fused_k's DMS)
+    __shared__ __attribute__((aligned(16))) char smem[OFF_DM + (DROP ? 2 * 4 * DMM * 4 : 16)];
     float* s_cs = reinterpret_cast<float*>(smem + OFF_CS);     // [w][part][d]
     float* s_lse = reinterpret_cast<float*>(smem + OFF_LSE);
     float* s_delta = reinterpret_cast<float*>(smem + OFF_DEL);
@@ -1321,7 +1336,7 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int idx = tid + NT * i, kw = idx >> 10, gq = (idx >> 8) & 3, q = idx & (FM - 1);
-            s_dm[idx] = q < S ? dmask[dmask_word(bh, S, kw, gq, q)] : 0u;
+            s_dm[(kw * 4 + gq) * DMM + q] = q < S ? dmask[dmask_word(bh, S, kw, gq, q)] : 0u;
         }
     }
     __syncthreads();
@@ -1339,7 +1354,7 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
         for (int kk = 0; kk < 2; ++kk) kf[kk] = frag_rows<true>(sK, 16 * w, kk);
         const float mb2 = s_mask[kok ? myk : 0];
         const int kq = kok ? myk : 0;
-        const uint32_t* dmw = s_dm + (DROP ? (kq >> 7) * 4 * FM + ((kq >> 2) & 3) * FM : 0);
+        const uint32_t* dmw = s_dm + (DROP ? ((kq >> 7) * 4 + ((kq >> 2) & 3)) * DMM : 0);
         const int kbit = ((kq >> 4) & 7) * 4 + (kq & 3);
         f32x4 dv[4], dk[4];
 #pragma unroll
@@ -1432,7 +1447,8 @@ __global__ __launch_bounds__(64 * MW, 1) void attn_bwd_med_k(const bf16_t* __res
             const int q0 = 16 * c + 4 * g;
             char* img = q0 < 64 ? sT0 : sT1;
             const int qq = q0 & 63;
-            *reinterpret_cast<uint2*>(img + lds_off<true, true>(myk, qq >> 3) + (qq & 7) * 2) = dsk[8 * half + c];
+            *reinterpret_cast<uint2*>(img + lds_off<true, true>(myk, qq >> 3) + ds_half(myk, (qq >> 2) & 1)) =
+                dsk[8 * half + c];
         }
         __syncthreads();
         const int qblk = 8 * half + qsub;
