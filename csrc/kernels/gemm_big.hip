@@ -220,7 +220,8 @@ struct Stager {
     // tiles).  Without KTAIL the KC / KO paths are a 64-bit add of a uniform
     // offset per DMA; the K-tail variant swaps lanes past K onto the zero page.
     __device__ __forceinline__ void stage(const BigParams& p, char* smem, int buf, int h, int kt) {
-        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        // (scalar wave index: the LDS-DMA destinations are SGPR values for M0, no v_readfirstlane per DMA)
+        const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
         char* hbase = smem + half_off(buf, IS_A ? 0 : 1, h);
         const bool ktail = KTAIL && (kt + 1) * BK > K;       // uniform: partial last tile
         if (L == KC) {
