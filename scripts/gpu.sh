@@ -138,7 +138,12 @@ step() {
           > gpurun_out/plans/tune.log 2>&1 || { tail -20 gpurun_out/plans/tune.log; return 1; }
         echo "$cmd: $(tail -1 gpurun_out/plans/tune.log | cut -c1-200)"
       done
-      python3 -c "import json; print(len(json.load(open('gpurun_out/plans/cache.json'))), 'signatures')" ;;
+      python3 -c "import json; print(len(json.load(open('gpurun_out/plans/cache.json'))), 'signatures')"
+      # the BERT-large preset fits a larger batch once the table is loaded (no tuner workspaces in its
+      # probe): after make_plan_table.py, run it again with the new table and add its misses with
+      #   DDL_GEMM_TUNE_CACHE=gpurun_out/plans/preset_large.json $TRAIN --preset bert_large_lamb ...
+      #   python scripts/make_plan_table.py --only-new gpurun_out/plans/preset_large.json
+      ;;
     rehearse2)
       DDL_BACKEND=gloo timeout -k 10 500 python bench.py --gpus 2 --steps 3 --warmup 1 --batch 64 --bert-batch 32 \
         > gpurun_out/rehearse2.log 2>&1 || { tail -30 gpurun_out/rehearse2.log; return 1; }
