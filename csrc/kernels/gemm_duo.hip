@@ -610,12 +610,16 @@ DDL_API int ddl_gemm_duo(int mode, const void* A, long lda, const void* B, long 
     p.tiles_m = (M + TM - 1) / TM;
     p.tiles_n = N / TN;
     if (mode == 3) {
-        static const bf16_t* zp = [] {
+        // the zero page's address on the current device (a __device__ symbol has one per device)
+        static const bf16_t* zp[64] = {};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+        if (!zp[dev]) {
             void* a = nullptr;
-            return hipGetSymbolAddress(&a, HIP_SYMBOL(g_duo_zero)) == hipSuccess ? (const bf16_t*)a : nullptr;
-        }();
-        if (!zp) return -1;
-        p.zero = zp;
+            if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_duo_zero)) != hipSuccess || !a) return -1;
+            zp[dev] = (const bf16_t*)a;
+        }
+        p.zero = zp[dev];
         p.cN = conv[0]; p.cH = conv[1]; p.cW = conv[2]; p.cC = conv[3]; p.cP = conv[4]; p.cQ = conv[5];
         p.cstride = conv[6]; p.h_off = conv[7]; p.w_off = conv[8]; p.h_step = conv[9]; p.w_step = conv[10];
         p.cR = conv[11]; p.cS = conv[12];
