@@ -114,6 +114,7 @@ struct BigParams {
     int xsplit;               // split-K on a 1-D grid whose XCDs run contiguous (split, tile) runs
     int part_bf16;            // split-K partial slabs stored as bf16 (DDL_GEMM_PART_BF16, default on)
     int zero_b1;              // 256 x 192 NT tiles: unused B rows from the zero page (DDL_GEMM_ZB1, default on)
+    int wg_tbl;               // gemm_wg_k CONVW: output-pixel row table in LDS (the split's rows fit; host)
 };
 // tile-ticket slot layout: 8 per-XCD counters + one exit counter, 128 B apart
 constexpr int SCHED_STRIDE = 32;
@@ -1581,12 +1582,32 @@ constexpr int WG_HALF = WG_BK * 256;     // bytes: 32 k-rows x 128 columns x 2 B
 // NW: 4 waves (one per SIMD, 256 x 128 tiles, "wg") or 8 waves (two per SIMD, 256 x 256 tiles,
 // "wg2": the 256 x 256 kernel's operand bytes per output, the second wave on each SIMD filling the
 // first one's read / barrier gaps).  Every wave owns 128 x 64 (acc 128 registers).
-template <bool CW, int NW>
+// CONVW row table (4-wave kernel): the B operand's reduction rows are output pixels, and decomposing a
+// row into (image, h, w) per DMA -- two divisions, the bounds and a 64-bit address per lane -- made the
+// conv weight gradient's loop 2.6 VALU per MFMA against 0.4 for a plain TN GEMM (15-35 % slower than
+// the same GEMM over a materialized im2col, profiles/wg_convw_r06.log).  The workgroup decomposes its
+// split's rows ONCE into an LDS table behind the operand ring -- per row the element offset of its
+// (h_off, w_off)-shifted corner pixel and the corner's (h, w) -- and a DMA then reads one 8-byte record:
+// two adds, the bounds test, one 32-bit add and the zero-page select.
+constexpr int WG_TBL_BYTES = 160 * 1024 - WG_ST * 3 * WG_HALF;   // 64 KB: 8192 rows
+// table records are read by inline asm: a compiler-visible read of the LDS object -- even through a
+// restrict-qualified pointer -- made its LDS-DMA alias tracking wait vmcnt(0), i.e. every in-flight
+// operand tile, before each record (that version ran 1.5x SLOWER than the decomposing loader).  The
+// caller waits lgkmcnt(0) itself before using the value.
+__device__ __forceinline__ uint2 wg_row_rec(uint32_t lds_addr) {
+    uint2 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(lds_addr));
+    return v;
+}
+
+template <bool CW, int NW, bool TBL = false>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_wg_k(BigParams p) {
     constexpr int WN = NW / 2, TNW = 64 * WN, BH = TNW / 128;   // waves along N, tile N, B halves
     constexpr int JW = 8 / NW;                                   // DMA instructions per wave per half
     constexpr int DMA = JW * (2 + BH);                           // ... per k-tile
-    __shared__ __attribute__((aligned(16))) char smem[WG_ST * (2 + BH) * WG_HALF];   // 96 / 128 KB, one LDS object
+    constexpr int RING = WG_ST * (2 + BH) * WG_HALF;
+    static_assert(!TBL || (CW && RING + WG_TBL_BYTES <= 160 * 1024), "row table: CONVW, behind the ring");
+    __shared__ __attribute__((aligned(16))) char smem[RING + (TBL ? WG_TBL_BYTES : 0)];   // one LDS object
     // stage s: A half 0, A half 1, B half 0 (, B half 1)
     auto wg_off = [](int s, int x, int h) { return (s * (2 + BH) + (x ? 2 + h : h)) * WG_HALF; };
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -1608,14 +1629,47 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_wg_k(BigParams p) {
     const int c = (l & 15) ^ swz_ko(krow0);
     const bf16_t* ga = p.A + (long)krow0 * p.lda + m0 + 8 * c;
     const bf16_t* gb = p.B + (long)krow0 * p.ldb + n0 + 8 * c;
-    int cdh[BH], cdw[BH], cci[BH];
+    int cdh[BH], cdw[BH], cci[BH], toff[BH];
 #pragma unroll
     for (int h = 0; h < BH; ++h) {
         cdh[h] = cdw[h] = cci[h] = 0;
         if (CW) tap_of(p.cd, n0 + h * 128 + 8 * c, cdh[h], cdw[h], cci[h]);
+        toff[h] = (cdh[h] * p.cd.W + cdw[h]) * p.cd.C + cci[h];   // the lane's tap / channel offset
+    }
+    if constexpr (TBL) {
+        for (int r = threadIdx.x; r < nt * WG_BK; r += NW * 64) {
+            const Pix x = decompose(p.cd, p.B, kt0 * WG_BK + r, p.K);
+            const int corner = (int)(x.img - p.B) + (x.hb * p.cd.W + x.wb) * p.cd.C;
+            *reinterpret_cast<uint2*>(smem + RING + r * 8) =
+                make_uint2((uint32_t)corner, ((uint32_t)x.hb & 0xffffu) | ((uint32_t)x.wb << 16));
+        }
+        __syncthreads();
     }
     auto stage = [&](int kt, int st) {
         const long ka = (long)kt * WG_BK;
+        if constexpr (TBL) {
+            // every DMA's row record first, the A tiles' DMAs under the LDS reads, then the B DMAs
+            uint2 rec[JW];
+#pragma unroll
+            for (int j = 0; j < JW; ++j)
+                rec[j] = wg_row_rec((uint32_t)(uintptr_t)(smem + RING) + ((int)ka - kt0 * WG_BK + krow0 + j * 4) * 8);
+#pragma unroll
+            for (int j = 0; j < JW; ++j) {
+                glds(ga + (ka + j * 4) * p.lda, smem + wg_off(st, 0, 0) + (w * JW + j) * 1024);
+                glds(ga + (ka + j * 4) * p.lda + 128, smem + wg_off(st, 0, 1) + (w * JW + j) * 1024);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < JW; ++j)
+#pragma unroll
+                for (int h = 0; h < BH; ++h) {
+                    const int hh = (int)(short)(rec[j].y & 0xffffu) + cdh[h], ww = ((int)rec[j].y >> 16) + cdw[h];
+                    const bool ok = (unsigned)hh < (unsigned)p.cd.H && (unsigned)ww < (unsigned)p.cd.W;
+                    glds(ok ? p.B + ((int)rec[j].x + toff[h]) : p.zero, smem + wg_off(st, 1, h) + (w * JW + j) * 1024);
+                }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < JW; ++j) {
             glds(ga + (ka + j * 4) * p.lda, smem + wg_off(st, 0, 0) + (w * JW + j) * 1024);
@@ -2031,6 +2085,9 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
     p.splits = splits;
     p.split_stride = (long)M * ldc;
     p.part_bf16 = !out_f32 && part_bf16_enabled() ? 1 : 0;
+    // the row table: the split's rows fit behind the ring and every element offset fits 31 bits
+    p.wg_tbl = conv && !wide && (long)p.kt_per_split * WG_BK * 8 <= WG_TBL_BYTES &&
+               (long)conv[0] * conv[1] * conv[2] * conv[3] < (1L << 31) && conv[1] < 32768 && conv[2] < 32768;
     if (!workspace || ws_elems < p.split_stride * splits) return -2;
     BigParams kp = p;
     kp.C = workspace;
@@ -2039,7 +2096,8 @@ DDL_API int ddl_gemm_wgrad(const void* A, long lda, const void* B, long ldb, voi
         if (conv) hipLaunchKernelGGL((gemm_wg_k<true, 8>), grid, dim3(512), 0, st, kp);
         else hipLaunchKernelGGL((gemm_wg_k<false, 8>), grid, dim3(512), 0, st, kp);
     } else {
-        if (conv) hipLaunchKernelGGL((gemm_wg_k<true, 4>), grid, dim3(256), 0, st, kp);
+        if (conv && p.wg_tbl) hipLaunchKernelGGL((gemm_wg_k<true, 4, true>), grid, dim3(256), 0, st, kp);
+        else if (conv) hipLaunchKernelGGL((gemm_wg_k<true, 4>), grid, dim3(256), 0, st, kp);
         else hipLaunchKernelGGL((gemm_wg_k<false, 4>), grid, dim3(256), 0, st, kp);
     }
     launch_reduce(p, workspace, st);
