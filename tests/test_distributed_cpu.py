@@ -132,10 +132,14 @@ def _train_zero_checkpoint(tmpdir):
     t = Trainer(cfg)
     assert t.opt.shard is not None
     s = t.run()
-    master, m, v = t.opt.master.clone(), t.opt.m.clone(), t.opt.v.clone()
-    t2 = Trainer(cfg.replace(resume=True, steps=1))
-    err = max((t2.opt.master - master).abs().max().item(), (t2.opt.m - m).abs().max().item(),
-              (t2.opt.v - v).abs().max().item())
+    # compare the full (gathered) state: the local shards depend on the bucket layout, which the
+    # default auto bucket policy sizes from a timed comm probe -- so pin a different layout on
+    # resume on purpose (the checkpoint is layout-independent)
+    before = {k: x.clone() for k, x in t.opt.state_dict().items() if torch.is_tensor(x)}
+    t2 = Trainer(cfg.replace(resume=True, steps=1, bucket_mb=1.0, first_bucket_mb=0.5))
+    after = {k: x for k, x in t2.opt.state_dict().items() if torch.is_tensor(x)}
+    assert set(before) == set(after) == {"master", "exp_avg", "exp_avg_sq"}
+    err = max((after[k] - before[k]).abs().max().item() for k in before)
     resumed = t2.step
     s2 = t2.run()
     return {"rank": dist.get_rank(), "err": err, "resumed_step": resumed, "loss": s["final_loss"],
