@@ -782,7 +782,8 @@ def test_duo_conv(N, H, W, C, K, stride, epi):
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(768, 768, 16384, None), (768, 3072, 4096, 3), (2304, 768, 2048, 1),
-                                          (256, 128, 96, 2), (512, 256, 4096, 7)])
+                                          (256, 128, 96, 2), (512, 256, 4096, 7), (1024, 128, 8192, 12),
+                                          (512, 256, 16384, 40), (256, 256, 32768, 100)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_duo_weight_gradient(M, N, K, splits, accumulate):
     """TN weight gradient on the dual-workgroup kernel (k-outer A staged as two [32 k][128] halves, split-K
