@@ -1,5 +1,5 @@
 # In-model kernel tables (BERT-base) for the split-K reduce A/B: tree library vs ab/libddl_old.so, both on
-# ab/gemm_plans_new.json (see ab_reduce.sh)
+# ab/gemm_plans_new.json (see ab_same_plans.sh)
 set -o pipefail
 A=$PWD/databricks_distributed_deep_learning_amd/_native/ab
 export DDL_GEMM_PLAN_TABLE=$A/gemm_plans_new.json
