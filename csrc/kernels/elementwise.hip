@@ -691,6 +691,27 @@ __global__ __launch_bounds__(256) void acc_f32_k(T* __restrict__ dst, const floa
 // Gradient-accumulation drain (micro-step of grad_accum): acc (fp32) += g; g = 0 -- one pass
 // over the arena instead of an ATen add plus a zero fill; 8 elements per thread per
 // iteration (16-byte gradient loads / stores, two float4 on the accumulator).
+// Gradient accumulation into the fp32 accumulator, one pass: acc = g (FIRST: the accumulator's
+// previous contents are dead, so it is neither zero-filled per step nor read) or acc += g, and g = 0
+// when ZERO (a micro-step's drain; the last micro-step's gradients are summed in place and left).
+template <typename T, bool FIRST, bool ZERO>
+__global__ __launch_bounds__(256) void acc_grad_k(float* __restrict__ acc, T* __restrict__ g, long n8) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+        float v[8], a[8];
+        load8(g + i * 8, v);
+        if (!FIRST) {
+            load8(acc + i * 8, a);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += a[e];
+        }
+        store8(acc + i * 8, v);
+        if (ZERO) {
+            const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            store8(g + i * 8, z);
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void drain_acc_k(float* __restrict__ acc, T* __restrict__ g, long n8) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
@@ -996,6 +1017,21 @@ DDL_API int ddl_acc_f32(int dtype, void* dst, const float* src, long n, hipStrea
     DDL_RETURN_LAUNCH();
 }
 
+// acc (fp32) = / += g (bf16 / fp32), then g = 0 if zero_g (see acc_grad_k).  n % 8 == 0, 16-byte aligned.
+DDL_API int ddl_acc_grad(int dtype, float* acc, void* g, long n, int first, int zero_g, hipStream_t st) {
+    if (n % 8) return -1;
+    const long n8 = n / 8;
+    const int grid = (int)std::min<long>(4096, (n8 + 255) / 256);
+#define AGK(T, F, Z) acc_grad_k<T, F, Z><<<grid, 256, 0, st>>>(acc, (T*)g, n8)
+#define AGT(T) do { if (first) { if (zero_g) AGK(T, true, true); else AGK(T, true, false); } \
+                    else { if (zero_g) AGK(T, false, true); else AGK(T, false, false); } } while (0)
+    if (dtype == 1) AGT(bf16_t);
+    else AGT(float);
+#undef AGT
+#undef AGK
+    DDL_RETURN_LAUNCH();
+}
+
 // acc (fp32) += g (bf16 / fp32); g = 0.  n % 8 == 0, 16-byte aligned buffers.
 DDL_API int ddl_drain_acc(int dtype, float* acc, void* g, long n, hipStream_t st) {
     if (n % 8) return -1;
@@ -1079,6 +1115,32 @@ __global__ __launch_bounds__(256) void rows_add_row_k(T* __restrict__ dst, const
                                                       long rows, long cols) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.x * blockDim.x)
         dst[i] = from_f<T>(to_f(a[i]) + to_f(v[i % cols]));
+}
+
+// ViT token assembly: out[b][s] = (s == 0 ? head : src[b][s - 1]) + table[s] for s < S, i.e. the
+// class token prepended to the patch tokens plus the position table, in one pass (it was an ATen
+// cat + broadcast add).  V = 8: 16-byte bf16 vectors (H % 8 == 0), V = 1: scalar.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void seq_prepend_add_k(T* __restrict__ out, const T* __restrict__ src,
+                                                         const T* __restrict__ head, const T* __restrict__ table,
+                                                         long B, long S, long H) {
+    const long hv = H / V, n = B * S * hv;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const long row = i / hv, c = (i - row * hv) * V;
+        const long b = row / S, s = row - b * S;
+        const T* a = s == 0 ? head + c : src + (b * (S - 1) + s - 1) * H + c;
+        const T* t = table + s * H + c;
+        if constexpr (V == 8) {
+            float x[8], y[8];
+            load8(a, x);
+            load8(t, y);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] += y[e];
+            store8(out + row * H + c, x);
+        } else {
+            out[row * H + c] = from_f<T>(to_f(*a) + to_f(*t));
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void zero16_k(uint4* __restrict__ p, long n16) {
@@ -1287,6 +1349,24 @@ DDL_API int ddl_rows_add_row(int dtype, void* dst, const void* a, const void* v,
                                                                             (const bf16_t*)v, rows, cols)),
                (rows_add_row_k<float><<<grid_for(rows * cols), 256, 0, st>>>((float*)dst, (const float*)a,
                                                                            (const float*)v, rows, cols)));
+    DDL_RETURN_LAUNCH();
+}
+
+// out [B][S][H] = [head | src[b] (S - 1 rows)] + table [S][H] (see seq_prepend_add_k)
+DDL_API int ddl_seq_prepend_add(int dtype, void* out, const void* src, const void* head, const void* table, long B,
+                                long S, long H, hipStream_t st) {
+    if (B <= 0 || S <= 0 || H <= 0) return 0;
+    const bool v8 = dtype == 1 && H % 8 == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)src % 16) == 0 &&
+                    ((uintptr_t)head % 16) == 0 && ((uintptr_t)table % 16) == 0;
+    if (v8)
+        seq_prepend_add_k<bf16_t, 8><<<grid_for(B * S * (H / 8)), 256, 0, st>>>(
+            (bf16_t*)out, (const bf16_t*)src, (const bf16_t*)head, (const bf16_t*)table, B, S, H);
+    else
+        DISPATCH_T(dtype,
+                   (seq_prepend_add_k<bf16_t, 1><<<grid_for(B * S * H), 256, 0, st>>>(
+                       (bf16_t*)out, (const bf16_t*)src, (const bf16_t*)head, (const bf16_t*)table, B, S, H)),
+                   (seq_prepend_add_k<float, 1><<<grid_for(B * S * H), 256, 0, st>>>(
+                       (float*)out, (const float*)src, (const float*)head, (const float*)table, B, S, H)));
     DDL_RETURN_LAUNCH();
 }
 

@@ -98,15 +98,15 @@ class ViTForImageClassification(nn.Module):
         return x.reshape(B, (Hh // P) * (Ww // P), P * P * C)
 
     def forward(self, x):
-        B = x.shape[0]
         # implicit im2col on the image (ops.patch_embed): no patchify copy on the GPU
         t = ops.patch_embed(x, self.patch_embed.weight, self.patch_embed.bias, self.config.patch_size)
-        t = torch.cat([self.cls_token.expand(B, -1, -1).to(t.dtype), t], 1) + self.position_embeddings.to(t.dtype)
+        # [cls | patches] + position embeddings in one native pass (ops/glue.py prepend_token_add)
+        t = ops.prepend_token_add(t, self.cls_token.to(t.dtype), self.position_embeddings.to(t.dtype))
         h = self.dropout(t)
         for layer in self.layers:
             h = layer(h)
         h = self.layernorm(h)
-        return self.classifier(h[:, 0].contiguous())
+        return self.classifier(ops.first_token(h))
 
 
 def vit_b16(num_classes: int = 1000, dropout: float = 0.0, image_size: int = 224) -> ViTForImageClassification:

@@ -19,4 +19,4 @@ from .attention import attention  # noqa: F401
 from .loss import cross_entropy, softmax_topk  # noqa: F401
 from .pool import max_pool2d, global_avg_pool  # noqa: F401
 from .embedding import embedding  # noqa: F401
-from .glue import embedding_residual, first_token  # noqa: F401
+from .glue import embedding_residual, first_token, prepend_token_add  # noqa: F401

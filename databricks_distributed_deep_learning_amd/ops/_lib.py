@@ -150,9 +150,11 @@ _SIGS = {
     "ddl_add_into": [I, P, P, L, P],
     "ddl_zero": [P, L, P],
     "ddl_rows_add_row": [I, P, P, P, L, L, P],
+    "ddl_seq_prepend_add": [I, P, P, P, P, L, L, L, P],
     "ddl_sort_ids_ok": [L, L],
     "ddl_sort_ids": [P, L, P, P, P],
     "ddl_drain_acc": [I, P, P, L, P],
+    "ddl_acc_grad": [I, P, P, L, I, I, P],
     "ddl_softmax_topk": [I, P, L, I, I, P, P, P, P],
     "ddl_gemm_conv_multi": [I, I, P, P, P, P, P, L, I, P, P],
     "ddl_conv3x3": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, I, P],

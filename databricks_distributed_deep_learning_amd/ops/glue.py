@@ -10,8 +10,13 @@ launch ATen kernels, each as ONE launch of the framework's o
   the two parameters' gradient-arena slots (rows 0..S-1 of the position table; the column sums over S
   into token type 0's row) -- no slice / select backward, no broadcast sum, no AccumulateGrad adds.
 
-Reference: the model files these replace call sites in (``models/bert.py``; HF's
-``BertEmbeddings`` / ``BertPooler``, which the CPU oracle tests compare against).
+* :func:`prepend_token_add` -- ViT's ``cat([cls_token.expand(B), patches], 1) + position_embeddings``
+  in one pass (``ddl_seq_prepend_add``).  Backward: the patch tokens' gradient as one strided copy, the
+  position table's as one column-sum pass over the batch, the class token's from that sum's first row --
+  straight into the parameters' gradient-arena slots when they have them.
+
+Reference: the model files these replace call sites in (``models/bert.py``, ``models/vit.py``; HF's
+``BertEmbeddings`` / ``BertPooler`` / ``ViTEmbeddings``, which the CPU oracle tests compare against).
 """
 from __future__ import annotations
 
@@ -89,3 +94,53 @@ def embedding_residual(pos_w: torch.Tensor, tok_w: torch.Tensor, S: int) -> torc
             and H % 8 == 0 and _lib.use_native(pos_w, tok_w)):
         return _EmbeddingResidual.apply(pos_w, tok_w, S)
     return pos_w[:S].unsqueeze(0) + tok_w[0].view(1, 1, -1)
+
+
+class _PrependTokenAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, head, table):
+        B, P, H = x.shape
+        S = P + 1
+        x = x.contiguous()
+        out = torch.empty(B, S, H, dtype=x.dtype, device=x.device)
+        call("ddl_seq_prepend_add", dcode(x), p(out), p(x), p(head), p(table), B, S, H)
+        ctx.params = (head, table)
+        ctx.shape = (B, S, H)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        head, table = ctx.params
+        B, S, H = ctx.shape
+        dout = dout.contiguous()
+        d2 = dout.view(B, S * H)
+        # patch tokens: rows 1.. of every sequence, one strided copy
+        dx = torch.empty(B, S - 1, H, dtype=dout.dtype, device=dout.device)
+        E.copy2d(dx.view(B, (S - 1) * H), d2[:, H:], (S - 1) * H, B, (S - 1) * H, S * H, B, (S - 1) * H)
+        # position table: the column sums over the batch; the class token: their first row
+        dtab = torch.empty(S * H, dtype=table.dtype, device=dout.device)
+        E.colsum(d2, dtab)
+        st, sh = grad_sink(table), grad_sink(head)
+        dt = dh = None
+        if st is not None:
+            E.add_into(st.view(-1)[:S * H], dtab)
+            grad_ready(table)
+        else:
+            dt = dtab.view(table.shape)
+        if sh is not None:
+            E.add_into(sh.view(-1)[:H], dtab[:H])
+            grad_ready(head)
+        else:
+            dh = dtab[:H].clone().view(head.shape)
+        return dx, dh, dt
+
+
+def prepend_token_add(x: torch.Tensor, head: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """``cat([head.expand(B, 1, H), x], 1) + table`` for x [B, P, H], head [1, 1, H] (or [H]), table
+    [1, P + 1, H] (or [P + 1, H]) -- ViT's class token and position embeddings."""
+    B, P, H = x.shape
+    if (x.dtype == head.dtype == table.dtype and x.dtype in (torch.bfloat16, torch.float32)
+            and head.numel() == H and table.numel() == (P + 1) * H and (P + 1) * H % 8 == 0
+            and head.is_contiguous() and table.is_contiguous() and _lib.use_native(x, head, table)):
+        return _PrependTokenAdd.apply(x, head, table)
+    return torch.cat([head.reshape(1, 1, H).expand(B, -1, -1), x], 1) + table.reshape(1, P + 1, H)

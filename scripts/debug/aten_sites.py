@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Which framework call sites still dispatch device work to ATen in a training step.
 
-    python scripts/debug/aten_sites.py [bert_base|resnet50]
+    python scripts/debug/aten_sites.py [bert_base|resnet50|vit_b16|bert_large_lamb]
 
 A TorchDispatchMode records every ATen op that touches a CUDA tensor during one steady-state step
 (forward, backward, reducer, optimizer), with the innermost frames of this package on the Python
@@ -53,9 +53,14 @@ class Sites(TorchDispatchMode):
 def main():
     model = sys.argv[1] if len(sys.argv) > 1 else "bert_base"
     ddist.init("auto")
-    cfg = get_preset("resnet50_ddp" if model == "resnet50" else "bert_base_ddp",
-                     batch_size=256 if model == "resnet50" else 128,
-                     **({} if model == "resnet50" else {"dropout": 0.1}))
+    if model == "resnet50":
+        cfg = get_preset("resnet50_ddp", batch_size=256)
+    elif model == "vit_b16":
+        cfg = get_preset("vit_b16")
+    elif model == "bert_large_lamb":     # the profiled configuration (scripts/gpu.sh run_model)
+        cfg = get_preset("bert_large_lamb", batch_size=32)
+    else:
+        cfg = get_preset("bert_base_ddp", batch_size=128, dropout=0.1)
     tr = Trainer(cfg.replace(log_every=0))
     for _ in range(3):
         tr.train_step()

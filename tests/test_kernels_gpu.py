@@ -445,17 +445,60 @@ def test_patch_embed_implicit_im2col(B, H, P, D):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_drain_acc(dtype):
-    """Grad-accumulation drain (ddl_drain_acc): acc32 += g and g = 0 in one pass, against the
-    fp32 reference; also through DataParallel.no_sync (accumulate_fp32)."""
+def test_acc_grad(dtype):
+    """Grad-accumulation pass (ddl_acc_grad): acc32 = g (first micro-step: no zero fill, the old
+    contents unread) or acc32 += g, g = 0 on a micro-step's drain and left as is on the last pass --
+    against the fp32 reference."""
     dev = gpu_device()
     _native_lib_loaded()
-    from databricks_distributed_deep_learning_amd.parallel.ddp import _drain_into
+    from databricks_distributed_deep_learning_amd.parallel.ddp import _acc_grad
     torch.manual_seed(0)
     n = 3 * 8192 + 40
-    g = torch.randn(n, device=dev).to(dtype)
-    acc = torch.randn(n, device=dev)
-    ref = acc + g.float()
-    _drain_into(acc, g)
-    torch.cuda.synchronize()
-    assert torch.equal(acc, ref) and not g.any()
+    for first in (True, False):
+        for zero in (True, False):
+            g = torch.randn(n, device=dev).to(dtype)
+            acc = torch.full((n,), float("nan"), device=dev) if first else torch.randn(n, device=dev)
+            ref = g.float().clone() if first else acc + g.float()
+            g0 = g.clone()
+            _acc_grad(acc, g, first=first, zero_grad=zero)
+            torch.cuda.synchronize()
+            assert torch.equal(acc, ref)
+            assert (not g.any()) if zero else torch.equal(g, g0)
+
+
+def test_no_sync_fp32_accumulation_over_steps():
+    """DataParallel.no_sync with accumulate_fp32 on a bf16 model, world 1: the gradient finish()
+    returns is the fp32 sum of the micro-steps' bf16 gradients in micro-step order -- bit for bit,
+    on the second step too (the accumulator is overwritten by a step's first drain, not zero-filled)."""
+    dev = gpu_device()
+    _native_lib_loaded()
+    from databricks_distributed_deep_learning_amd.optim import ParamArena
+    from databricks_distributed_deep_learning_amd.parallel import DataParallel
+    torch.manual_seed(5)
+
+    def model():
+        torch.manual_seed(6)
+        return torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 16)).to(dev).bfloat16()
+
+    m, ref = model(), model()
+    arena = ParamArena(list(m.named_parameters()))
+    ddp = DataParallel(m, arena, bucket_mb=0.01, first_bucket_mb=0.005, accumulate_fp32=True, comm="torch")
+    for step in range(2):
+        xs = [torch.randn(8, 64, device=dev).bfloat16() for _ in range(3)]
+        ys = [torch.randint(0, 16, (8,), device=dev) for _ in range(3)]
+        ddp.zero_grad()
+        for i in range(3):
+            ctx = ddp.no_sync() if i < 2 else torch.enable_grad()
+            with ctx:
+                torch.nn.functional.cross_entropy(ddp(xs[i]).float(), ys[i]).backward()
+        g = ddp.finish().clone()
+        # reference: each micro-step's bf16 gradient on its own, summed in fp32 in order
+        acc = {}
+        for i in range(3):
+            ref.zero_grad(set_to_none=True)
+            torch.nn.functional.cross_entropy(ref(xs[i]).float(), ys[i]).backward()
+            for n, p_ in ref.named_parameters():
+                acc[n] = p_.grad.float() if i == 0 else acc[n] + p_.grad.float()
+        for e in arena.entries:
+            got = g[e.offset:e.offset + e.numel].view(acc[e.name].shape)
+            assert torch.equal(got, acc[e.name]), (step, e.name, (got - acc[e.name]).abs().max())
