@@ -1099,7 +1099,15 @@ __global__ __launch_bounds__(1024) void ln_colsum_k(const float* __restrict__ pa
 
 // slices for nblk partial rows: S = ceil(nblk / FIN_RPS), capped so the last arriver's pass over
 // the slice rows stays one round trip of 16 row lanes x 8 (ws holds S x 2C floats)
-static int fin_slices(int nblk) { return std::max(1, std::min(128, (nblk + FIN_RPS - 1) / FIN_RPS)); }
+// DDL_FIN_RPS (>= 32: the partial-row buffers hold ceil(nblk / 32) slice rows): rows per slice (A/B)
+static int fin_rps_target() {
+    static const int v = [] { const char* e = getenv("DDL_FIN_RPS"); return e ? std::max(32, atoi(e)) : FIN_RPS; }();
+    return v;
+}
+static int fin_slices(int nblk) {
+    const int t = fin_rps_target();
+    return std::max(1, std::min(128, (nblk + t - 1) / t));
+}
 static int fin_rps(int nblk) { return (nblk + fin_slices(nblk) - 1) / fin_slices(nblk); }
 // The merged launch took 7.6-8.3 us against 6.7 us for one finalize workgroup on <= 512 rows in
 // the round-5 kernel tables, but whole-step A/B prefers it for every row count: ResNet-50 +0.3 %
