@@ -29,7 +29,7 @@ def main():
         y.backward(g)
     e1.record()
     torch.cuda.synchronize()
-    print(f"rows/blk={os.environ.get('DDL_LN_BWD_ROWS', '16')} cap={os.environ.get('DDL_LN_BWD_MAXBLK', '1024')} "
+    print(f"rows/blk={os.environ.get('DDL_LN_BWD_ROWS', '32')} cap={os.environ.get('DDL_LN_BWD_MAXBLK', '1024')} "
           f"ln backward {e0.elapsed_time(e1) / n * 1000:.1f} us")
 
 
