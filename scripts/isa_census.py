@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Instruction census of the MFMA main loops in a kernel source (ISA level, no GPU needed).
 
-    python scripts/isa_census.py csrc/kernels/gemm_duo.hip [--filter REGEX] [--asm OUT.s]
+    python scripts/isa_census.py csrc/kernels/gemm_duo.hip [--filter REGEX] [--asm OUT.s] [--min-mfma N]
 
 Compiles the file for gfx950 to assembly (hipcc --cuda-device-only -S, the library's -O3 and the
 MFMA VGPR-form flag of csrc/build.py where it applies), then for every kernel whose name matches
---filter finds its innermost loop holding >= 32 MFMAs (a back-edge branch to a label at or before
+--filter finds its innermost loop holding >= 32 MFMAs (--min-mfma) (a back-edge branch to a label at or before
 the branch) and counts the instructions by class: MFMA, VALU, SALU, LDS (ds_*), VMEM
 (buffer / global, incl. LDS-DMA), plus the kernel's VGPR count and spill count.  VALU / MFMA in the
 loop is what the per-MFMA-gap issue budget is spent on (MI355X_MICROARCH.md: a 16x16x32 MFMA gap
@@ -65,7 +65,7 @@ def classify(op: str) -> str:
     return "other"
 
 
-def main_loop(body):
+def main_loop(body, min_mfma=32):
     labels = {b.split(":")[0]: j for j, b in enumerate(body) if re.match(r"^\.LBB\d+_\d+:", b)}
     best = None
     for j, b in enumerate(body):
@@ -80,7 +80,7 @@ def main_loop(body):
                 c[classify(t[0])] += 1
         # the innermost loop with the main loop's MFMAs: the shortest span holding >= 32 of them (a
         # persistent kernel's outer tile loop also holds the epilogue)
-        if c["mfma"] >= 32 and (best is None or j - lo < best[2] - best[1]):
+        if c["mfma"] >= min_mfma and (best is None or j - lo < best[2] - best[1]):
             best = (c, lo, j)
     return best
 
@@ -90,6 +90,7 @@ def main() -> int:
     ap.add_argument("src")
     ap.add_argument("--filter", default=".")
     ap.add_argument("--asm", default="")
+    ap.add_argument("--min-mfma", type=int, default=32)
     a = ap.parse_args()
     out = a.asm or os.path.join(tempfile.mkdtemp(), "k.s")
     compile_asm(a.src, out)
@@ -100,7 +101,7 @@ def main() -> int:
     for name, body, meta in kernels(lines):
         if not pat.search(name):
             continue
-        r = main_loop(body)
+        r = main_loop(body, a.min_mfma)
         if r is None:
             continue
         c = r[0]
