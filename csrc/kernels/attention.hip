@@ -209,6 +209,9 @@ __device__ __forceinline__ bf16x8 load_frag_global(const bf16_t* rowp, int kk) {
 // 8 waves (128 queries) per workgroup: each K / V tile is staged once for 128 queries (it was
 // once per 64 with 4 waves: half the staging per query); (512, 1) leaves the compiler its
 // register budget, LDS allows two workgroups per CU
+// MASK / DROP: key-padding mask / probability dropout present (uniform per launch; as run-time
+// checks they put ~50 branches into the tile loop: VALU:MFMA 36 in pmc_bert_large.md)
+template <bool MASK, bool DROP>
 __global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                   bf16_t* __restrict__ out, float* __restrict__ lse, int B, int S, int H,
                                                   float scale, float p_drop, uint64_t seed, uint32_t* __restrict__ dmask) {
@@ -238,9 +241,9 @@ __global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restri
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const uint32_t thresh = drop_thresh16(p_drop);
-    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const float inv_keep = DROP ? 1.f / (1.f - p_drop) : 1.f;
     const uint64_t rowidx = ((uint64_t)bh * S + myq) * S;     // score index of (myq, key 0)
-    const float* mrow = mask ? mask + (long)b * S : nullptr;
+    const float* mrow = MASK ? mask + (long)b * S : nullptr;
 
     const int nt = (S + TK - 1) / TK;
     uint32_t kbits = 0;                                      // dropout keep bits of a 128-key word
@@ -250,14 +253,14 @@ __global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restri
     auto load_mk = [&](int t) __attribute__((always_inline)) {
         const int k = t * TK + (int)threadIdx.x;
         mk_ok = k < S;
-        if (mrow && threadIdx.x < TK) nmk = mrow[min(k, S - 1)];
+        if (MASK && threadIdx.x < TK) nmk = mrow[min(k, S - 1)];
     };
     sk.load(kb, rs, 0, S);
     sv.load(vb, rs, 0, S);
     load_mk(0);
     sk.store<false>(smem);
     sv.store<true>(smem + TK * ROWB);
-    if (mrow && threadIdx.x < TK) s_mk[0][threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
+    if (MASK && threadIdx.x < TK) s_mk[0][threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
         char* sK = smem + (t & 1) * 2 * TK * ROWB;
@@ -286,12 +289,12 @@ __global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restri
         for (int blk = 0; blk < 4; ++blk) {
             const int k0 = t * TK + 16 * blk + 4 * g;
             float4 mk4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (mrow) mk4 = *reinterpret_cast<const float4*>(sM + 16 * blk + 4 * g);
+            if (MASK) mk4 = *reinterpret_cast<const float4*>(sM + 16 * blk + 4 * g);
             const float mk[4] = {mk4.x, mk4.y, mk4.z, mk4.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float v = s[blk][r] * c2;
-                if (mrow) v += mk[r];
+                if (MASK) v += mk[r];
                 if (tail && k0 + r >= S) v = -INFINITY;
                 s[blk][r] = v;
                 tmax = fmaxf(tmax, v);
@@ -307,19 +310,19 @@ __global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restri
 #pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
             bool keep[4] = {true, true, true, true};
-            if (p_drop > 0.f) attn_keep4(seed, rowidx + t * TK + 16 * blk + 4 * g, thresh, S & 1, keep);
+            if (DROP) attn_keep4(seed, rowidx + t * TK + 16 * blk + 4 * g, thresh, S & 1, keep);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float pv = fast_exp2(s[blk][r] - msub);
                 psum += pv;
-                if (p_drop > 0.f) {
+                if (DROP) {
                     pv = keep[r] ? pv * inv_keep : 0.f;
                     kbits |= (uint32_t)keep[r] << ((t & 1) * 16 + 4 * blk + r);
                 }
                 s[blk][r] = pv;
             }
         }
-        if (p_drop > 0.f && ((t & 1) || t == nt - 1)) {      // a 128-key word is complete
+        if (DROP && ((t & 1) || t == nt - 1)) {      // a 128-key word is complete
             if (qok) dmask[dmask_word(bh, S, t >> 1, g, myq)] = kbits;
             kbits = 0;
         }
@@ -338,7 +341,7 @@ __global__ __launch_bounds__(64 * TWF, 1) void attn_fwd_k(const bf16_t* __restri
             char* nK = smem + ((t + 1) & 1) * 2 * TK * ROWB;
             sk.store<false>(nK);
             sv.store<true>(nK + TK * ROWB);
-            if (mrow && threadIdx.x < TK) s_mk[(t + 1) & 1][threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
+            if (MASK && threadIdx.x < TK) s_mk[(t + 1) & 1][threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
         }
         __syncthreads();
     }
@@ -387,6 +390,7 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16_t* __restrict__ d
 // (256, 3): three waves per SIMD -- the compiler then allocates ~160 VGPRs instead of 176 (two
 // waves per SIMD) without spilling; the tiled kernels wait on memory ~45-50 % of wave time,
 // which more resident waves hide (same for the dQ kernel below)
+template <bool DROP>
 __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
     }
     const float mbias = (mask && kok) ? mask[(long)b * S + myk] : 0.f;
     const float c2 = scale * LOG2E;
-    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const float inv_keep = DROP ? 1.f / (1.f - p_drop) : 1.f;
     // my key's keep bits: word (kw, gk) of each query (staged per tile in s_dm), bit kbit; the
     // workgroup's keys share kw
     static_assert(TROWS_B <= 128 && 128 % TROWS_B == 0, "a workgroup's keys in one 128-key keep word");
@@ -445,7 +449,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
         a.load(qb, rs, t * TQ, S);
         c.load(dob, (long)H * D, t * TQ, S);
         const int q = t * TQ + (threadIdx.x & (TQ - 1));
-        if (p_drop > 0.f && threadIdx.x < 4 * TQ)   // keep word (g, q) of the tile, one per thread
+        if (DROP && threadIdx.x < 4 * TQ)   // keep word (g, q) of the tile, one per thread
             wd = q < S ? dmask[dmask_word(bh, S, kw_blk, threadIdx.x >> 6, q)] : 0u;
         if (threadIdx.x < TQ) {
             nlse = q < S ? lse[(long)bh * S + q] : 0.f;
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
         __syncthreads();             // previous tile fully consumed
         a.store<true>(sQ);
         c.store<true>(sO);
-        if (p_drop > 0.f && threadIdx.x < 4 * TQ) s_dm[(threadIdx.x >> 6) * DMT + (threadIdx.x & (TQ - 1))] = wd;
+        if (DROP && threadIdx.x < 4 * TQ) s_dm[(threadIdx.x >> 6) * DMT + (threadIdx.x & (TQ - 1))] = wd;
         if (threadIdx.x < TQ) {
             s_lse[threadIdx.x] = nlse;
             s_delta[threadIdx.x] = ndel;
@@ -480,7 +484,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
 #pragma unroll
         for (int qbk = 0; qbk < 4; ++qbk) {
             const int qa = t * TQ + 16 * qbk + 4 * g;
-            const uint32_t kb4 = p_drop > 0.f ? dmask_pick4(*reinterpret_cast<const uint4*>(dmw + (qa - t * TQ)), kbit)
+            const uint32_t kb4 = DROP ? dmask_pick4(*reinterpret_cast<const uint4*>(dmw + (qa - t * TQ)), kbit)
                                               : 0xfu;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
                 float pv = (q < S && kok) ? fast_exp2(sc[qbk][r] * c2 + mbias * LOG2E - s_lse[ql] * LOG2E) : 0.f;
                 float dpv = dp[qbk][r];
                 float pdrop = pv;
-                if (p_drop > 0.f) {
+                if (DROP) {
                     const bool keep = (kb4 >> r) & 1u;
                     pdrop = keep ? pv * inv_keep : 0.f;
                     dpv = keep ? dpv * inv_keep : 0.f;
@@ -544,6 +548,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dkv_k(const bf16_t* __re
 
 // ============================================================ backward dQ
 // workgroup = 16 TWB queries; wave owns 16 queries (query on the lane), loops over key tiles.
+template <bool MASK, bool DROP>
 __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                      const float* __restrict__ lse, const float* __restrict__ delta,
                                                      const float* __restrict__ mask, bf16_t* __restrict__ dqkv, int B,
@@ -571,12 +576,12 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __res
     const float my_lse = qok ? lse[(long)bh * S + myq] : 0.f;
     const float my_delta = qok ? delta[(long)bh * S + myq] : 0.f;
     const float c2 = scale * LOG2E;
-    const float inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-    const float* mrow = mask ? mask + (long)b * S : nullptr;
+    const float inv_keep = DROP ? 1.f / (1.f - p_drop) : 1.f;
+    const float* mrow = MASK ? mask + (long)b * S : nullptr;
     // this query's keep words, one per 128 keys, loaded up front (S <= 512 here: 4 words)
     constexpr int MAXKW = 4;
     uint32_t kwds[MAXKW] = {~0u, ~0u, ~0u, ~0u};
-    if (p_drop > 0.f && qok) {
+    if (DROP && qok) {
 #pragma unroll
         for (int i = 0; i < MAXKW; ++i)
             if (i < dmask_nkw(S)) kwds[i] = dmask[dmask_word(bh, S, i, g, myq)];
@@ -594,7 +599,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __res
     auto load_mk = [&](int t) __attribute__((always_inline)) {
         const int k = t * TK + (int)threadIdx.x;
         mk_ok = k < S;
-        if (mrow && threadIdx.x < TK) nmk = mrow[min(k, S - 1)];
+        if (MASK && threadIdx.x < TK) nmk = mrow[min(k, S - 1)];
     };
     a.load(kb, rs, 0, S);
     c.load(vb, rs, 0, S);
@@ -603,7 +608,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __res
         __syncthreads();
         a.store<true>(sK);
         c.store<false>(sV);
-        if (mrow && threadIdx.x < TK) s_mk[threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
+        if (MASK && threadIdx.x < TK) s_mk[threadIdx.x] = mk_ok ? nmk * LOG2E : 0.f;
         __syncthreads();
         if (t + 1 < nt) {
             a.load(kb, rs, (t + 1) * TK, S);
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __res
         const float lse2 = my_lse * LOG2E;
         // the forward's keep bits of my query for this tile's keys (one word per 128 keys)
         uint32_t kbits = ~0u;
-        if (p_drop > 0.f && qok) {
+        if (DROP && qok) {
             const int kwi = t >> 1;
             const uint32_t wv = kwi < MAXKW ? (kwi == 0 ? kwds[0] : kwi == 1 ? kwds[1] : kwi == 2 ? kwds[2] : kwds[3])
                                             : dmask[dmask_word(bh, S, kwi, g, myq)];
@@ -636,14 +641,14 @@ __global__ __launch_bounds__(64 * TWB, 3) void attn_bwd_dq_k(const bf16_t* __res
         for (int blk = 0; blk < 4; ++blk) {
             const int k0 = t * TK + 16 * blk + 4 * g;
             float4 mk4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (mrow) mk4 = *reinterpret_cast<const float4*>(s_mk + 16 * blk + 4 * g);
+            if (MASK) mk4 = *reinterpret_cast<const float4*>(s_mk + 16 * blk + 4 * g);
             const float mk[4] = {mk4.x, mk4.y, mk4.z, mk4.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const bool ok = qok && k0 + r < S;
                 const float pv = ok ? fast_exp2(sc[blk][r] * c2 + mk[r] - lse2) : 0.f;
                 float dpv = dp[blk][r];
-                if (p_drop > 0.f) dpv = ((kbits >> (4 * blk + r)) & 1u) ? dpv * inv_keep : 0.f;
+                if (DROP) dpv = ((kbits >> (4 * blk + r)) & 1u) ? dpv * inv_keep : 0.f;
                 ds[blk][r] = pv * (dpv - my_delta);
             }
         }
@@ -1567,7 +1572,10 @@ DDL_API int ddl_attn_fwd(const void* qkv, const float* mask, void* out, float* l
         DDL_RETURN_LAUNCH();
     }
     dim3 grid((S + TROWS_F - 1) / TROWS_F, B * H);
-    attn_fwd_k<<<grid, 64 * TWF, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed, dmask);
+#define FWD_TILED(M, D) attn_fwd_k<M, D><<<grid, 64 * TWF, 0, st>>>((const bf16_t*)qkv, mask, (bf16_t*)out, lse, B, S, H, scale, p_drop, seed, dmask)
+    if (mask) { if (p_drop > 0.f) FWD_TILED(true, true); else FWD_TILED(true, false); }
+    else { if (p_drop > 0.f) FWD_TILED(false, true); else FWD_TILED(false, false); }
+#undef FWD_TILED
     DDL_RETURN_LAUNCH();
 }
 
@@ -1597,10 +1605,16 @@ DDL_API int ddl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     const long rows = (long)B * S * H;
     attn_delta_k<<<(int)((rows * 8 + 255) / 256), 256, 0, st>>>((const bf16_t*)dout, (const bf16_t*)out, delta, B, S, H);
     dim3 grid((S + TROWS_B - 1) / TROWS_B, B * H);    // the dKV and dQ workgroups share the colsum rows
-    attn_bwd_dkv_k<<<grid, 64 * TWB, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B,
-                                         S, H, scale, p_drop, dmask, colsum);
-    attn_bwd_dq_k<<<grid, 64 * TWB, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, mask, (bf16_t*)dqkv, B, S,
-                                        H, scale, p_drop, dmask, colsum);
+    const bool drp = p_drop > 0.f;
+#define BWD_DKV(DR) attn_bwd_dkv_k<DR><<<grid, 64 * TWB, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, \
+        mask, (bf16_t*)dqkv, B, S, H, scale, p_drop, dmask, colsum)
+#define BWD_DQ(M, DR) attn_bwd_dq_k<M, DR><<<grid, 64 * TWB, 0, st>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, \
+        mask, (bf16_t*)dqkv, B, S, H, scale, p_drop, dmask, colsum)
+    if (drp) BWD_DKV(true); else BWD_DKV(false);
+    if (mask) { if (drp) BWD_DQ(true, true); else BWD_DQ(true, false); }
+    else { if (drp) BWD_DQ(false, true); else BWD_DQ(false, false); }
+#undef BWD_DKV
+#undef BWD_DQ
     const int rc = (int)hipGetLastError();
     return rc ? rc : (colsum ? 2 : 0);
 }
