@@ -108,7 +108,8 @@ def main() -> int:
         demangled = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip() or name
         short = re.sub(r"\(anonymous namespace\)::", "", demangled).split("(")[0]
         print(f"| `{short}` | {c['mfma']} | {c['valu']} | {c['salu']} | {c['lds']} | {c['vmem']} | "
-              f"{c['valu'] / c['mfma']:.2f} | {meta.get('vgpr_count', '?')} | {meta.get('vgpr_spill_count', '?')} |")
+              f"{c['valu'] / c['mfma'] if c['mfma'] else float('nan'):.2f} | {meta.get('vgpr_count', '?')} | "
+              f"{meta.get('vgpr_spill_count', '?')} |")
     return 0
 
 
