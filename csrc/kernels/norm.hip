@@ -628,7 +628,9 @@ __global__ __launch_bounds__(256) void ln_fwd8_k(const bf16_t* __restrict__ x, c
 // block's residual branch) is added to dx in the same pass, before the column sums, so dx is
 // the input's WHOLE gradient (no autograd add kernel, and the column sums are the producing
 // Linear's complete bias gradient)
-template <typename T, int VPL, bool ADD = false>
+// KNOWN (0: run-time checks): 4 | 2 (residual present) | 1 (dropout present) -- the BERT / ViT widths
+// are compiled per case, so the row loop carries no uniform branches for absent operands
+template <typename T, int VPL, bool ADD = false, int KNOWN = 0>
 __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                 const T* __restrict__ res, long res_rows, const T* __restrict__ gamma,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -641,6 +643,8 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
     // whose two dwords fell on one bank at a stride of VPL * 256 floats -- 2-way conflicts on every read)
     __shared__ __attribute__((aligned(16))) float s_acc[3][4][VPL * 256 + 4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool has_res = KNOWN ? (KNOWN & 2) != 0 : res != nullptr;
+    const bool has_drop = KNOWN ? (KNOWN & 1) != 0 : drop.thresh != 0;
     float dg[VPL][4], db[VPL][4], ds[VPL][4], g[VPL][4];
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
@@ -668,8 +672,8 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             const int col = 256 * k + 4 * lane;
             R.x[k] = ld_raw4(x + row * H + col);
             R.d[k] = ld_raw4(dy + row * H + col);
-            if (res) R.r[k] = ld_raw4(res + (row % res_rows) * H + col);
-            R.kb[k] = drop.thresh ? drop_bits4(drop, row * H + col) : 0xfu;
+            if (has_res) R.r[k] = ld_raw4(res + (row % res_rows) * H + col);
+            R.kb[k] = has_drop ? drop_bits4(drop, row * H + col) : 0xfu;
         }
     };
     // converted input (dropout(x) + residual) and dy of a loaded row
@@ -678,8 +682,8 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
         for (int k = 0; k < VPL; ++k) {
             cvt_raw4(R.x[k], xv[k]);
             cvt_raw4(R.d[k], d[k]);
-            if (drop.thresh) apply4(drop, R.kb[k], xv[k]);
-            if (res) {
+            if (has_drop) apply4(drop, R.kb[k], xv[k]);
+            if (has_res) {
                 float r[4];
                 cvt_raw4(R.r[k], r);
 #pragma unroll
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
             const long idx = row * H + 256 * k + 4 * lane;
 #pragma unroll
             for (int j = 0; j < 4; ++j) o[j] = rs * (gy[k][j] - m1 - xh[k][j] * m2);
-            if (drop.thresh) {
+            if (has_drop) {
                 store4((T*)drop.dres + idx, o);      // residual gradient: unmasked
                 apply4(drop, kb[k], o);              // x gradient: through the dropout mask
             }
@@ -1546,26 +1550,31 @@ static int ln_bwd_dispatch(const T* dy, const T* x, const T* res, long res_rows,
                            float* dxsum, T* dxsink, Drop drop, const T* dadd, hipStream_t st) {
     const int nblk = ddl_ln_bwd_nblk(rows);
     const int rpb = (int)((rows + nblk - 1) / nblk);
-#define LNB_ADD(V) ln_bwd_k<T, V, true><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop, dadd)
+#define LNB(V, A, KN) ln_bwd_k<T, V, A, KN><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop, dadd)
+    // H = 768 / 1024 (BERT, ViT): compiled per (residual, dropout) case; other widths check at run time
+    const int known = 4 | (res ? 2 : 0) | (drop.thresh ? 1 : 0);
+#define LNB_KNOWN(V, A) do { switch (known) { case 4: LNB(V, A, 4); break; case 5: LNB(V, A, 5); break; \
+                                             case 6: LNB(V, A, 6); break; default: LNB(V, A, 7); break; } } while (0)
     if (dadd) {
         switch (H / 256) {
-            case 1: LNB_ADD(1); break;
-            case 2: LNB_ADD(2); break;
-            case 3: LNB_ADD(3); break;
-            case 4: LNB_ADD(4); break;
+            case 1: LNB(1, true, 0); break;
+            case 2: LNB(2, true, 0); break;
+            case 3: LNB_KNOWN(3, true); break;
+            case 4: LNB_KNOWN(4, true); break;
             default: return -4;
         }
     } else switch (H / 256) {
         case 1: ln_bwd_k<T, 1><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         case 2: ln_bwd_k<T, 2><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
-        case 3: ln_bwd_k<T, 3><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
-        case 4: ln_bwd_k<T, 4><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
+        case 3: LNB_KNOWN(3, false); break;
+        case 4: LNB_KNOWN(4, false); break;
         case 5: ln_bwd_k<T, 5><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         case 6: ln_bwd_k<T, 6><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         case 8: ln_bwd_k<T, 8><<<nblk, 256, 0, st>>>(dy, x, res, res_rows, g, mean, rstd, dx, part, rows, H, rpb, dxsum != nullptr, drop); break;
         default: return -1;
     }
-#undef LNB_ADD
+#undef LNB_KNOWN
+#undef LNB
     if (merged_finalize(nblk, H)) {
         // one launch: 128-row slices + last-arriver combine (ws: the room behind the partial rows)
         const int S = fin_slices(nblk);
